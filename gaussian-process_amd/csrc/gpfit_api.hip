@@ -1,0 +1,574 @@
+// gpfit_api.hip — host side of libgpfit.so: the C-ABI declared in include/gpfit.h.
+//
+// One context = one HIP device + one stream + device-resident training data.
+// gpf_eval_batch replaces the reference's process-pool fan-out over particles
+// (find_len_scales.py:73-77,102-104,133-135): non-sentinel particles are packed
+// into chunks that fit HBM and every chunk is one batched factorise+score.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gpfit.h"
+#include "gpfit_kernels.hip"
+
+using gpf::NTHR;
+using gpf::T;
+
+namespace {
+
+enum ProfClass { PC_PANEL = 0, PC_DIAG = 1, PC_BUILD = 2, PC_LOSS = 3, PC_N = 4 };
+
+struct Pending {
+  hipEvent_t a, b;
+  int cls;
+  double work;  // algorithmic flops or bytes of this launch
+};
+
+}  // namespace
+
+struct gpf_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+
+  // training data
+  int64_t N = 0, Npad = 0;
+  int d = 0, nt = 0;
+  double* d_x = nullptr;
+  double* d_y = nullptr;
+  double* d_e = nullptr;
+  std::vector<double> h_y;
+
+  // objective grid / box
+  int K = 0;
+  double* d_sig = nullptr;
+  double* d_exp = nullptr;
+  double* d_lo = nullptr;
+  double* d_hi = nullptr;
+  std::vector<double> h_lo, h_hi;
+
+  // per-chunk workspace
+  int cap = 0;  // particles per chunk the workspace holds
+  double* d_L = nullptr;
+  double* d_U = nullptr;
+  double* d_yb = nullptr;
+  double* d_s2p = nullptr;
+  double* d_szp = nullptr;
+  double* d_ls = nullptr;
+  double* d_mu = nullptr;
+  double* d_sd = nullptr;
+  double* d_loss = nullptr;
+  int* d_info = nullptr;
+  int* d_hist = nullptr;
+
+  // profiling
+  bool prof = false;
+  double acc[PC_N][3] = {};  // ms, launches, work
+  double evals = 0;
+  std::vector<Pending> pend;
+  std::vector<hipEvent_t> pool;
+};
+
+#define GPF_HIP(ctx, expr)                                                                   \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess) {                                                                  \
+      (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(_e);                        \
+      return GPF_HIP_ERROR;                                                                  \
+    }                                                                                        \
+  } while (0)
+
+static int bad_arg(gpf_ctx* c, const char* m) {
+  c->err = m;
+  return GPF_BAD_ARG;
+}
+
+static hipEvent_t take_event(gpf_ctx* c) {
+  if (!c->pool.empty()) {
+    hipEvent_t e = c->pool.back();
+    c->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Launch helper: brackets the launch with events when profiling is on.
+template <typename F>
+static int launch(gpf_ctx* c, int cls, double work, F f) {
+  hipEvent_t a = nullptr, b = nullptr;
+  if (c->prof) {
+    a = take_event(c);
+    b = take_event(c);
+    if (a && b) hipEventRecord(a, c->stream);
+  }
+  f();
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    c->err = std::string("kernel launch: ") + hipGetErrorString(e);
+    return GPF_HIP_ERROR;
+  }
+  if (c->prof && a && b) {
+    hipEventRecord(b, c->stream);
+    c->pend.push_back({a, b, cls, work});
+  }
+  return GPF_OK;
+}
+
+static void harvest(gpf_ctx* c) {
+  for (auto& p : c->pend) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      c->acc[p.cls][0] += ms;
+      c->acc[p.cls][1] += 1;
+      c->acc[p.cls][2] += p.work;
+    }
+    c->pool.push_back(p.a);
+    c->pool.push_back(p.b);
+  }
+  c->pend.clear();
+}
+
+static void free_work(gpf_ctx* c) {
+  hipFree(c->d_L); hipFree(c->d_U); hipFree(c->d_yb); hipFree(c->d_s2p); hipFree(c->d_szp);
+  hipFree(c->d_ls); hipFree(c->d_mu); hipFree(c->d_sd); hipFree(c->d_loss); hipFree(c->d_info);
+  hipFree(c->d_hist);
+  c->d_L = c->d_U = c->d_yb = c->d_s2p = c->d_szp = c->d_ls = c->d_mu = c->d_sd = c->d_loss = nullptr;
+  c->d_info = nullptr;
+  c->d_hist = nullptr;
+  c->cap = 0;
+}
+
+static size_t bytes_per_particle(const gpf_ctx* c) {
+  const size_t np = (size_t)c->Npad;
+  return 2 * np * np * 8 + (2 * (size_t)c->nt * np + 3 * np) * 8 + (size_t)(c->K + 1) * 4 + 64 * 8;
+}
+
+// Chunk capacity from free HBM (GPF_MAX_CHUNK caps it, GPF_MEM_FRACTION scales the budget).
+static int ensure_work(gpf_ctx* c, int want) {
+  if (want <= c->cap) return GPF_OK;
+  free_work(c);
+  size_t fr = 0, tot = 0;
+  GPF_HIP(c, hipMemGetInfo(&fr, &tot));
+  double frac = 0.85;
+  if (const char* s = getenv("GPF_MEM_FRACTION")) frac = atof(s);
+  const size_t per = bytes_per_particle(c);
+  long long fit = (long long)((double)fr * frac / (double)per);
+  if (const char* s = getenv("GPF_MAX_CHUNK")) fit = std::min<long long>(fit, atoll(s));
+  if (fit < 1) {
+    c->err = "not enough device memory for one particle at N=" + std::to_string(c->N);
+    return GPF_HIP_ERROR;
+  }
+  const int cap = (int)std::min<long long>(want, fit);
+  const size_t np = (size_t)c->Npad;
+  GPF_HIP(c, hipMalloc(&c->d_L, (size_t)cap * np * np * 8));
+  GPF_HIP(c, hipMalloc(&c->d_U, (size_t)cap * np * np * 8));
+  GPF_HIP(c, hipMalloc(&c->d_yb, (size_t)cap * np * 8));
+  GPF_HIP(c, hipMalloc(&c->d_s2p, (size_t)cap * c->nt * np * 8));
+  GPF_HIP(c, hipMalloc(&c->d_szp, (size_t)cap * c->nt * np * 8));
+  GPF_HIP(c, hipMalloc(&c->d_ls, (size_t)cap * std::max(c->d, 1) * 8));
+  GPF_HIP(c, hipMalloc(&c->d_mu, (size_t)cap * np * 8));
+  GPF_HIP(c, hipMalloc(&c->d_sd, (size_t)cap * np * 8));
+  GPF_HIP(c, hipMalloc(&c->d_loss, (size_t)cap * 8));
+  GPF_HIP(c, hipMalloc(&c->d_info, (size_t)cap * 4));
+  GPF_HIP(c, hipMalloc(&c->d_hist, (size_t)cap * (c->K + 1) * 4));
+  c->cap = cap;
+  return GPF_OK;
+}
+
+// Factorise `pc` particles whose length scales are already in d_ls:
+// K build, then nt block columns of (diag, panel).
+static int run_factor(gpf_ctx* c, int pc) {
+  const int nt = c->nt, Np = (int)c->Npad, N = (int)c->N;
+  const double Tf = (double)T;
+  const int ntri = nt * (nt + 1) / 2;
+  int rc = launch(c, PC_BUILD, 8.0 * ntri * T * T * (double)pc, [&] {
+    hipLaunchKernelGGL(gpf::k_build_cov, dim3(ntri, pc), dim3(NTHR), 0, c->stream, N, Np, c->d, c->d_x, c->d_y,
+                       c->d_e, c->d_ls, c->d_L, c->d_yb);
+  });
+  if (rc) return rc;
+  for (int j = 0; j < nt; ++j) {
+    // diag: 64^3/3 (potrf) + 64^3/3 (inverse) + 64^2 (z)
+    rc = launch(c, PC_DIAG, (2.0 / 3.0 * Tf * Tf * Tf + Tf * Tf) * pc, [&] {
+      hipLaunchKernelGGL(gpf::k_diag, dim3(pc), dim3(NTHR), 0, c->stream, j, nt, Np, c->d_L, c->d_U, c->d_yb,
+                         c->d_s2p, c->d_szp, c->d_info);
+    });
+    if (rc) return rc;
+    if (nt > 1) {
+      // algorithmic flops of this block column, counted on the 2/3 N^3 (potrf + trtri) formulation:
+      // L tiles: the depth-j GEMM (2*64^3*j) + the triangular multiply (64^3) ; the look-ahead syrk is
+      // the diagonal's share of potrf (64^3). U tiles: depth-(j-k) GEMM on a triangular operand
+      // (2*64^3*(j-k) - 64^3) + the triangular multiply (64^3).
+      double fl = 0.0;
+      const double t3 = Tf * Tf * Tf;
+      for (int w = 0; w < nt - 1; ++w) {
+        if (w >= j) fl += 2.0 * t3 * j + t3 + t3;
+        else fl += 2.0 * t3 * (j - w);
+      }
+      rc = launch(c, PC_PANEL, fl * pc, [&] {
+        hipLaunchKernelGGL(gpf::k_panel, dim3(nt - 1, pc), dim3(NTHR), 0, c->stream, j, nt, Np, c->d_L, c->d_U,
+                           c->d_yb, c->d_s2p, c->d_szp);
+      });
+      if (rc) return rc;
+    }
+  }
+  return GPF_OK;
+}
+
+extern "C" {
+
+int gpf_version(void) { return GPF_ABI_VERSION; }
+int gpf_tile(void) { return T; }
+
+int gpf_open(int device, gpf_ctx** out) {
+  if (!out) return GPF_BAD_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return GPF_HIP_ERROR;
+  if (device < 0 || device >= n) return GPF_BAD_ARG;
+  if (hipSetDevice(device) != hipSuccess) return GPF_HIP_ERROR;
+  gpf_ctx* c = new gpf_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return GPF_HIP_ERROR;
+  }
+  *out = c;
+  return GPF_OK;
+}
+
+void gpf_close(gpf_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  harvest(c);
+  free_work(c);
+  hipFree(c->d_x); hipFree(c->d_y); hipFree(c->d_e);
+  hipFree(c->d_sig); hipFree(c->d_exp); hipFree(c->d_lo); hipFree(c->d_hi);
+  for (auto e : c->pool) hipEventDestroy(e);
+  hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* gpf_last_error(gpf_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int gpf_set_data(gpf_ctx* c, const double* x, const double* y, const double* e, int64_t N, int d) {
+  if (!c) return GPF_BAD_ARG;
+  if (N <= 0 || d <= 0 || !x || !y || !e) return bad_arg(c, "gpf_set_data: empty or null input");
+  if (d > gpf::DMAX) return bad_arg(c, "gpf_set_data: d exceeds DMAX (32)");
+  if (N > (int64_t)1 << 20) return bad_arg(c, "gpf_set_data: N too large");
+  hipSetDevice(c->device);
+  GPF_HIP(c, hipStreamSynchronize(c->stream));
+  free_work(c);
+  hipFree(c->d_x); hipFree(c->d_y); hipFree(c->d_e);
+  c->d_x = c->d_y = c->d_e = nullptr;
+  c->N = N;
+  c->d = d;
+  c->nt = (int)((N + T - 1) / T);
+  c->Npad = (int64_t)c->nt * T;
+  GPF_HIP(c, hipMalloc(&c->d_x, (size_t)N * d * 8));
+  GPF_HIP(c, hipMalloc(&c->d_y, (size_t)N * 8));
+  GPF_HIP(c, hipMalloc(&c->d_e, (size_t)N * 8));
+  GPF_HIP(c, hipMemcpy(c->d_x, x, (size_t)N * d * 8, hipMemcpyHostToDevice));
+  GPF_HIP(c, hipMemcpy(c->d_y, y, (size_t)N * 8, hipMemcpyHostToDevice));
+  GPF_HIP(c, hipMemcpy(c->d_e, e, (size_t)N * 8, hipMemcpyHostToDevice));
+  c->h_y.assign(y, y + N);
+  return GPF_OK;
+}
+
+int gpf_set_grid(gpf_ctx* c, const double* sig, const double* expct, int K, const double* lo, const double* hi) {
+  if (!c) return GPF_BAD_ARG;
+  if (c->d <= 0) return bad_arg(c, "gpf_set_grid: call gpf_set_data first");
+  if (K < 2 || K > gpf::KGRID_MAX || !sig || !expct || !lo || !hi) return bad_arg(c, "gpf_set_grid: bad grid");
+  hipSetDevice(c->device);
+  GPF_HIP(c, hipStreamSynchronize(c->stream));
+  if (K != c->K) {
+    free_work(c);  // histogram size depends on K
+    hipFree(c->d_sig); hipFree(c->d_exp);
+    c->d_sig = c->d_exp = nullptr;
+    GPF_HIP(c, hipMalloc(&c->d_sig, (size_t)K * 8));
+    GPF_HIP(c, hipMalloc(&c->d_exp, (size_t)K * 8));
+  }
+  if (!c->d_lo) {
+    GPF_HIP(c, hipMalloc(&c->d_lo, gpf::DMAX * 8));
+    GPF_HIP(c, hipMalloc(&c->d_hi, gpf::DMAX * 8));
+  }
+  c->K = K;
+  GPF_HIP(c, hipMemcpy(c->d_sig, sig, (size_t)K * 8, hipMemcpyHostToDevice));
+  GPF_HIP(c, hipMemcpy(c->d_exp, expct, (size_t)K * 8, hipMemcpyHostToDevice));
+  GPF_HIP(c, hipMemcpy(c->d_lo, lo, (size_t)c->d * 8, hipMemcpyHostToDevice));
+  GPF_HIP(c, hipMemcpy(c->d_hi, hi, (size_t)c->d * 8, hipMemcpyHostToDevice));
+  c->h_lo.assign(lo, lo + c->d);
+  c->h_hi.assign(hi, hi + c->d);
+  return GPF_OK;
+}
+
+int gpf_eval_batch(gpf_ctx* c, const double* ls, int P, double* loss, double* mu, double* sd, int* bad_idx) {
+  if (!c) return GPF_BAD_ARG;
+  if (bad_idx) *bad_idx = -1;
+  if (P < 0 || (P > 0 && (!ls || !loss))) return bad_arg(c, "gpf_eval_batch: bad arguments");
+  if (c->N <= 0 || c->K <= 0) return bad_arg(c, "gpf_eval_batch: call gpf_set_data and gpf_set_grid first");
+  hipSetDevice(c->device);
+  const int d = c->d;
+  const int64_t N = c->N, Np = c->Npad;
+  // sentinel particles (find_len_scales.py:156-157) never reach the GPU
+  std::vector<int> act;
+  act.reserve(P);
+  for (int p = 0; p < P; ++p) {
+    bool out = false;
+    for (int k = 0; k < d; ++k) {
+      const double v = ls[(size_t)p * d + k];
+      if (v <= c->h_lo[k] || v >= c->h_hi[k]) out = true;
+    }
+    if (out) {
+      loss[p] = 1e13;
+      if (mu) for (int64_t i = 0; i < N; ++i) mu[(size_t)p * N + i] = NAN;
+      if (sd) for (int64_t i = 0; i < N; ++i) sd[(size_t)p * N + i] = NAN;
+    } else {
+      act.push_back(p);
+    }
+  }
+  if (act.empty()) return GPF_OK;
+  int rc = ensure_work(c, (int)act.size());
+  if (rc) return rc;
+  const int cap = c->cap;
+  std::vector<double> hls((size_t)cap * d), hloss(cap);
+  std::vector<int> hinfo(cap);
+  std::vector<double> hmu, hsd;
+  if (mu) hmu.resize((size_t)cap * Np);
+  if (sd) hsd.resize((size_t)cap * Np);
+  for (size_t s = 0; s < act.size(); s += cap) {
+    const int pc = (int)std::min<size_t>(cap, act.size() - s);
+    for (int q = 0; q < pc; ++q)
+      for (int k = 0; k < d; ++k) hls[(size_t)q * d + k] = ls[(size_t)act[s + q] * d + k];
+    GPF_HIP(c, hipMemcpyAsync(c->d_ls, hls.data(), (size_t)pc * d * 8, hipMemcpyHostToDevice, c->stream));
+    GPF_HIP(c, hipMemsetAsync(c->d_info, 0, (size_t)pc * 4, c->stream));
+    GPF_HIP(c, hipMemsetAsync(c->d_hist, 0, (size_t)pc * (c->K + 1) * 4, c->stream));
+    rc = run_factor(c, pc);
+    if (rc) return rc;
+    rc = launch(c, PC_LOSS, 0.0, [&] {
+      hipLaunchKernelGGL(gpf::k_points, dim3((unsigned)((N + NTHR - 1) / NTHR), pc), dim3(NTHR), 0, c->stream,
+                         (int)N, (int)Np, c->nt, c->K, c->d_y, c->d_e, c->d_sig, c->d_s2p, c->d_szp, c->d_mu,
+                         c->d_sd, c->d_hist);
+      hipLaunchKernelGGL(gpf::k_score, dim3(pc), dim3(NTHR), 0, c->stream, (int)N, c->K, d, c->d_sig, c->d_exp,
+                         c->d_hist, c->d_ls, c->d_lo, c->d_hi, c->d_loss);
+    });
+    if (rc) return rc;
+    GPF_HIP(c, hipMemcpyAsync(hloss.data(), c->d_loss, (size_t)pc * 8, hipMemcpyDeviceToHost, c->stream));
+    GPF_HIP(c, hipMemcpyAsync(hinfo.data(), c->d_info, (size_t)pc * 4, hipMemcpyDeviceToHost, c->stream));
+    if (mu) GPF_HIP(c, hipMemcpyAsync(hmu.data(), c->d_mu, (size_t)pc * Np * 8, hipMemcpyDeviceToHost, c->stream));
+    if (sd) GPF_HIP(c, hipMemcpyAsync(hsd.data(), c->d_sd, (size_t)pc * Np * 8, hipMemcpyDeviceToHost, c->stream));
+    GPF_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->prof) harvest(c);
+    c->evals += pc;
+    for (int q = 0; q < pc; ++q) {
+      const int p = act[s + q];
+      if (hinfo[q] != 0) {
+        if (bad_idx) *bad_idx = p;
+        c->err = "Matrix is not positive definite";
+        return GPF_NOT_PD;
+      }
+      loss[p] = hloss[q];
+      if (mu) std::memcpy(mu + (size_t)p * N, hmu.data() + (size_t)q * Np, (size_t)N * 8);
+      if (sd) std::memcpy(sd + (size_t)p * N, hsd.data() + (size_t)q * Np, (size_t)N * 8);
+    }
+  }
+  return GPF_OK;
+}
+
+// Factorise one particle (slot 0 of the workspace) and produce alpha on device.
+static int factor_single(gpf_ctx* c, const double* ls, double** alpha_out) {
+  int rc = ensure_work(c, 1);
+  if (rc) return rc;
+  GPF_HIP(c, hipMemcpyAsync(c->d_ls, ls, (size_t)c->d * 8, hipMemcpyHostToDevice, c->stream));
+  GPF_HIP(c, hipMemsetAsync(c->d_info, 0, 4, c->stream));
+  rc = run_factor(c, 1);
+  if (rc) return rc;
+  // alpha into the mu slot of particle 0
+  rc = launch(c, PC_LOSS, 0.0, [&] {
+    hipLaunchKernelGGL(gpf::k_alpha, dim3((unsigned)((c->N + NTHR - 1) / NTHR)), dim3(NTHR), 0, c->stream,
+                       (int)c->N, (int)c->Npad, c->nt, c->d_szp, c->d_mu);
+  });
+  if (rc) return rc;
+  int info = 0;
+  GPF_HIP(c, hipMemcpyAsync(&info, c->d_info, 4, hipMemcpyDeviceToHost, c->stream));
+  GPF_HIP(c, hipStreamSynchronize(c->stream));
+  if (info != 0) {
+    c->err = "Matrix is not positive definite";
+    return GPF_NOT_PD;
+  }
+  *alpha_out = c->d_mu;
+  return GPF_OK;
+}
+
+int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int64_t batch, double* mu,
+                double* sd) {
+  if (!c) return GPF_BAD_ARG;
+  if (c->N <= 0) return bad_arg(c, "gpf_predict: call gpf_set_data first");
+  if (M < 0 || (M > 0 && (!xfit || !mu || !sd)) || !ls) return bad_arg(c, "gpf_predict: bad arguments");
+  if (M == 0) return GPF_OK;
+  hipSetDevice(c->device);
+  if (c->K <= 0) {  // predict does not need the objective grid; size the histogram minimally
+    c->K = 2;
+  }
+  double* alpha = nullptr;
+  int rc = factor_single(c, ls, &alpha);
+  if (rc) return rc;
+  // Query chunk: as large as memory allows (the reference's batch_size only bounds its
+  // own host memory, GP_func.py:28-30; results do not depend on it).
+  const int64_t Np = c->Npad;
+  int64_t chunk = std::max<int64_t>(batch, 1);
+  size_t fr = 0, tot = 0;
+  GPF_HIP(c, hipMemGetInfo(&fr, &tot));
+  const int64_t per_col = (Np + c->nt) * 8;
+  const int64_t maxcols = std::max<int64_t>(T, (int64_t)((double)fr * 0.5 / (double)per_col));
+  chunk = std::min<int64_t>(std::max<int64_t>(chunk, 16384), maxcols);
+  chunk = std::min<int64_t>(chunk, M);
+  const int64_t Cp = ((chunk + T - 1) / T) * T;
+  double *d_xf = nullptr, *d_ks = nullptr, *d_vsq = nullptr, *d_mu = nullptr, *d_sd = nullptr;
+  GPF_HIP(c, hipMalloc(&d_xf, (size_t)c->d * Cp * 8));
+  GPF_HIP(c, hipMalloc(&d_ks, (size_t)Np * Cp * 8));
+  GPF_HIP(c, hipMalloc(&d_vsq, (size_t)c->nt * Cp * 8));
+  GPF_HIP(c, hipMalloc(&d_mu, (size_t)Cp * 8));
+  GPF_HIP(c, hipMalloc(&d_sd, (size_t)Cp * 8));
+  std::vector<double> hx((size_t)c->d * Cp);
+  rc = GPF_OK;
+  for (int64_t s = 0; s < M && rc == GPF_OK; s += chunk) {
+    const int64_t m = std::min<int64_t>(chunk, M - s);
+    for (int k = 0; k < c->d; ++k)
+      std::memcpy(hx.data() + (size_t)k * Cp, xfit + (size_t)k * M + s, (size_t)m * 8);
+    if (hipMemcpyAsync(d_xf, hx.data(), (size_t)c->d * Cp * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+      rc = GPF_HIP_ERROR;
+      break;
+    }
+    const int nqt = (int)((m + T - 1) / T);
+    const int Cm = nqt * T;
+    rc = launch(c, PC_BUILD, 8.0 * Np * Cm, [&] {
+      hipLaunchKernelGGL(gpf::k_cross_cov, dim3(nqt, c->nt), dim3(NTHR), 0, c->stream, (int)c->N, (int)m, (int)Np,
+                         Cm, c->d, c->d_x, (int)c->N, d_xf, (int)Cp, c->d_ls, d_ks, (int64_t)Cp);
+    });
+    if (rc) break;
+    rc = launch(c, PC_PANEL, 0.0, [&] {
+      hipLaunchKernelGGL(gpf::k_predict_vsq, dim3(nqt, c->nt), dim3(NTHR), 0, c->stream, c->nt, (int)Np, c->d_U,
+                         d_ks, (int)Cp, d_vsq);
+      hipLaunchKernelGGL(gpf::k_predict_out, dim3((unsigned)((m + NTHR - 1) / NTHR)), dim3(NTHR), 0, c->stream,
+                         (int)c->N, c->nt, (int)m, d_ks, (int)Cp, alpha, d_vsq, d_mu, d_sd);
+    });
+    if (rc) break;
+    if (hipMemcpyAsync(mu + s, d_mu, (size_t)m * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipMemcpyAsync(sd + s, d_sd, (size_t)m * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+      rc = GPF_HIP_ERROR;
+      c->err = "gpf_predict: copy back failed";
+    }
+  }
+  hipStreamSynchronize(c->stream);
+  if (c->prof) harvest(c);
+  hipFree(d_xf); hipFree(d_ks); hipFree(d_vsq); hipFree(d_mu); hipFree(d_sd);
+  return rc;
+}
+
+int gpf_kernel(gpf_ctx* c, const double* x1, int64_t N1, const double* x2, int64_t N2, int d, const double* l,
+               double* out) {
+  if (!c) return GPF_BAD_ARG;
+  if (N1 < 0 || N2 < 0 || d <= 0 || d > gpf::DMAX || !l) return bad_arg(c, "gpf_kernel: bad arguments");
+  if (N1 == 0 || N2 == 0) return GPF_OK;
+  if (!x1 || !x2 || !out) return bad_arg(c, "gpf_kernel: null buffer");
+  hipSetDevice(c->device);
+  double *dx1 = nullptr, *dx2 = nullptr, *dl = nullptr, *dout = nullptr;
+  GPF_HIP(c, hipMalloc(&dx1, (size_t)N1 * d * 8));
+  GPF_HIP(c, hipMalloc(&dx2, (size_t)N2 * d * 8));
+  GPF_HIP(c, hipMalloc(&dl, (size_t)d * 8));
+  GPF_HIP(c, hipMalloc(&dout, (size_t)N1 * N2 * 8));
+  GPF_HIP(c, hipMemcpyAsync(dx1, x1, (size_t)N1 * d * 8, hipMemcpyHostToDevice, c->stream));
+  GPF_HIP(c, hipMemcpyAsync(dx2, x2, (size_t)N2 * d * 8, hipMemcpyHostToDevice, c->stream));
+  GPF_HIP(c, hipMemcpyAsync(dl, l, (size_t)d * 8, hipMemcpyHostToDevice, c->stream));
+  int rc = launch(c, PC_BUILD, 8.0 * N1 * N2, [&] {
+    hipLaunchKernelGGL(gpf::k_cross_cov, dim3((unsigned)((N2 + T - 1) / T), (unsigned)((N1 + T - 1) / T)),
+                       dim3(NTHR), 0, c->stream, (int)N1, (int)N2, (int)N1, (int)N2, d, dx1, (int)N1, dx2, (int)N2,
+                       dl, dout, (int64_t)N2);
+  });
+  if (rc == GPF_OK) {
+    if (hipMemcpyAsync(out, dout, (size_t)N1 * N2 * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+      rc = GPF_HIP_ERROR;
+      c->err = "gpf_kernel: copy back failed";
+    }
+  }
+  if (c->prof) harvest(c);
+  hipFree(dx1); hipFree(dx2); hipFree(dl); hipFree(dout);
+  return rc;
+}
+
+int gpf_log_marginal_likelihood(gpf_ctx* c, const double* ls, double* out) {
+  if (!c || !ls || !out) return GPF_BAD_ARG;
+  if (c->N <= 0) return bad_arg(c, "gpf_log_marginal_likelihood: call gpf_set_data first");
+  hipSetDevice(c->device);
+  if (c->K <= 0) c->K = 2;
+  double* alpha = nullptr;
+  int rc = factor_single(c, ls, &alpha);
+  if (rc) return rc;
+  const int64_t N = c->N, Np = c->Npad;
+  std::vector<double> a(N), dg(N);
+  GPF_HIP(c, hipMemcpy(a.data(), alpha, (size_t)N * 8, hipMemcpyDeviceToHost));
+  GPF_HIP(c, hipMemcpy2D(dg.data(), 8, c->d_L, (size_t)(Np + 1) * 8, 8, (size_t)N, hipMemcpyDeviceToHost));
+  double ya = 0.0, ld = 0.0;
+  for (int64_t i = 0; i < N; ++i) ya += c->h_y[i] * a[i];
+  for (int64_t i = 0; i < N; ++i) ld += std::log(dg[i]);
+  *out = -0.5 * ya - ld - 0.5 * (double)N * std::log(2.0 * M_PI);
+  return GPF_OK;
+}
+
+int gpf_set_profiling(gpf_ctx* c, int on) {
+  if (!c) return GPF_BAD_ARG;
+  c->prof = on != 0;
+  return GPF_OK;
+}
+
+int gpf_reset_profile(gpf_ctx* c) {
+  if (!c) return GPF_BAD_ARG;
+  hipStreamSynchronize(c->stream);
+  harvest(c);
+  std::memset(c->acc, 0, sizeof(c->acc));
+  c->evals = 0;
+  return GPF_OK;
+}
+
+int gpf_get_profile(gpf_ctx* c, double* out, int n) {
+  if (!c || !out) return 0;
+  hipStreamSynchronize(c->stream);
+  harvest(c);
+  double v[12] = {c->acc[PC_PANEL][0], c->acc[PC_PANEL][1], c->acc[PC_PANEL][2], c->acc[PC_DIAG][0],
+                  c->acc[PC_DIAG][1],  c->acc[PC_DIAG][2],  c->acc[PC_BUILD][0], c->acc[PC_BUILD][1],
+                  c->acc[PC_BUILD][2], c->acc[PC_LOSS][0],  c->acc[PC_LOSS][1],  c->evals};
+  const int m = std::min(n, 12);
+  for (int i = 0; i < m; ++i) out[i] = v[i];
+  return m;
+}
+
+int gpf_selftest_mfma(gpf_ctx* c, const double* a, const double* b, double* out) {
+  if (!c || !a || !b || !out) return GPF_BAD_ARG;
+  hipSetDevice(c->device);
+  double *da = nullptr, *db = nullptr, *dc = nullptr;
+  GPF_HIP(c, hipMalloc(&da, 64 * 8));
+  GPF_HIP(c, hipMalloc(&db, 64 * 8));
+  GPF_HIP(c, hipMalloc(&dc, 256 * 8));
+  GPF_HIP(c, hipMemcpy(da, a, 64 * 8, hipMemcpyHostToDevice));
+  GPF_HIP(c, hipMemcpy(db, b, 64 * 8, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(gpf::k_selftest_mfma, dim3(1), dim3(64), 0, c->stream, da, db, dc);
+  GPF_HIP(c, hipGetLastError());
+  GPF_HIP(c, hipStreamSynchronize(c->stream));
+  GPF_HIP(c, hipMemcpy(out, dc, 256 * 8, hipMemcpyDeviceToHost));
+  hipFree(da); hipFree(db); hipFree(dc);
+  return GPF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,6 @@
+"""gpfit — MI355X-native GP-fit hot path (HIP kernels behind a C-ABI).
+
+Internal package of the drop-in modules that sit next to it
+(GP_func.py, find_len_scales.py, ...). See DESIGN.md.
+"""
+from ._lib import Context, GPFitError, default_context, load_library  # noqa: F401

@@ -1,0 +1,214 @@
+"""ctypes binding of libgpfit.so (the C-ABI in include/gpfit.h).
+
+There is deliberately no CPU fallback: if the HIP library is missing or no
+device is visible, every entry point raises. The checker (oracle/) is a
+separate, test-only tree.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent.parent
+LIB_PATH = Path(os.environ.get("GPFIT_LIB", PKG_DIR / "libgpfit.so"))
+
+GPF_OK, GPF_NOT_PD, GPF_HIP_ERROR, GPF_BAD_ARG = 0, 1, 2, 3
+ABI_VERSION = 1
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int)
+_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); mirrors include/gpfit.h
+SIGNATURES = {
+    "gpf_version": (ctypes.c_int, []),
+    "gpf_tile": (ctypes.c_int, []),
+    "gpf_open": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
+    "gpf_close": (None, [_vp]),
+    "gpf_last_error": (ctypes.c_char_p, [_vp]),
+    "gpf_set_data": (ctypes.c_int, [_vp, _dp, _dp, _dp, ctypes.c_int64, ctypes.c_int]),
+    "gpf_set_grid": (ctypes.c_int, [_vp, _dp, _dp, ctypes.c_int, _dp, _dp]),
+    "gpf_eval_batch": (ctypes.c_int, [_vp, _dp, ctypes.c_int, _dp, _dp, _dp, _ip]),
+    "gpf_predict": (ctypes.c_int, [_vp, _dp, _dp, ctypes.c_int64, ctypes.c_int64, _dp, _dp]),
+    "gpf_kernel": (ctypes.c_int, [_vp, _dp, ctypes.c_int64, _dp, ctypes.c_int64, ctypes.c_int, _dp, _dp]),
+    "gpf_log_marginal_likelihood": (ctypes.c_int, [_vp, _dp, _dp]),
+    "gpf_set_profiling": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "gpf_get_profile": (ctypes.c_int, [_vp, _dp, ctypes.c_int]),
+    "gpf_reset_profile": (ctypes.c_int, [_vp]),
+    "gpf_selftest_mfma": (ctypes.c_int, [_vp, _dp, _dp, _dp]),
+}
+
+_LIB = None
+
+
+class GPFitError(RuntimeError):
+    """HIP runtime failure inside libgpfit."""
+
+
+def load_library():
+    """Load libgpfit.so (raises OSError with a build hint if it is missing)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not LIB_PATH.exists():
+        raise OSError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(str(LIB_PATH))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.gpf_version() != ABI_VERSION:
+        raise OSError(f"libgpfit ABI {lib.gpf_version()} != expected {ABI_VERSION}")
+    _LIB = lib
+    return lib
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _ptr(a):
+    return a.ctypes.data_as(_dp)
+
+
+def default_device():
+    """One process per GPU: torch.distributed launchers export LOCAL_RANK."""
+    return int(os.environ.get("GPFIT_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+
+
+class Context:
+    """One HIP device, one stream, device-resident training data (gpf_ctx)."""
+
+    def __init__(self, device=None):
+        self.lib = load_library()
+        self.device = default_device() if device is None else int(device)
+        h = _vp()
+        rc = self.lib.gpf_open(self.device, ctypes.byref(h))
+        if rc != GPF_OK or not h.value:
+            raise GPFitError(f"gpf_open(device={self.device}) failed (rc={rc}); is a GPU visible?")
+        self._h = h
+        self.N = 0
+        self.d = 0
+        self._data_key = None
+        self._grid_key = None
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self.lib.gpf_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- error mapping: same exception types as the reference's numpy path --
+    def _check(self, rc, what):
+        if rc == GPF_OK:
+            return
+        msg = self.lib.gpf_last_error(self._h).decode(errors="replace")
+        if rc == GPF_NOT_PD:
+            raise np.linalg.LinAlgError("Matrix is not positive definite")
+        if rc == GPF_BAD_ARG:
+            raise ValueError(f"{what}: {msg}")
+        raise GPFitError(f"{what}: {msg}")
+
+    def set_data(self, x_dN, y, e):
+        x = _f64(x_dN)
+        if x.ndim != 2:
+            raise ValueError("x must be (d, N)")
+        y, e = _f64(y), _f64(e)
+        d, n = x.shape
+        key = (d, n, hash(x.tobytes()), hash(y.tobytes()), hash(e.tobytes()))
+        if key == self._data_key:
+            return
+        self._check(self.lib.gpf_set_data(self._h, _ptr(x), _ptr(y), _ptr(e), n, d), "gpf_set_data")
+        self.N, self.d = n, d
+        self._data_key = key
+        self._grid_key = None
+
+    def set_grid(self, sigma_vals, expected, lo, hi):
+        s, ex = _f64(sigma_vals), _f64(expected)
+        lo, hi = _f64(lo).reshape(-1), _f64(hi).reshape(-1)
+        key = (hash(s.tobytes()), hash(ex.tobytes()), hash(lo.tobytes()), hash(hi.tobytes()))
+        if key == self._grid_key:
+            return
+        self._check(self.lib.gpf_set_grid(self._h, _ptr(s), _ptr(ex), s.shape[0], _ptr(lo), _ptr(hi)),
+                    "gpf_set_grid")
+        self._grid_key = key
+
+    def eval_batch(self, positions, want_mu_sd=False):
+        P = _f64(positions)
+        if P.ndim == 1:
+            P = P.reshape(1, -1)
+        n = P.shape[0]
+        loss = np.empty(n)
+        mu = np.empty((n, self.N)) if want_mu_sd else None
+        sd = np.empty((n, self.N)) if want_mu_sd else None
+        bad = ctypes.c_int(-1)
+        rc = self.lib.gpf_eval_batch(self._h, _ptr(P), n, _ptr(loss),
+                                     _ptr(mu) if want_mu_sd else None,
+                                     _ptr(sd) if want_mu_sd else None, ctypes.byref(bad))
+        self._check(rc, "gpf_eval_batch")
+        return (loss, mu, sd) if want_mu_sd else loss
+
+    def predict(self, lengths, x_fit, batch_size=10000):
+        ls = _f64(lengths).reshape(-1)
+        xf = _f64(x_fit)
+        m = xf.shape[1]
+        mu, sd = np.empty(m), np.empty(m)
+        self._check(self.lib.gpf_predict(self._h, _ptr(ls), _ptr(xf), m, int(batch_size), _ptr(mu), _ptr(sd)),
+                    "gpf_predict")
+        return mu, sd
+
+    def kernel(self, x1, x2, l):
+        a, b = _f64(x1), _f64(x2)
+        ls = _f64(l).reshape(-1)
+        out = np.empty((a.shape[1], b.shape[1]))
+        self._check(self.lib.gpf_kernel(self._h, _ptr(a), a.shape[1], _ptr(b), b.shape[1], a.shape[0],
+                                        _ptr(ls), _ptr(out)), "gpf_kernel")
+        return out
+
+    def log_marginal_likelihood(self, lengths):
+        ls = _f64(lengths).reshape(-1)
+        out = ctypes.c_double(0.0)
+        self._check(self.lib.gpf_log_marginal_likelihood(self._h, _ptr(ls), ctypes.byref(out)),
+                    "gpf_log_marginal_likelihood")
+        return out.value
+
+    # -- measurement hooks --
+    def set_profiling(self, on=True):
+        self._check(self.lib.gpf_set_profiling(self._h, int(bool(on))), "gpf_set_profiling")
+
+    def reset_profile(self):
+        self._check(self.lib.gpf_reset_profile(self._h), "gpf_reset_profile")
+
+    def profile(self):
+        buf = np.zeros(12)
+        self.lib.gpf_get_profile(self._h, _ptr(buf), 12)
+        keys = ["panel_ms", "panel_launches", "panel_flops", "diag_ms", "diag_launches", "diag_flops",
+                "build_ms", "build_launches", "build_bytes", "loss_ms", "loss_launches", "evals"]
+        return dict(zip(keys, buf.tolist()))
+
+    def selftest_mfma(self, a, b):
+        a, b = _f64(a), _f64(b)
+        c = np.empty((16, 16))
+        self._check(self.lib.gpf_selftest_mfma(self._h, _ptr(a), _ptr(b), _ptr(c)), "gpf_selftest_mfma")
+        return c
+
+
+_DEFAULT = {}
+
+
+def default_context():
+    """Process-wide context on this process's GPU (created on first use)."""
+    dev = default_device()
+    ctx = _DEFAULT.get(dev)
+    if ctx is None:
+        ctx = Context(dev)
+        _DEFAULT[dev] = ctx
+    return ctx

@@ -1,0 +1,121 @@
+/*
+ * gpfit.h — C-ABI of the MI355X GP-fit hot path (libgpfit.so).
+ *
+ * The reference (rferguson22/Gaussian-Process) is pure Python: its "plugin
+ * surface" for this path is a set of Python functions, not an FFI. Each entry
+ * point below replaces one of those seams; the Python drop-in modules in
+ * gaussian-process_amd/ bind them through ctypes.
+ *
+ *   gpf_eval_batch  replaces the particle fan-out
+ *                     list(executor.map(evaluate_loss_helper, args))
+ *                   at find_len_scales.py:77, :103, :134 — i.e. P calls of
+ *                   evaluate_loss (:181) -> wass_loss (:154-177) -> GP(x,y,e,x,l,
+ *                   batch_size=N) (GP_func.py:12-45, called at :159).
+ *   gpf_predict     replaces GP(x_known,y_known,e_known,x_fit,lengths,batch_size)
+ *                   (GP_func.py:12-45) for arbitrary query points (GP_fit.py:32).
+ *   gpf_kernel      replaces kernel_func(x1,x2,l) (GP_func.py:49-65).
+ *
+ * Conventions (mirroring the reference):
+ *   - all floating point is IEEE fp64;
+ *   - x arrays are dims-major (d, N), C-contiguous (the Python side calls
+ *     np.ascontiguousarray on the reference's F-order view, read_in.py:229);
+ *   - host buffers are caller-owned; data set by gpf_set_data stays resident
+ *     on the device until the next gpf_set_data / gpf_close;
+ *   - a context drives ONE device and is not thread-safe (one host thread per
+ *     context; one process per GPU, torch.distributed over RCCL above it).
+ *
+ * Return codes: GPF_OK, GPF_NOT_PD (Cholesky pivot <= 0 or NaN: the Python side
+ * raises numpy.linalg.LinAlgError("Matrix is not positive definite") exactly
+ * like numpy.linalg.cholesky at GP_func.py:22), GPF_HIP_ERROR, GPF_BAD_ARG.
+ */
+#ifndef GPFIT_H
+#define GPFIT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPF_OK 0
+#define GPF_NOT_PD 1
+#define GPF_HIP_ERROR 2
+#define GPF_BAD_ARG 3
+
+#define GPF_ABI_VERSION 1
+
+typedef struct gpf_ctx gpf_ctx;
+
+/* ABI version of the loaded library (== GPF_ABI_VERSION). */
+int gpf_version(void);
+
+/* Open a context on HIP device `device` (after HIP_VISIBLE_DEVICES). */
+int gpf_open(int device, gpf_ctx** out);
+void gpf_close(gpf_ctx* ctx);
+
+/* Message for the last non-OK return on this context ("" if none). */
+const char* gpf_last_error(gpf_ctx* ctx);
+
+/* Training data: x_dN is (d, N) dims-major; y, e are (N,).
+ * Reference: the (x_known, y_known, e_known) tuple members pickled per task at
+ * find_len_scales.py:76,102,133; here uploaded once per len_scale_opt call. */
+int gpf_set_data(gpf_ctx* ctx, const double* x_dN, const double* y,
+                 const double* e, int64_t N, int d);
+
+/* Objective grid and search box: sigma_vals/expected are the K-point grid of
+ * find_len_scales.py:66-67 (K = 1000 in the reference), lo/hi the (d,) bounds of
+ * :56-61. */
+int gpf_set_grid(gpf_ctx* ctx, const double* sigma_vals, const double* expected,
+                 int K, const double* lo, const double* hi);
+
+/* Batched objective. ls_Pd is (P, d) row-major particle positions. Writes
+ * loss_P[p] = evaluate_loss(ls[p], ...) (find_len_scales.py:181); sentinel
+ * particles (any ls <= lo or ls >= hi, :156-157) get 1e13 without touching the
+ * GPU. mu_PN / sd_PN (nullable, (P, N) row-major) receive the GP mean / sd at
+ * the training points (GP_func.py:36-40 with x_fit = x_known); rows of
+ * sentinel particles are filled with NaN. On GPF_NOT_PD *bad_idx is the first
+ * particle whose covariance is not positive definite. */
+int gpf_eval_batch(gpf_ctx* ctx, const double* ls_Pd, int P, double* loss_P,
+                   double* mu_PN, double* sd_PN, int* bad_idx);
+
+/* GP prediction at M query points xfit_dM (d, M), chunked by `batch` like
+ * GP_func.py:28-30 (the chunking does not change the result here). */
+int gpf_predict(gpf_ctx* ctx, const double* ls, const double* xfit_dM,
+                int64_t M, int64_t batch, double* mu_M, double* sd_M);
+
+/* kernel_func(x1, x2, l) (GP_func.py:49-65): out is (N1, N2) row-major. */
+int gpf_kernel(gpf_ctx* ctx, const double* x1_dN1, int64_t N1,
+               const double* x2_dN2, int64_t N2, int d, const double* l,
+               double* out);
+
+/* Diagnostic log marginal likelihood from the same factor (the reference has
+ * none): -1/2 y^T alpha - sum log L_ii - N/2 log(2 pi). */
+int gpf_log_marginal_likelihood(gpf_ctx* ctx, const double* ls, double* out);
+
+/* ---- measurement hooks (bench.py) ---- */
+
+/* Enable per-kernel-class HIP event timing on the context's stream. */
+int gpf_set_profiling(gpf_ctx* ctx, int on);
+
+/* Fill out[0..n) with accumulated counters since the last reset:
+ *  [0] panel kernel ms   [1] panel launches  [2] panel algorithmic flops
+ *  [3] diag kernel ms    [4] diag launches   [5] diag algorithmic flops
+ *  [6] K-build ms        [7] K-build launches[8] K-build algorithmic bytes
+ *  [9] loss kernel ms    [10] loss launches  [11] evals (non-sentinel)
+ * Returns the number of values written. */
+int gpf_get_profile(gpf_ctx* ctx, double* out, int n);
+int gpf_reset_profile(gpf_ctx* ctx);
+
+/* Tile edge used by the factorisation (padding granule). */
+int gpf_tile(void);
+
+/* Self-test of the f64 MFMA fragment layout: C = A(16x4) B(4x16) on device,
+ * compared on the host by the caller. a: 16x4 row-major, b: 4x16 row-major,
+ * c: 16x16 row-major. */
+int gpf_selftest_mfma(gpf_ctx* ctx, const double* a, const double* b, double* c);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GPFIT_H */

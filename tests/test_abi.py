@@ -1,0 +1,64 @@
+"""The C-ABI library loads and exports everything include/gpfit.h declares (no GPU needed)."""
+import ctypes
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def _declared():
+    hdr = (ROOT / "include" / "gpfit.h").read_text()
+    return sorted(set(re.findall(r"\b(gpf_[a-z_0-9]+)\s*\(", hdr)))
+
+
+def test_library_exports_every_declared_symbol():
+    import gpfit._lib as L
+    lib = L.load_library()
+    names = _declared()
+    assert len(names) >= 14
+    for n in names:
+        assert getattr(lib, n) is not None, n
+    # the ctypes signature table covers the header exactly
+    assert sorted(L.SIGNATURES) == names
+
+
+def test_abi_version_and_tile():
+    import gpfit._lib as L
+    lib = L.load_library()
+    assert lib.gpf_version() == L.ABI_VERSION == 1
+    assert lib.gpf_tile() == 64
+
+
+def test_library_is_gfx950_code_object():
+    import subprocess
+    so = ROOT / "gaussian-process_amd" / "libgpfit.so"
+    out = subprocess.run(["/opt/rocm/bin/roc-obj-ls", str(so)], capture_output=True, text=True)
+    if out.returncode != 0:
+        pytest.skip("roc-obj-ls unavailable")
+    assert "gfx950" in out.stdout
+
+
+def test_no_cpu_fallback_without_device():
+    """The product path must fail loudly when no GPU is visible."""
+    import gpfit._lib as L
+    lib = L.load_library()
+    n = ctypes.c_int(0)
+    h = ctypes.c_void_p()
+    if lib.gpf_open(0, ctypes.byref(h)) == 0:
+        lib.gpf_close(h)
+        pytest.skip("a GPU is visible")
+    with pytest.raises(L.GPFitError):
+        L.Context(0)
+    import GP_func
+    import numpy as np
+    with pytest.raises(L.GPFitError):
+        GP_func.GP(np.zeros((1, 3)), np.zeros(3), np.ones(3), np.zeros((1, 3)), np.ones(1))
+    del n
+
+
+def test_bad_arguments_are_value_errors_without_touching_device():
+    import gpfit._lib as L
+    lib = L.load_library()
+    assert lib.gpf_set_data(None, None, None, None, 0, 0) == L.GPF_BAD_ARG
+    assert lib.gpf_eval_batch(None, None, 0, None, None, None, None) == L.GPF_BAD_ARG

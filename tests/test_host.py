@@ -1,0 +1,79 @@
+"""Host logic of the product package, checked on CPU with the oracle injected
+as the objective (the oracle is only the checker; the code under test is
+gpfit.swarm, the drop-in PSO driver)."""
+import numpy as np
+import pytest
+
+from oracle import ref_cpu
+
+
+def _fx(x):
+    return np.asfortranarray(x)
+
+
+@pytest.mark.parametrize("k", [0, 1, 2])
+def test_swarm_driver_reproduces_reference_trajectory(f4, k, capsys):
+    from gpfit.swarm import particle_swarm
+    x, y, e = _fx(f4[f"c{k}_x"]), f4[f"c{k}_y"], f4[f"c{k}_e"]
+    best, info = particle_swarm(x, y, e, True, init_positions=f4[f"c{k}_init"], seed=int(f4[f"c{k}_seed"]),
+                                evaluator=lambda args: [ref_cpu.evaluate_loss_helper(a) for a in args])
+    out = capsys.readouterr().out
+    assert np.array_equal(best, f4[f"c{k}_best"])
+    assert out == str(f4[f"c{k}_log"])
+    assert info["evals"] == 40 * (501 + info["restarts"])
+
+
+def test_search_bounds_match_oracle(f2):
+    from gpfit.swarm import search_bounds
+    for i in range(int(f2["ncases"])):
+        x = _fx(f2[f"c{i}_x"])
+        lo, hi = search_bounds(x)
+        rlo, rhi = ref_cpu.search_bounds(x)
+        assert np.array_equal(lo, rlo) and np.array_equal(hi, rhi)
+        assert np.array_equal(lo, f2[f"c{i}_lo"]) and np.array_equal(hi, f2[f"c{i}_hi"])
+
+
+def test_sigma_grid_matches_reference(f2):
+    from gpfit.swarm import sigma_grid
+    s, ex = sigma_grid()
+    assert np.array_equal(s, f2["sigma_vals"]) and np.array_equal(ex, f2["expected"])
+
+
+def test_centred_lhs_is_latin_and_leaves_global_rng_alone():
+    from gpfit.swarm import centred_lhs
+    np.random.seed(3)
+    before = np.random.get_state()[1].copy()
+    lo, hi = np.array([0.1, 1.0, -2.0]), np.array([0.5, 3.0, 2.0])
+    P = centred_lhs(lo, hi, 40, seed=11)
+    assert np.array_equal(np.random.get_state()[1], before)
+    for k in range(3):
+        u = np.sort((P[:, k] - lo[k]) / (hi[k] - lo[k]))
+        np.testing.assert_allclose(u, (np.arange(40) + 0.5) / 40, atol=1e-12)
+    np.testing.assert_array_equal(P, centred_lhs(lo, hi, 40, seed=11))
+
+
+def test_kmeans_representatives_match_oracle():
+    from gpfit.swarm import kmeans_representatives
+    rng = np.random.default_rng(0)
+    x = rng.uniform(size=(2, 300))
+    y, e = rng.standard_normal(300), np.full(300, 0.1)
+    a = kmeans_representatives(x, y, e, 100)
+    b = ref_cpu.kmeans_subsample(x, y, e, 100)
+    for u, v in zip(a, b):
+        assert np.array_equal(u, v)
+
+
+def test_kmeans_path_taken_above_max_points(capsys):
+    from gpfit.swarm import particle_swarm
+    rng = np.random.default_rng(1)
+    x = rng.uniform(size=(2, 130))
+    y, e = np.sin(4 * x[0]) + 0.1 * rng.standard_normal(130), np.full(130, 0.1)
+    seen = []
+
+    def ev(args):
+        seen.append(args[0][1].shape[1])
+        return [ref_cpu.evaluate_loss_helper(a) for a in args]
+
+    particle_swarm(x, y, e, False, num_particles=4, max_iter=2, max_points=100, seed=0, evaluator=ev)
+    assert "Subsampling to 100" in capsys.readouterr().out
+    assert set(seen) == {100}
