@@ -1,0 +1,306 @@
+// gpf_common.hip — shared device machinery for the gfx950 GP-fit kernels:
+// FP64 MFMA tile GEMMs (streamed through LDS or fully LDS-resident), the
+// accumulator ownership map and small reduction helpers.
+//
+// All arithmetic is IEEE fp64 (an fp32 factor misses the 1e-6
+// tolerance by orders of magnitude). The file is compiled with -ffp-contract=off;
+// the only fused multiply-adds are the MFMA contractions and explicit fma().
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gpf {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2 __attribute__((ext_vector_type(2)));  // plain vector type: SROA-friendly (HIP's double2 is a class)
+
+constexpr int NTHR = 256;   // 4 waves of 64 lanes per workgroup (covariance / objective kernels)
+constexpr int DNTH = 512;   // 8 waves: the factorisation kernels (k_step, k_diag)
+constexpr int T = 128;      // factorisation block (block column width, padding granule)
+constexpr int H = 64;       // half block: the unblocked diagonal factor works on 64x64
+constexpr int LDH = H + 2;  // [row][k] stride of an LDS-resident 64x64 tile (ld/2 odd: conflict-free b64 reads)
+constexpr int DMAX = 32;    // max input dimensionality of the covariance builders
+constexpr int KGRID_MAX = 4096;
+
+__device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
+  // v_mfma_f64_16x16x4_f64: A 16x4 (lane l: row l&15, k l>>4), B 4x16 (k l>>4, col l&15),
+  // C/D 16x16: col = lane&15, row = (lane>>4) + 4*reg.
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// Per-tile-size geometry. A TM x TM output tile is owned by NW waves arranged
+// WR x WC; each wave holds a (TM/WR) x (TM/WC) sub-tile as MBR x MBC MFMA blocks
+// of 16x16 (accumulators: 4 doubles per lane per block).
+template <int TM> struct TileCfg;
+template <> struct TileCfg<128> {  // the factorisation / prediction GEMMs: 8 waves, 64x32 per wave
+  static constexpr int KC = 16, NW = 8, WR = 2, WC = 4;
+};
+template <> struct TileCfg<64> {   // LDS-resident 64x64 products inside the diagonal factor: 8 waves, 32x16 each
+  static constexpr int KC = 32, NW = 8, WR = 2, WC = 4;
+};
+
+template <int TM> struct Geo {
+  static constexpr int KC = TileCfg<TM>::KC;
+  static constexpr int NW = TileCfg<TM>::NW;
+  static constexpr int WR = TileCfg<TM>::WR;
+  static constexpr int WC = TileCfg<TM>::WC;
+  static constexpr int NTH = 64 * NW;
+  static constexpr int MBR = TM / WR / 16;
+  static constexpr int MBC = TM / WC / 16;
+  static constexpr int RK = KC + 2;   // [row][k] staging stride (ld/2 odd)
+  static constexpr int KN = TM + 16;  // [k][col] staging stride (2*ld == 32 mod 64 dwords)
+  static constexpr int SA = TM * RK;
+  static constexpr int SB = (TM * RK > KC * KN) ? TM * RK : KC * KN;
+  static constexpr int STAGE = 2 * (SA + SB);  // double-buffered A + B chunks (doubles)
+  static constexpr int NLD = TM * KC / 2 / NTH;  // 16-byte loads per thread per operand per chunk
+  static_assert(NLD * 2 * NTH == TM * KC, "staging map");
+  static_assert(WR * WC == NW, "wave grid");
+};
+
+template <int TM> struct Quad {
+  int lane, rb, cb;
+  __device__ Quad() {
+    const int tid = threadIdx.x;
+    lane = tid & 63;
+    const int w = tid >> 6;
+    rb = (w / Geo<TM>::WC) * (TM / Geo<TM>::WR);
+    cb = (w % Geo<TM>::WC) * (TM / Geo<TM>::WC);
+  }
+  __device__ __forceinline__ int wrow() const { return (threadIdx.x >> 6) / Geo<TM>::WC; }
+  __device__ __forceinline__ int row(int mi, int r) const { return rb + mi * 16 + (lane >> 4) + 4 * r; }
+  __device__ __forceinline__ int col(int ni) const { return cb + ni * 16 + (lane & 15); }
+};
+
+// Hide a pointer's value from the optimiser so addresses derived from it are
+// recomputed per use instead of being kept live (and spilled) across GEMMs.
+template <typename P>
+__device__ __forceinline__ P* launder(P* p) {
+  asm volatile("" : "+v"(p));
+  return p;
+}
+
+template <int TM> struct Acc {
+  static constexpr int MBR = Geo<TM>::MBR, MBC = Geo<TM>::MBC;
+  d4 v[MBR][MBC];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < MBR; ++i)
+#pragma unroll
+      for (int j = 0; j < MBC; ++j) v[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+  }
+  template <typename F>
+  __device__ __forceinline__ void foreach(const Quad<TM>& q, F f) const {
+#pragma unroll
+    for (int mi = 0; mi < MBR; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < MBC; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) f(q.row(mi, r), q.col(ni), v[mi][ni][r]);
+  }
+  // Load / store the owned elements of a row-major global tile.
+  __device__ __forceinline__ void load(const Quad<TM>& q, const double* base, size_t ld) {
+    const double* p0 = launder(base + (size_t)(q.rb + (q.lane >> 4)) * ld + q.cb + (q.lane & 15));
+#pragma unroll
+    for (int mi = 0; mi < MBR; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < MBC; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[mi][ni][r] = p0[(size_t)(mi * 16 + 4 * r) * ld + ni * 16];
+  }
+  __device__ __forceinline__ void store(const Quad<TM>& q, double* base, size_t ld) const {
+    double* p0 = launder(base + (size_t)(q.rb + (q.lane >> 4)) * ld + q.cb + (q.lane & 15));
+#pragma unroll
+    for (int mi = 0; mi < MBR; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < MBC; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) p0[(size_t)(mi * 16 + 4 * r) * ld + ni * 16] = v[mi][ni][r];
+  }
+  // Visit each owned element together with its slot in a row-major global tile.
+  // The per-lane base is formed once; the per-element offsets are wave-uniform
+  // (scalar registers), so no per-element 64-bit address stays live.
+  template <typename F>
+  __device__ __forceinline__ void visit(const Quad<TM>& q, double* base, size_t ld, F f) const {
+    double* p0 = launder(base + (size_t)(q.rb + (q.lane >> 4)) * ld + q.cb + (q.lane & 15));
+#pragma unroll
+    for (int mi = 0; mi < MBR; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < MBC; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) f(p0[(size_t)(mi * 16 + 4 * r) * ld + ni * 16], v[mi][ni][r]);
+  }
+};
+
+// ----------------------------------------------------------------------------
+// Streaming tile GEMM: acc(TM x TM) += A(TM x K) * B(K x TM)
+//   A (r,k) at Ap[r*lda + k]                      (row panel, k contiguous)
+//   B (k,c) at Bp[c*ldb + k]   (!NN: B^T given as a row panel)
+//           at Bp[k*ldb + c]   ( NN: B given as a row panel)
+// K is a multiple of KC. Chunks are double-buffered through LDS: the global loads
+// of chunk t+1 are in flight while chunk t feeds the MFMAs; one barrier per chunk.
+// NEG stages A negated, i.e. acc -= A B (sign flips are exact: acc = C - A B
+// rounds exactly like a subtraction). Ends with a barrier, so the staging area
+// may be reused right after.
+// ----------------------------------------------------------------------------
+template <int TM, bool NN>
+__device__ __forceinline__ void stage_load(d2 (&ra)[Geo<TM>::NLD], d2 (&rb)[Geo<TM>::NLD],
+                                           const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
+                                           int ldb, int k0, int tid) {
+  constexpr int KC = Geo<TM>::KC;
+#pragma unroll
+  for (int u = 0; u < Geo<TM>::NLD; ++u) {
+    const int q = tid + Geo<TM>::NTH * u;
+    const int row = q / (KC / 2), c2 = q % (KC / 2);
+    ra[u] = *reinterpret_cast<const d2*>(Ap + (size_t)row * lda + k0 + 2 * c2);
+    if (!NN) {
+      rb[u] = *reinterpret_cast<const d2*>(Bp + (size_t)row * ldb + k0 + 2 * c2);
+    } else {
+      const int kr = q / (TM / 2), cc = q % (TM / 2);
+      rb[u] = *reinterpret_cast<const d2*>(Bp + (size_t)(k0 + kr) * ldb + 2 * cc);
+    }
+  }
+}
+
+template <int TM, bool NN, bool NEG>
+__device__ __forceinline__ void stage_store(double* sA, double* sB, const d2 (&ra)[Geo<TM>::NLD],
+                                            const d2 (&rb)[Geo<TM>::NLD], int tid) {
+  constexpr int KC = Geo<TM>::KC, RK = Geo<TM>::RK, KN = Geo<TM>::KN;
+#pragma unroll
+  for (int u = 0; u < Geo<TM>::NLD; ++u) {
+    const int q = tid + Geo<TM>::NTH * u;
+    const int row = q / (KC / 2), c2 = q % (KC / 2);
+    *reinterpret_cast<d2*>(sA + row * RK + 2 * c2) = NEG ? -ra[u] : ra[u];
+    if (!NN) {
+      *reinterpret_cast<d2*>(sB + row * RK + 2 * c2) = rb[u];
+    } else {
+      const int kr = q / (TM / 2), cc = q % (TM / 2);
+      *reinterpret_cast<d2*>(sB + kr * KN + 2 * cc) = rb[u];
+    }
+  }
+}
+
+template <int TM, bool NN>
+__device__ __forceinline__ void stage_mma(Acc<TM>& acc, const double* sA, const double* sB, const Quad<TM>& qd) {
+  constexpr int KC = Geo<TM>::KC, RK = Geo<TM>::RK, KN = Geo<TM>::KN;
+  constexpr int MBR = Geo<TM>::MBR, MBC = Geo<TM>::MBC;
+  const int lr = qd.lane & 15, lk = qd.lane >> 4;
+#pragma unroll
+  for (int ks = 0; ks < KC; ks += 4) {
+    double a[MBR], b[MBC];
+#pragma unroll
+    for (int mi = 0; mi < MBR; ++mi) a[mi] = sA[(qd.rb + mi * 16 + lr) * RK + ks + lk];
+#pragma unroll
+    for (int ni = 0; ni < MBC; ++ni) {
+      if (!NN)
+        b[ni] = sB[(qd.cb + ni * 16 + lr) * RK + ks + lk];
+      else
+        b[ni] = sB[(ks + lk) * KN + qd.cb + ni * 16 + lr];
+    }
+#pragma unroll
+    for (int mi = 0; mi < MBR; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < MBC; ++ni) acc.v[mi][ni] = mfma(a[mi], b[ni], acc.v[mi][ni]);
+  }
+}
+
+template <int TM, bool NN, bool NEG = false>
+__device__ void gemm_stream(Acc<TM>& acc, const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
+                            int ldb, int K, double* smem, const Quad<TM>& qd) {
+  constexpr int KC = Geo<TM>::KC, SA = Geo<TM>::SA, SB = Geo<TM>::SB, NLD = Geo<TM>::NLD;
+  const int tid = threadIdx.x;
+  const int nch = K / KC;
+  if (nch <= 0) return;
+  Ap = launder(Ap);
+  Bp = launder(Bp);
+  d2 ra[NLD], rb[NLD];
+  stage_load<TM, NN>(ra, rb, Ap, lda, Bp, ldb, 0, tid);
+  stage_store<TM, NN, NEG>(smem, smem + SA, ra, rb, tid);
+  __syncthreads();
+#pragma unroll 1
+  for (int t = 0; t < nch; ++t) {
+    const bool more = (t + 1) < nch;
+    if (more) stage_load<TM, NN>(ra, rb, Ap, lda, Bp, ldb, (t + 1) * KC, tid);
+    const double* cur = smem + (t & 1) * (SA + SB);
+    stage_mma<TM, NN>(acc, cur, cur + SA, qd);
+    if (more) {
+      double* nxt = smem + ((t + 1) & 1) * (SA + SB);
+      stage_store<TM, NN, NEG>(nxt, nxt + SA, ra, rb, tid);
+    }
+    __syncthreads();
+  }
+}
+
+// 64x64x64 GEMM with both operands resident in LDS (8 waves, 32x16 each):
+//   A (r,k) at sA[r*la + k];  B (k,c) at sB[c*lb + k] (!NN) or sB[k*lb + c] (NN).
+template <bool NN>
+__device__ __forceinline__ void gemm_lds64(Acc<64>& acc, const double* sA, int la, const double* sB, int lb,
+                                           const Quad<64>& qd) {
+  constexpr int MBR = Geo<64>::MBR, MBC = Geo<64>::MBC;
+  const int lr = qd.lane & 15, lk = qd.lane >> 4;
+#pragma unroll 4
+  for (int ks = 0; ks < H; ks += 4) {
+    double a[MBR], b[MBC];
+#pragma unroll
+    for (int mi = 0; mi < MBR; ++mi) a[mi] = sA[(qd.rb + mi * 16 + lr) * la + ks + lk];
+#pragma unroll
+    for (int ni = 0; ni < MBC; ++ni) {
+      if (!NN)
+        b[ni] = sB[(qd.cb + ni * 16 + lr) * lb + ks + lk];
+      else
+        b[ni] = sB[(ks + lk) * lb + qd.cb + ni * 16 + lr];
+    }
+#pragma unroll
+    for (int mi = 0; mi < MBR; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < MBC; ++ni) acc.v[mi][ni] = mfma(a[mi], b[ni], acc.v[mi][ni]);
+  }
+}
+
+// Coalesced 64x64 global tile -> LDS [row][col] with stride ld, 16 B per lane (DNTH threads).
+__device__ __forceinline__ void tile64_to_lds(double* s, int ld, const double* __restrict__ g, size_t gld) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < 2048 / DNTH; ++u) {
+    const int q = tid + DNTH * u;
+    const int row = q >> 5, c2 = q & 31;
+    const d2 v = *reinterpret_cast<const d2*>(g + (size_t)row * gld + 2 * c2);
+    s[row * ld + 2 * c2] = v.x;
+    s[row * ld + 2 * c2 + 1] = v.y;
+  }
+}
+
+// LDS 64x64 -> global, optionally zeroing the strict upper triangle.
+__device__ __forceinline__ void lds_to_tile64(double* __restrict__ g, size_t gld, const double* s, int ld,
+                                              bool lower_only) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < 2048 / DNTH; ++u) {
+    const int q = tid + DNTH * u;
+    const int row = q >> 5, c2 = q & 31;
+    d2 v;
+    v.x = (lower_only && 2 * c2 > row) ? 0.0 : s[row * ld + 2 * c2];
+    v.y = (lower_only && 2 * c2 + 1 > row) ? 0.0 : s[row * ld + 2 * c2 + 1];
+    *reinterpret_cast<d2*>(g + (size_t)row * gld + 2 * c2) = v;
+  }
+}
+
+__device__ __forceinline__ void zero_tile64(double* __restrict__ g, size_t gld) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < 2048 / DNTH; ++u) {
+    const int q = tid + DNTH * u;
+    const int row = q >> 5, c2 = q & 31;
+    *reinterpret_cast<d2*>(g + (size_t)row * gld + 2 * c2) = d2{0.0, 0.0};
+  }
+}
+
+// Sum over the 4 lane groups {l, l^16, l^32, l^48} of a wave; the result is
+// bitwise identical in all four lanes ((g0+g1)+(g2+g3), addition commutes).
+__device__ __forceinline__ double sum_lane_groups(double v) {
+  v = v + __shfl_xor(v, 16);
+  v = v + __shfl_xor(v, 32);
+  return v;
+}
+
+}  // namespace gpf

@@ -1,0 +1,132 @@
+// gpf_covariance.hip — squared-exponential covariance builders (HBM-bound writes).
+//
+// kernel_func (GP_func.py:49-65): a = x / l per dimension (:56-57), squared norms
+// summed over dimensions in order (:59-60), (|a_i|^2 + |a_j|^2) - 2 a_i.a_j (:62),
+// clamp at 0 (:63), exp(-0.5 r2) (:65); K adds diag(e^2) (:21). One 64x64 output
+// tile per workgroup: the scaled coordinates of its 64 rows and 64 columns are
+// staged in LDS once, then every lane writes 16 outputs, consecutive lanes on
+// consecutive columns (512 contiguous bytes per row per wave).
+#pragma once
+#include "gpf_common.hip"
+
+namespace gpf {
+
+constexpr int BT = 64;  // covariance build tile
+
+// ----------------------------------------------------------------------------
+// K build: lower tiles of K = SE(x,x;l) + diag(e^2) for every particle, padded
+// to Npad with an identity block (so padded rows factor to L = I, z = 0).
+// Op order mirrors kernel_func (GP_func.py:56-65): a = x / l, |a|^2 summed over
+// dims in order, (|a_i|^2 + |a_j|^2) - 2 a_i.a_j, clamp >= 0, exp(-0.5 r2).
+// Also seeds the per-particle RHS workspace with y (padded with zeros).
+// grid: (nt*(nt+1)/2, P)
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(NTHR) void k_build_cov(int N, int Npad, int d, const double* __restrict__ x,
+                                                    const double* __restrict__ y, const double* __restrict__ e,
+                                                    const double* __restrict__ ls, double* __restrict__ Lb,
+                                                    double* __restrict__ yb) {
+  __shared__ double ai[DMAX][BT];
+  __shared__ double aj[DMAX][BT];
+  __shared__ double ni[BT], nj[BT];
+  const int tid = threadIdx.x;
+  const int p = blockIdx.y;
+  // lower-triangular tile index -> (bi, bj), bi >= bj
+  const int idx = blockIdx.x;
+  int bi = (int)((sqrt(8.0 * idx + 1.0) - 1.0) * 0.5);
+  while ((bi + 1) * (bi + 2) / 2 <= idx) ++bi;
+  while (bi * (bi + 1) / 2 > idx) --bi;
+  const int bj = idx - bi * (bi + 1) / 2;
+  const double* lp = ls + (size_t)p * d;
+
+  if (tid < 128) {
+    const int t = tid & 63;
+    const int g = (tid < 64 ? bi : bj) * BT + t;
+    double(*a)[BT] = (tid < 64) ? ai : aj;
+    double nrm = 0.0;
+    if (g < N) {
+      for (int k = 0; k < d; ++k) {
+        const double v = x[(size_t)k * N + g] / lp[k];
+        a[k][t] = v;
+        nrm = nrm + v * v;
+      }
+    }
+    if (tid < 64) ni[t] = nrm; else nj[t] = nrm;
+  }
+  __syncthreads();
+
+  double* Lp = Lb + (size_t)p * Npad * Npad;
+#pragma unroll 4
+  for (int u = 0; u < (BT * BT) / NTHR; ++u) {
+    const int q = tid + NTHR * u;
+    const int r = q >> 6, c = q & 63;
+    const int gi = bi * BT + r, gj = bj * BT + c;
+    double v;
+    if (gi < N && gj < N) {
+      double dot = ai[0][r] * aj[0][c];
+      for (int k = 1; k < d; ++k) dot = fma(ai[k][r], aj[k][c], dot);
+      double r2 = (ni[r] + nj[c]) - 2.0 * dot;
+      r2 = r2 > 0.0 ? r2 : 0.0;  // np.maximum(sq_dist, 0)
+      v = exp(-0.5 * r2);
+      if (gi == gj) v = v + e[gi] * e[gi];
+    } else {
+      v = (gi == gj) ? 1.0 : 0.0;
+    }
+    Lp[(size_t)gi * Npad + gj] = v;
+  }
+  if (bi == bj && tid < BT) {
+    const int g = bi * BT + tid;
+    yb[(size_t)p * Npad + g] = (g < N) ? y[g] : 0.0;
+  }
+}
+
+// Rectangular cross-covariance kernel_func(x1, x2, l) (no noise) into
+// out[i*ldo + j] for i < R, j < C; entries with i >= N1 or j >= N2 are 0.
+// grid: (ceil(C/64), ceil(R/64))
+__global__ __launch_bounds__(NTHR) void k_cross_cov(int N1, int N2, int R, int C, int d,
+                                                    const double* __restrict__ x1, int ld1,
+                                                    const double* __restrict__ x2, int ld2,
+                                                    const double* __restrict__ l, double* __restrict__ out,
+                                                    int64_t ldo) {
+  __shared__ double ai[DMAX][BT];
+  __shared__ double aj[DMAX][BT];
+  __shared__ double ni[BT], nj[BT];
+  const int tid = threadIdx.x;
+  const int bi = blockIdx.y, bj = blockIdx.x;
+  if (tid < 128) {
+    const int t = tid & 63;
+    const bool first = tid < 64;
+    const int g = (first ? bi : bj) * BT + t;
+    const int lim = first ? N1 : N2;
+    const double* xs = first ? x1 : x2;
+    const int ldx = first ? ld1 : ld2;
+    double(*a)[BT] = first ? ai : aj;
+    double nrm = 0.0;
+    if (g < lim) {
+      for (int k = 0; k < d; ++k) {
+        const double v = xs[(size_t)k * ldx + g] / l[k];
+        a[k][t] = v;
+        nrm = nrm + v * v;
+      }
+    }
+    if (first) ni[t] = nrm; else nj[t] = nrm;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int u = 0; u < (BT * BT) / NTHR; ++u) {
+    const int q = tid + NTHR * u;
+    const int r = q >> 6, c = q & 63;
+    const int gi = bi * BT + r, gj = bj * BT + c;
+    if (gi >= R || gj >= C) continue;
+    double v = 0.0;
+    if (gi < N1 && gj < N2) {
+      double dot = ai[0][r] * aj[0][c];
+      for (int k = 1; k < d; ++k) dot = fma(ai[k][r], aj[k][c], dot);
+      double r2 = (ni[r] + nj[c]) - 2.0 * dot;
+      r2 = r2 > 0.0 ? r2 : 0.0;
+      v = exp(-0.5 * r2);
+    }
+    out[(size_t)gi * ldo + gj] = v;
+  }
+}
+
+}  // namespace gpf

@@ -1,0 +1,412 @@
+// gpf_factor.hip — batched left-looking Cholesky + triangular inverse on gfx950.
+//
+// Reference op replaced (per particle, GP_func.py:21-24,38 via find_len_scales.py:159):
+//   L = cholesky(K)            LAPACK dpotrf
+//   solve(L.T, solve(L, y))    2x LAPACK dgesv on triangular factors
+//   solve(L, K_s)              LAPACK dgesv with N right-hand sides
+// Here: L = chol(K), U = L^-1 and z = U y, plus the column partials of
+// diag(K^-1) = colsum(U o U) and alpha = U^T z, in 2/3 N^3 flops (potrf + trtri)
+// instead of the reference's ~4.3 N^3.
+//
+// Blocking: 128-wide block columns J (T = 128). Launch J (k_step) advances every
+// particle of the chunk by one block column:
+//   L tiles (I > J):  L_IJ = (A_IJ - L_I,<J L_J,<J^T) U_JJ^T       streamed MFMA GEMM, depth 128 J
+//                     A_II -= L_IJ L_IJ^T ; y_I -= L_IJ z_J         look-ahead (keeps A_II and y current)
+//   U tiles (K < J):  U_JK = -U_JJ (L_J,[K,J) U_[K,J),K)           streamed MFMA GEMM, depth 128 (J-K)
+// and k_diag factors the next diagonal block (L_JJ, U_JJ = L_JJ^-1, z_J) in between.
+// A left-looking step streams each factored panel once per 128 output columns,
+// so the GEMMs run at ~32 flop per HBM byte (64-wide columns: ~16, HBM-bound).
+
+#pragma once
+#include "gpf_common.hip"
+
+namespace gpf {
+
+// The diagonal-block routines below run on all DNTH (= 512) threads of the
+// factorisation workgroups (k_diag and, fused, k_step).
+
+// ----------------------------------------------------------------------------
+// Unblocked 64x64 Cholesky with the inverse riding along ([A | I] -> [L | L^-1]).
+// Thread (r = tid>>3, g = tid&7) keeps row r, columns s = g + 8m, of both the
+// trailing A and X in registers (8 + 8 doubles). Whoever updates element
+// (r, c+1) also publishes it to `nxt[r]`, so column c+1 (and its pivot
+// nxt[c+1]) is read from LDS, never picked out of the register row by a runtime
+// index (which would go to scratch). Finished columns of L are written to sA as
+// they are produced. The update is branch-free (masked multipliers), one
+// reciprocal per column, two barriers per column; the column loop stays rolled
+// (small code, I-cache resident).
+//   in : sA[r*la + s] lower triangle of the tile
+//   out: sA = L (zeros above the diagonal), sX = L^-1; returns true if a pivot
+//        was not > 0 (numpy: LinAlgError, GP_func.py:22)
+// xbuf: >= 192 doubles of LDS scratch.
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx, double* xbuf) {
+  constexpr int G = DNTH / 64, NM = 64 / G;  // 8 column groups, 8 columns per lane
+  const int tid = threadIdx.x;
+  const int r = tid / G, g = tid % G;
+  double* colbuf = xbuf;       // column c of L
+  double* rowbuf = xbuf + 64;  // row c of L^-1
+  double* nxt = xbuf + 128;    // column c+1 of the reduced A (its pivot included)
+  double a[NM], x[NM];
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    const int s = g + G * m;
+    a[m] = (s <= r) ? sA[r * la + s] : 0.0;
+    x[m] = (s == r) ? 1.0 : 0.0;
+  }
+  if (g == 0) {
+    nxt[r] = a[0];  // column 0
+    colbuf[r] = 0.0;
+    rowbuf[r] = 0.0;
+  }
+  bool bad = false;
+#pragma unroll 1
+  for (int c = 0; c < 64; ++c) {
+    __syncthreads();
+    const double p = nxt[c];
+    bad = bad || !(p > 0.0);
+    const double dg = sqrt(p);
+    const double inv = 1.0 / dg;
+    if (g == 0 && r >= c) {
+      const double l = (r > c) ? nxt[r] * inv : dg;
+      colbuf[r] = l;
+      sA[r * la + c] = l;
+    }
+    if (r == c) {
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        if (g + G * m <= c) x[m] = x[m] * inv;
+        rowbuf[g + G * m] = x[m];
+      }
+    }
+    __syncthreads();
+    if (r > c) {
+      const double l = colbuf[r];
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        const int s = g + G * m;
+        const double la_ = (s > c && s <= r) ? l : 0.0;  // trailing update of A
+        const double lx_ = (s <= c) ? l : 0.0;           // elimination of X
+        a[m] = a[m] - la_ * colbuf[s];
+        x[m] = x[m] - lx_ * rowbuf[s];
+        if (s == c + 1) nxt[r] = a[m];
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    const int s = g + G * m;
+    if (s > r) sA[r * la + s] = 0.0;
+    sX[r * lx + s] = x[m];
+  }
+  return bad;
+}
+
+// Fixed-order sum of the 8 partials scratch[q*64 + i], q = 0..7.
+__device__ __forceinline__ double sum8(const double* scratch, int i) {
+  return (((scratch[i] + scratch[64 + i]) + (scratch[128 + i] + scratch[192 + i])) +
+          ((scratch[256 + i] + scratch[320 + i]) + (scratch[384 + i] + scratch[448 + i])));
+}
+
+// out[r] = (sum_c s1[r][c] v1[c]) for r < 64 (or out[r] -= that); 8 partial sums
+// per row combined in fixed order. Ends with a barrier.
+__device__ __forceinline__ void rows_dot64(double* out, const double* s1, int l1, const double* v1, double* scratch,
+                                           bool accumulate) {
+  const int tid = threadIdx.x;
+  const int r = tid & 63, q = tid >> 6;
+  double acc = 0.0;
+  for (int c = q * 8; c < q * 8 + 8; ++c) acc = fma(s1[r * l1 + c], v1[c], acc);
+  scratch[q * 64 + r] = acc;
+  __syncthreads();
+  if (tid < 64) {
+    const double s = sum8(scratch, tid);
+    out[tid] = accumulate ? out[tid] - s : s;
+  }
+  __syncthreads();
+}
+
+// Column partials of a 64x64 LDS tile s (rows r, cols c): s2[c] += sum_r s^2,
+// sz[c] += sum_r s * z[r]. Fixed order. Ends with a barrier. scratch: 512 doubles.
+__device__ __forceinline__ void cols_partial64(double* s2, double* sz, const double* s, int ls, const double* z,
+                                               double* scratch) {
+  const int tid = threadIdx.x;
+  const int c = tid & 63, q = tid >> 6;
+  double a2 = 0.0, az = 0.0;
+  for (int r = q * 8; r < q * 8 + 8; ++r) {
+    const double v = s[r * ls + c];
+    a2 = fma(v, v, a2);
+    az = fma(v, z[r], az);
+  }
+  scratch[q * 64 + c] = a2;
+  __syncthreads();
+  if (tid < 64) s2[tid] = s2[tid] + sum8(scratch, tid);
+  __syncthreads();
+  scratch[q * 64 + c] = az;
+  __syncthreads();
+  if (tid < 64) sz[tid] = sz[tid] + sum8(scratch, tid);
+  __syncthreads();
+}
+
+struct DiagSmem {
+  double* t0;       // 64 x LDH
+  double* t1;       // 64 x LDH
+  double* xbuf;     // 192
+  double* y;        // 128
+  double* z;        // 128
+  double* ps2;      // 128
+  double* psz;      // 128
+  double* scratch;  // 512
+};
+
+// ----------------------------------------------------------------------------
+// Factor one fully reduced 128x128 diagonal block in place (2x2 blocks of 64):
+//   L11,U11 = factor64(A11) ; L21 = A21 U11^T ; A22 -= L21 L21^T ; L22,U22 = factor64(A22)
+//   U21 = -U22 (L21 U11) ; z = L^-1 y by forward substitution ; partials of colsum(U^2),
+//   U^T z for the 128 columns.
+// Lt/Ut: top-left of the block in the particle's L / U buffers (row stride ld);
+// yseg: the block's 128 RHS entries (replaced by z); s2o/szo: 128 partial outputs.
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __restrict__ Ut, size_t ld,
+                                          double* __restrict__ yseg, double* __restrict__ s2o,
+                                          double* __restrict__ szo, int* __restrict__ info, const DiagSmem& sm) {
+  const int tid = threadIdx.x;
+  const Quad<64> qd;
+  double* const t0 = sm.t0;
+  double* const t1 = sm.t1;
+
+  // (a) L11, U11, z1
+  tile64_to_lds(t0, LDH, Lt, ld);
+  if (tid < T) {
+    sm.y[tid] = yseg[tid];
+    sm.ps2[tid] = 0.0;
+    sm.psz[tid] = 0.0;
+  }
+  __syncthreads();
+  bool bad = factor64(t0, LDH, t1, LDH, sm.xbuf);
+  __syncthreads();
+  lds_to_tile64(Lt, ld, t0, LDH, true);
+  zero_tile64(Lt + H, ld);
+  lds_to_tile64(Ut, ld, t1, LDH, false);
+  zero_tile64(Ut + H, ld);
+  rows_dot64(sm.z, t1, LDH, sm.y, sm.scratch, false);          // z1 = U11 y1
+  cols_partial64(sm.ps2, sm.psz, t1, LDH, sm.z, sm.scratch);   // U11 columns
+
+  // (b) L21 = A21 U11^T
+  tile64_to_lds(t0, LDH, Lt + (size_t)H * ld, ld);
+  __syncthreads();
+  Acc<64> acc;
+  acc.zero();
+  gemm_lds64<false>(acc, t0, LDH, t1, LDH, qd);
+  __syncthreads();
+  acc.foreach(qd, [&](int r, int c, double v) {
+      t0[r * LDH + c] = v;
+      Lt[(size_t)(H + r) * ld + c] = v;
+    });
+  __syncthreads();
+
+  // (c) A22 -= L21 L21^T ; y2 -= L21 z1 ; T = L21 U11 (to the U21 slot as scratch)
+  acc.zero();
+  gemm_lds64<false>(acc, t0, LDH, t0, LDH, qd);
+  rows_dot64(sm.y + H, t0, LDH, sm.z, sm.scratch, true);
+  Acc<64> tt;
+  tt.zero();
+  gemm_lds64<true>(tt, t0, LDH, t1, LDH, qd);
+  __syncthreads();
+  double* U21 = Ut + (size_t)H * ld;
+  const double* A22 = Lt + (size_t)H * ld + H;
+  tt.foreach(qd, [&](int r, int c, double v) { U21[(size_t)r * ld + c] = v; });
+  acc.foreach(qd, [&](int r, int c, double v) { t0[r * LDH + c] = A22[(size_t)r * ld + c] - v; });
+  __syncthreads();
+
+  // (d) L22, U22
+  bad = factor64(t0, LDH, t1, LDH, sm.xbuf) || bad;
+  __syncthreads();
+  lds_to_tile64(Lt + (size_t)H * ld + H, ld, t0, LDH, true);
+  lds_to_tile64(Ut + (size_t)H * ld + H, ld, t1, LDH, false);
+  __syncthreads();
+
+  // (e) U21 = -U22 T
+  tile64_to_lds(t0, LDH, U21, ld);
+  __syncthreads();
+  acc.zero();
+  gemm_lds64<true>(acc, t1, LDH, t0, LDH, qd);
+  __syncthreads();
+  acc.foreach(qd, [&](int r, int c, double v) {
+      t0[r * LDH + c] = -v;
+      U21[(size_t)r * ld + c] = -v;
+    });
+  __syncthreads();
+
+  // (f) forward substitution: z2 = U22 (y2 - L21 z1) (y2 already reduced in (c))
+  rows_dot64(sm.z + H, t1, LDH, sm.y + H, sm.scratch, false);
+  // (g) partials: columns 0..63 get the U21 rows, columns 64..127 the U22 rows
+  cols_partial64(sm.ps2, sm.psz, t0, LDH, sm.z + H, sm.scratch);
+  cols_partial64(sm.ps2 + H, sm.psz + H, t1, LDH, sm.z + H, sm.scratch);
+  if (tid < T) {
+    s2o[tid] = sm.ps2[tid];
+    szo[tid] = sm.psz[tid];
+    yseg[tid] = sm.z[tid];
+  }
+  if (bad && tid == 0 && *info == 0) *info = 1;
+}
+
+// Shared-memory carve-up for the diagonal factor: two 64x64 tiles and the small
+// vectors live in `base` (the GEMM staging area, DIAG_BASE doubles), the
+// 512-double reduction scratch in `small`.
+constexpr int DIAG_BASE = 2 * H * LDH + 192 + 4 * T;
+constexpr int DIAG_SMALL = 512;
+__device__ __forceinline__ DiagSmem carve_diag(double* base, double* small) {
+  DiagSmem s;
+  s.t0 = base;
+  s.t1 = base + H * LDH;
+  s.xbuf = base + 2 * H * LDH;
+  s.y = s.xbuf + 192;
+  s.z = s.y + T;
+  s.ps2 = s.z + T;
+  s.psz = s.ps2 + T;
+  s.scratch = small;
+  return s;
+}
+
+// Diagonal block J of every particle (A_JJ already reduced by the look-ahead of
+// all earlier block columns). Launched for J = 0 only; every later diagonal
+// block is factored inside k_step by the workgroup that finishes reducing it.
+// grid: (P)
+__global__ __launch_bounds__(DNTH) void k_diag(int J, int nt, int Npad, double* __restrict__ Lb,
+                                                  double* __restrict__ Ub, double* __restrict__ yb,
+                                                  double* __restrict__ s2p, double* __restrict__ szp,
+                                                  int* __restrict__ info) {
+  __shared__ __attribute__((aligned(16))) double tiles[DIAG_BASE];
+  __shared__ double small[DIAG_SMALL];
+  const int p = blockIdx.x;
+  const size_t ld = (size_t)Npad;
+  const size_t off = (size_t)p * ld * ld + (size_t)J * T * ld + (size_t)J * T;
+  const DiagSmem sm = carve_diag(tiles, small);
+  const size_t poff = ((size_t)p * nt + J) * Npad + (size_t)J * T;
+  factor128(Lb + off, Ub + off, ld, yb + (size_t)p * Npad + J * T, s2p + poff, szp + poff, info + p, sm);
+}
+
+// ----------------------------------------------------------------------------
+// Block column J for every particle. grid: (nt-1, P)
+//   blockIdx.x <  nt-1-J : L tile I = J+1+blockIdx.x; the workgroup with I = J+1
+//                          (dispatched first) then factors the now fully reduced
+//                          diagonal block J+1 while the rest of the grid runs
+//   blockIdx.x >= nt-1-J : U tile K = blockIdx.x-(nt-1-J)
+// ----------------------------------------------------------------------------
+constexpr int STEP_SMEM = Geo<T>::STAGE;  // 9216 doubles = 72 KiB: two workgroups per CU
+constexpr int STEP_SMALL = 5 * T;         // z_J + reduction scratch (also the diagonal's scratch)
+static_assert(DIAG_BASE <= STEP_SMEM && DIAG_SMALL <= STEP_SMALL, "fused diagonal fits the step's LDS");
+constexpr int STEP_NTH = Geo<T>::NTH;     // 512 threads: 8 waves, 64x32 per wave
+static_assert(STEP_NTH == DNTH, "the fused diagonal runs on the step workgroup");
+
+__global__ __launch_bounds__(STEP_NTH, 4) void k_step(int J, int nt, int Npad, double* __restrict__ Lb,
+                                                  double* __restrict__ Ub, double* __restrict__ yb,
+                                                  double* __restrict__ s2p, double* __restrict__ szp,
+                                                  int* __restrict__ info) {
+  __shared__ __attribute__((aligned(16))) double smem[STEP_SMEM];
+  __shared__ double small[STEP_SMALL];
+  const int tid = threadIdx.x;
+  const int p = blockIdx.y;
+  const int nL = nt - 1 - J;
+  const size_t ld = (size_t)Npad;
+  double* Lp = Lb + (size_t)p * ld * ld;
+  double* Up = Ub + (size_t)p * ld * ld;
+  double* yp = yb + (size_t)p * Npad;
+  const Quad<T> qd;
+  const double* Ujj = Up + (size_t)J * T * ld + (size_t)J * T;
+  double* zj = small;  // z_J (128), written by the previous launch's diagonal
+  double* scratch = small + T;
+
+  if ((int)blockIdx.x < nL) {
+    const int I = J + 1 + blockIdx.x;
+    double* Aij = Lp + (size_t)I * T * ld + (size_t)J * T;
+    double* Aii = Lp + (size_t)I * T * ld + (size_t)I * T;
+    Acc<T> acc;
+    // C = A_IJ - L_I,<J L_J,<J^T (accumulator seeded with A_IJ, A operand staged negated)
+    acc.load(qd, Aij, ld);
+    if (J > 0)
+      gemm_stream<T, false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, J * T, smem, qd);
+    acc.store(qd, Aij, ld);
+    __syncthreads();
+    // L_IJ = C U_JJ^T
+    acc.zero();
+    gemm_stream<T, false>(acc, Aij, Npad, Ujj, Npad, T, smem, qd);
+    acc.store(qd, Aij, ld);
+    if (tid < T) zj[tid] = yp[J * T + tid];
+    __syncthreads();
+    // look-ahead: A_II -= L_IJ L_IJ^T (the full tile; only its lower half is ever read), y_I -= L_IJ z_J
+    acc.load(qd, Aii, ld);
+    gemm_stream<T, false, true>(acc, Aij, Npad, Aij, Npad, T, smem, qd);
+    acc.store(qd, Aii, ld);
+    {
+      const int r = tid & (T - 1), h = tid >> 7;  // 4 quarter-row partial dot products
+      const double* row = Aij + (size_t)r * ld + h * 32;
+      double s = 0.0;
+      for (int c = 0; c < 32; ++c) s = fma(row[c], zj[h * 32 + c], s);
+      scratch[h * T + r] = s;
+    }
+    __syncthreads();
+    if (tid < T)
+      yp[I * T + tid] =
+          yp[I * T + tid] - (((scratch[tid] + scratch[T + tid]) + scratch[2 * T + tid]) + scratch[3 * T + tid]);
+    if (I == J + 1) {  // fused diagonal factor of block J+1 (every reduction of A_II and y_I is done)
+      __syncthreads();
+      const DiagSmem sm = carve_diag(smem, small);
+      const size_t poff = ((size_t)p * nt + I) * Npad + (size_t)I * T;
+      factor128(Aii, Up + (size_t)I * T * ld + (size_t)I * T, ld, yp + I * T, s2p + poff, szp + poff, info + p, sm);
+    }
+  } else {
+    const int K = blockIdx.x - nL;
+    double* Ujk = Up + (size_t)J * T * ld + (size_t)K * T;
+    Acc<T> acc;
+    acc.zero();
+    // W = L_J,[K,J) U_[K,J),K, parked in the U_JK slot
+    gemm_stream<T, true>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad, Up + (size_t)K * T * ld + (size_t)K * T,
+                         Npad, (J - K) * T, smem, qd);
+    acc.store(qd, Ujk, ld);
+    if (tid < T) zj[tid] = yp[J * T + tid];
+    __syncthreads();
+    // U_JK = -U_JJ W (A operand staged negated)
+    acc.zero();
+    gemm_stream<T, true, true>(acc, Ujj, Npad, Ujk, Npad, T, smem, qd);
+    acc.store(qd, Ujk, ld);
+    // column partials straight from the accumulators: sum over this wave's rows,
+    // then the 4 lane groups, then the two row-halves of the tile (fixed order)
+    constexpr int MBR = Geo<T>::MBR, MBC = Geo<T>::MBC;
+    double* half = scratch;  // [2 quantities][T cols] from the lower row-half waves
+    const int wr = qd.wrow();
+#pragma unroll
+    for (int ni = 0; ni < MBC; ++ni) {
+      double a2 = 0.0, az = 0.0;
+#pragma unroll
+      for (int mi = 0; mi < MBR; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double v = acc.v[mi][ni][r];
+          a2 = fma(v, v, a2);
+          az = fma(v, zj[qd.row(mi, r)], az);
+        }
+      a2 = sum_lane_groups(a2);
+      az = sum_lane_groups(az);
+      if (wr == 1 && (qd.lane >> 4) == 0) {
+        half[qd.col(ni)] = a2;
+        half[T + qd.col(ni)] = az;
+      }
+      acc.v[0][ni][0] = a2;  // park the upper-half sums (accumulators are dead now)
+      acc.v[0][ni][1] = az;
+    }
+    __syncthreads();
+    if (wr == 0 && (qd.lane >> 4) == 0) {
+      const size_t poff = ((size_t)p * nt + J) * Npad + (size_t)K * T;
+#pragma unroll
+      for (int ni = 0; ni < MBC; ++ni) {
+        const int c = qd.col(ni);
+        s2p[poff + c] = acc.v[0][ni][0] + half[c];
+        szp[poff + c] = acc.v[0][ni][1] + half[T + c];
+      }
+    }
+  }
+}
+
+}  // namespace gpf

@@ -1,0 +1,101 @@
+// gpf_predict.hip — GP prediction at arbitrary query points (GP_func.py:26-45).
+//
+// With U = L^-1 from the factorisation, the reference's v = solve(L, K_s) (:38)
+// is V = U K_s; only its column sums of squares are needed (:39), so every
+// 128x128 tile of V is reduced in registers and never stored.
+#pragma once
+#include "gpf_common.hip"
+
+namespace gpf {
+
+// vsq[t][q*128 + c] = sum over the 128 rows of tile t of (U_t,<=t K_s[:, q-tile])^2.
+// grid: (nqt, nt)
+__global__ __launch_bounds__(Geo<T>::NTH, 4) void k_predict_vsq(int Npad, const double* __restrict__ U,
+                                                         const double* __restrict__ Ks, int ldks,
+                                                         double* __restrict__ vsq) {
+  __shared__ __attribute__((aligned(16))) double smem[Geo<T>::STAGE];
+  __shared__ double half[T];
+  const int q = blockIdx.x, t = blockIdx.y;
+  const Quad<T> qd;
+  Acc<T> acc;
+  acc.zero();
+  // U is lower triangular: row tile t needs columns [0, (t+1) * 128)
+  gemm_stream<T, true>(acc, U + (size_t)t * T * Npad, Npad, Ks + (size_t)q * T, ldks, (t + 1) * T, smem, qd);
+  constexpr int MBR = Geo<T>::MBR, MBC = Geo<T>::MBC;
+  const int wr = qd.wrow();
+  double part[MBC];
+#pragma unroll
+  for (int ni = 0; ni < MBC; ++ni) {
+    double a2 = 0.0;
+#pragma unroll
+    for (int mi = 0; mi < MBR; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a2 = fma(acc.v[mi][ni][r], acc.v[mi][ni][r], a2);
+    a2 = sum_lane_groups(a2);
+    part[ni] = a2;
+    if (wr == 1 && (qd.lane >> 4) == 0) half[qd.col(ni)] = a2;
+  }
+  __syncthreads();
+  if (wr == 0 && (qd.lane >> 4) == 0) {
+#pragma unroll
+    for (int ni = 0; ni < MBC; ++ni) {
+      const int c = qd.col(ni);
+      vsq[(size_t)t * ldks + (size_t)q * T + c] = part[ni] + half[c];
+    }
+  }
+}
+
+// mu_q = K_s[:, q]^T alpha (GP_func.py:36); var = clip(1 - sum v^2, 1e-12) (:39-40)
+// grid: (ceil(M/256))
+__global__ __launch_bounds__(NTHR) void k_predict_out(int N, int nt, int M, const double* __restrict__ Ks, int ldks,
+                                                      const double* __restrict__ alpha,
+                                                      const double* __restrict__ vsq, double* __restrict__ mu,
+                                                      double* __restrict__ sd) {
+  const int q = blockIdx.x * NTHR + threadIdx.x;
+  if (q >= M) return;
+  double m = 0.0;
+  for (int i = 0; i < N; ++i) m = fma(Ks[(size_t)i * ldks + q], alpha[i], m);
+  double s = 0.0;
+  for (int t = 0; t < nt; ++t) s = s + vsq[(size_t)t * ldks + q];
+  double var = 1.0 - s;
+  var = (var < 1e-12) ? 1e-12 : var;
+  mu[q] = m;
+  sd[q] = sqrt(var);
+}
+
+// alpha_c = sum_t szp[t][c] over row tiles t >= c/128 (particle slot 0). grid: ceil(N/256)
+__global__ __launch_bounds__(NTHR) void k_alpha(int N, int Npad, int nt, const double* __restrict__ szp,
+                                                double* __restrict__ alpha) {
+  const int c = blockIdx.x * NTHR + threadIdx.x;
+  if (c >= N) return;
+  double a = 0.0;
+  for (int t = c / T; t < nt; ++t) a = a + szp[(size_t)t * Npad + c];
+  alpha[c] = a;
+}
+
+// f64 MFMA layout self-test: one wave, C = A(16x4) * B(4x16)
+__global__ void k_selftest_mfma(const double* a, const double* b, double* c) {
+  const int l = threadIdx.x;
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  acc = mfma(a[(l & 15) * 4 + (l >> 4)], b[(l >> 4) * 16 + (l & 15)], acc);
+  for (int r = 0; r < 4; ++r) c[((l >> 4) + 4 * r) * 16 + (l & 15)] = acc[r];
+}
+
+// FP64 MFMA issue-rate probe: every wave runs `iters` rounds of 8 independent
+// v_mfma_f64_16x16x4_f64 chains (2048 flops each); out[block] keeps the result live.
+__global__ __launch_bounds__(NTHR) void k_mfma_rate(int iters, double seed, double* out) {
+  d4 acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = d4{0.0, 0.0, 0.0, 0.0};
+  const double a = seed + threadIdx.x * 1e-3, b = seed - threadIdx.x * 1e-3;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = mfma(a, b, acc[i]);
+  }
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+  if (s == 12345.678) out[blockIdx.x] = s;  // practically never taken; keeps the chains live
+}
+
+}  // namespace gpf

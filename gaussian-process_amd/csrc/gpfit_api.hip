@@ -16,8 +16,13 @@
 #include <vector>
 
 #include "../../include/gpfit.h"
-#include "gpfit_kernels.hip"
+#include "gpf_common.hip"
+#include "gpf_covariance.hip"
+#include "gpf_factor.hip"
+#include "gpf_objective.hip"
+#include "gpf_predict.hip"
 
+using gpf::BT;
 using gpf::NTHR;
 using gpf::T;
 
@@ -185,40 +190,40 @@ static int ensure_work(gpf_ctx* c, int want) {
 }
 
 // Factorise `pc` particles whose length scales are already in d_ls:
-// K build, then nt block columns of (diag, panel).
+// K build (lower 64x64 tiles), the first diagonal block (k_diag), then one
+// k_step per 128-wide block column (each also factors the next diagonal block).
 static int run_factor(gpf_ctx* c, int pc) {
   const int nt = c->nt, Np = (int)c->Npad, N = (int)c->N;
-  const double Tf = (double)T;
-  const int ntri = nt * (nt + 1) / 2;
-  int rc = launch(c, PC_BUILD, 8.0 * ntri * T * T * (double)pc, [&] {
+  const double Tf = (double)T, t3 = Tf * Tf * Tf;
+  const int nb = Np / BT;
+  const int ntri = nb * (nb + 1) / 2;
+  int rc = launch(c, PC_BUILD, 8.0 * ntri * BT * BT * (double)pc, [&] {
     hipLaunchKernelGGL(gpf::k_build_cov, dim3(ntri, pc), dim3(NTHR), 0, c->stream, N, Np, c->d, c->d_x, c->d_y,
                        c->d_e, c->d_ls, c->d_L, c->d_yb);
   });
   if (rc) return rc;
-  for (int j = 0; j < nt; ++j) {
-    // diag: 64^3/3 (potrf) + 64^3/3 (inverse) + 64^2 (z)
-    rc = launch(c, PC_DIAG, (2.0 / 3.0 * Tf * Tf * Tf + Tf * Tf) * pc, [&] {
-      hipLaunchKernelGGL(gpf::k_diag, dim3(pc), dim3(NTHR), 0, c->stream, j, nt, Np, c->d_L, c->d_U, c->d_yb,
-                         c->d_s2p, c->d_szp, c->d_info);
+  // potrf + trtri of the first 128 block: 2/3 T^3 (later blocks are fused into k_step)
+  rc = launch(c, PC_DIAG, (2.0 / 3.0) * t3 * pc, [&] {
+    hipLaunchKernelGGL(gpf::k_diag, dim3(pc), dim3(gpf::DNTH), 0, c->stream, 0, nt, Np, c->d_L, c->d_U, c->d_yb,
+                       c->d_s2p, c->d_szp, c->d_info);
+  });
+  if (rc) return rc;
+  for (int J = 0; nt > 1 && J < nt; ++J) {
+    // algorithmic flops on the potrf + trtri (2/3 N^3) formulation:
+    //   L tile: depth-128J GEMM 2 T^3 J + triangular multiply T^3 + look-ahead syrk share T^3
+    //   U tile: depth-128(J-K) GEMM with a triangular factor 2 T^3 (J-K) - T^3 + triangular multiply T^3
+    //   fused diagonal block J+1: 2/3 T^3
+    double fl = 0.0;
+    for (int w = 0; w < nt - 1; ++w) {
+      if (w < nt - 1 - J) fl += 2.0 * t3 * J + 2.0 * t3;
+      else fl += 2.0 * t3 * (J - (w - (nt - 1 - J)));
+    }
+    if (J + 1 < nt) fl += (2.0 / 3.0) * t3;
+    rc = launch(c, PC_PANEL, fl * pc, [&] {
+      hipLaunchKernelGGL(gpf::k_step, dim3(nt - 1, pc), dim3(gpf::STEP_NTH), 0, c->stream, J, nt, Np, c->d_L,
+                         c->d_U, c->d_yb, c->d_s2p, c->d_szp, c->d_info);
     });
     if (rc) return rc;
-    if (nt > 1) {
-      // algorithmic flops of this block column, counted on the 2/3 N^3 (potrf + trtri) formulation:
-      // L tiles: the depth-j GEMM (2*64^3*j) + the triangular multiply (64^3) ; the look-ahead syrk is
-      // the diagonal's share of potrf (64^3). U tiles: depth-(j-k) GEMM on a triangular operand
-      // (2*64^3*(j-k) - 64^3) + the triangular multiply (64^3).
-      double fl = 0.0;
-      const double t3 = Tf * Tf * Tf;
-      for (int w = 0; w < nt - 1; ++w) {
-        if (w >= j) fl += 2.0 * t3 * j + t3 + t3;
-        else fl += 2.0 * t3 * (j - w);
-      }
-      rc = launch(c, PC_PANEL, fl * pc, [&] {
-        hipLaunchKernelGGL(gpf::k_panel, dim3(nt - 1, pc), dim3(NTHR), 0, c->stream, j, nt, Np, c->d_L, c->d_U,
-                           c->d_yb, c->d_s2p, c->d_szp);
-      });
-      if (rc) return rc;
-    }
   }
   return GPF_OK;
 }
@@ -452,13 +457,13 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
     const int nqt = (int)((m + T - 1) / T);
     const int Cm = nqt * T;
     rc = launch(c, PC_BUILD, 8.0 * Np * Cm, [&] {
-      hipLaunchKernelGGL(gpf::k_cross_cov, dim3(nqt, c->nt), dim3(NTHR), 0, c->stream, (int)c->N, (int)m, (int)Np,
-                         Cm, c->d, c->d_x, (int)c->N, d_xf, (int)Cp, c->d_ls, d_ks, (int64_t)Cp);
+      hipLaunchKernelGGL(gpf::k_cross_cov, dim3(Cm / BT, (unsigned)(Np / BT)), dim3(NTHR), 0, c->stream, (int)c->N,
+                         (int)m, (int)Np, Cm, c->d, c->d_x, (int)c->N, d_xf, (int)Cp, c->d_ls, d_ks, (int64_t)Cp);
     });
     if (rc) break;
     rc = launch(c, PC_PANEL, 0.0, [&] {
-      hipLaunchKernelGGL(gpf::k_predict_vsq, dim3(nqt, c->nt), dim3(NTHR), 0, c->stream, c->nt, (int)Np, c->d_U,
-                         d_ks, (int)Cp, d_vsq);
+      hipLaunchKernelGGL(gpf::k_predict_vsq, dim3(nqt, c->nt), dim3(gpf::Geo<T>::NTH), 0, c->stream, (int)Np, c->d_U, d_ks,
+                         (int)Cp, d_vsq);
       hipLaunchKernelGGL(gpf::k_predict_out, dim3((unsigned)((m + NTHR - 1) / NTHR)), dim3(NTHR), 0, c->stream,
                          (int)c->N, c->nt, (int)m, d_ks, (int)Cp, alpha, d_vsq, d_mu, d_sd);
     });
@@ -492,7 +497,7 @@ int gpf_kernel(gpf_ctx* c, const double* x1, int64_t N1, const double* x2, int64
   GPF_HIP(c, hipMemcpyAsync(dx2, x2, (size_t)N2 * d * 8, hipMemcpyHostToDevice, c->stream));
   GPF_HIP(c, hipMemcpyAsync(dl, l, (size_t)d * 8, hipMemcpyHostToDevice, c->stream));
   int rc = launch(c, PC_BUILD, 8.0 * N1 * N2, [&] {
-    hipLaunchKernelGGL(gpf::k_cross_cov, dim3((unsigned)((N2 + T - 1) / T), (unsigned)((N1 + T - 1) / T)),
+    hipLaunchKernelGGL(gpf::k_cross_cov, dim3((unsigned)((N2 + BT - 1) / BT), (unsigned)((N1 + BT - 1) / BT)),
                        dim3(NTHR), 0, c->stream, (int)N1, (int)N2, (int)N1, (int)N2, d, dx1, (int)N1, dx2, (int)N2,
                        dl, dout, (int64_t)N2);
   });
@@ -568,6 +573,44 @@ int gpf_selftest_mfma(gpf_ctx* c, const double* a, const double* b, double* out)
   GPF_HIP(c, hipStreamSynchronize(c->stream));
   GPF_HIP(c, hipMemcpy(out, dc, 256 * 8, hipMemcpyDeviceToHost));
   hipFree(da); hipFree(db); hipFree(dc);
+  return GPF_OK;
+}
+
+int gpf_debug_factor(gpf_ctx* c, const double* ls, double* L, double* U, double* z, double* alpha) {
+  if (!c || !ls || !L || !U || !z || !alpha) return GPF_BAD_ARG;
+  if (c->N <= 0) return bad_arg(c, "gpf_debug_factor: call gpf_set_data first");
+  hipSetDevice(c->device);
+  if (c->K <= 0) c->K = 2;
+  double* al = nullptr;
+  int rc = factor_single(c, ls, &al);
+  if (rc && rc != GPF_NOT_PD) return rc;
+  const size_t np = (size_t)c->Npad;
+  GPF_HIP(c, hipMemcpy(L, c->d_L, np * np * 8, hipMemcpyDeviceToHost));
+  GPF_HIP(c, hipMemcpy(U, c->d_U, np * np * 8, hipMemcpyDeviceToHost));
+  GPF_HIP(c, hipMemcpy(z, c->d_yb, np * 8, hipMemcpyDeviceToHost));
+  GPF_HIP(c, hipMemcpy(alpha, al, (size_t)c->N * 8, hipMemcpyDeviceToHost));
+  return rc;
+}
+
+int gpf_mfma_peak(gpf_ctx* c, int blocks, int iters, double* tflops) {
+  if (!c || !tflops || blocks <= 0 || iters <= 0) return GPF_BAD_ARG;
+  hipSetDevice(c->device);
+  double* out = nullptr;
+  GPF_HIP(c, hipMalloc(&out, (size_t)blocks * 8));
+  hipEvent_t a, b;
+  GPF_HIP(c, hipEventCreate(&a));
+  GPF_HIP(c, hipEventCreate(&b));
+  hipLaunchKernelGGL(gpf::k_mfma_rate, dim3(blocks), dim3(NTHR), 0, c->stream, iters, 1.0, out);  // warm-up
+  GPF_HIP(c, hipEventRecord(a, c->stream));
+  hipLaunchKernelGGL(gpf::k_mfma_rate, dim3(blocks), dim3(NTHR), 0, c->stream, iters, 1.0, out);
+  GPF_HIP(c, hipEventRecord(b, c->stream));
+  GPF_HIP(c, hipEventSynchronize(b));
+  float ms = 0.f;
+  GPF_HIP(c, hipEventElapsedTime(&ms, a, b));
+  *tflops = (double)blocks * 4.0 * iters * 8.0 * 2048.0 / (ms * 1e-3) / 1e12;
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  hipFree(out);
   return GPF_OK;
 }
 

@@ -39,6 +39,8 @@ SIGNATURES = {
     "gpf_get_profile": (ctypes.c_int, [_vp, _dp, ctypes.c_int]),
     "gpf_reset_profile": (ctypes.c_int, [_vp]),
     "gpf_selftest_mfma": (ctypes.c_int, [_vp, _dp, _dp, _dp]),
+    "gpf_debug_factor": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _dp]),
+    "gpf_mfma_peak": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _dp]),
 }
 
 _LIB = None
@@ -193,6 +195,23 @@ class Context:
         keys = ["panel_ms", "panel_launches", "panel_flops", "diag_ms", "diag_launches", "diag_flops",
                 "build_ms", "build_launches", "build_bytes", "loss_ms", "loss_launches", "evals"]
         return dict(zip(keys, buf.tolist()))
+
+    def debug_factor(self, lengths):
+        """(L, U, z, alpha) of one particle: Npad x Npad factor and inverse (diagnostic)."""
+        ls = _f64(lengths).reshape(-1)
+        t = self.lib.gpf_tile()
+        npad = -(-self.N // t) * t
+        L, U = np.empty((npad, npad)), np.empty((npad, npad))
+        z, al = np.empty(npad), np.empty(self.N)
+        rc = self.lib.gpf_debug_factor(self._h, _ptr(ls), _ptr(L), _ptr(U), _ptr(z), _ptr(al))
+        if rc not in (GPF_OK, GPF_NOT_PD):
+            self._check(rc, "gpf_debug_factor")
+        return L, U, z, al
+
+    def mfma_peak(self, blocks=1024, iters=4096):
+        out = ctypes.c_double(0.0)
+        self._check(self.lib.gpf_mfma_peak(self._h, int(blocks), int(iters), ctypes.byref(out)), "gpf_mfma_peak")
+        return out.value
 
     def selftest_mfma(self, a, b):
         a, b = _f64(a), _f64(b)

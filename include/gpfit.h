@@ -114,6 +114,15 @@ int gpf_tile(void);
  * c: 16x16 row-major. */
 int gpf_selftest_mfma(gpf_ctx* ctx, const double* a, const double* b, double* c);
 
+/* Diagnostic: factorise one particle and copy back its Npad x Npad L and
+ * U = L^-1 (row-major; the strict upper triangles hold scratch), the
+ * forward-substituted RHS z (Npad) and alpha (N). Npad = ceil(N/128)*128. */
+int gpf_debug_factor(gpf_ctx* ctx, const double* ls, double* L, double* U, double* z, double* alpha);
+
+/* Diagnostic: measured FP64 MFMA throughput (TFLOP/s) of a register-only
+ * v_mfma_f64_16x16x4_f64 loop over `blocks` workgroups of 4 waves. */
+int gpf_mfma_peak(gpf_ctx* ctx, int blocks, int iters, double* tflops);
+
 #ifdef __cplusplus
 }
 #endif

@@ -27,7 +27,7 @@ def test_abi_version_and_tile():
     import gpfit._lib as L
     lib = L.load_library()
     assert lib.gpf_version() == L.ABI_VERSION == 1
-    assert lib.gpf_tile() == 64
+    assert lib.gpf_tile() == 128
 
 
 def test_library_is_gfx950_code_object():
