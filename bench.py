@@ -43,6 +43,20 @@ FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (dense), spec; see DESIGN.md
 HBM_PEAK_GBS = 8000.0
 
 
+def pmc_traffic(N, d, swarm):
+    """HBM bytes per k_step launch from the committed rocprofv3 PMC passes
+    (scripts/pmc_traffic.py writes profiles/<round>/k_step_traffic.json), or None."""
+    best = None
+    for f in sorted((ROOT / "profiles").glob("*/k_step_traffic.json")):
+        try:
+            t = json.loads(f.read_text())
+        except (OSError, ValueError):
+            continue
+        if t.get("N") == N and t.get("d") == d and t.get("swarm") == swarm:
+            best = {"bytes_per_launch": t["bytes_per_launch"], "source": str(f.relative_to(ROOT))}
+    return best
+
+
 def synthetic(N, d, seed, hetero=False):
     """x ~ U[0,1)^d, y = sum_k sin(2 pi x_k) + 0.1 N(0,1), e = 0.1."""
     rng = np.random.default_rng(seed)
@@ -168,9 +182,14 @@ def main():
 
     # roofline of the dominant kernel, from HIP events on the library stream
     achieved = prof["panel_flops"] / (prof["panel_ms"] * 1e-3) / 1e12 if prof["panel_ms"] > 0 else None
-    roof = {"kernel": "k_panel", "bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
+    ceiling = ctx.mfma_peak(blocks=2048, iters=4096) if rank == 0 else None
+    traffic = pmc_traffic(N, d, args.swarm_per_gpu)
+    roof = {"kernel": "k_step", "bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
-            "traffic": None,
+            "traffic": traffic["bytes_per_launch"] if traffic else None,
+            "traffic_source": traffic["source"] if traffic else None,
+            "measured_mfma_ceiling_tflops": ceiling,
+            "frac_of_measured_ceiling": (achieved / ceiling) if (achieved and ceiling) else None,
             "launches": prof["panel_launches"], "avg_launch_ms": prof["panel_ms"] / max(prof["panel_launches"], 1),
             "flops_per_launch": prof["panel_flops"] / max(prof["panel_launches"], 1),
             "formulation": "potrf+trtri (2/3 N^3 per eval)"}

@@ -19,7 +19,7 @@ constexpr int NTHR = 256;   // 4 waves of 64 lanes per workgroup (covariance / o
 constexpr int DNTH = 512;   // 8 waves: the factorisation kernels (k_step, k_diag)
 constexpr int T = 128;      // factorisation block (block column width, padding granule)
 constexpr int H = 64;       // half block: the unblocked diagonal factor works on 64x64
-constexpr int LDH = H + 2;  // [row][k] stride of an LDS-resident 64x64 tile (ld/2 odd: conflict-free b64 reads)
+constexpr int LDH = H + 1;  // [row][k] stride of an LDS-resident 64x64 tile (odd: conflict-free b64 / read2_b64)
 constexpr int DMAX = 32;    // max input dimensionality of the covariance builders
 constexpr int KGRID_MAX = 4096;
 
@@ -48,7 +48,9 @@ template <int TM> struct Geo {
   static constexpr int NTH = 64 * NW;
   static constexpr int MBR = TM / WR / 16;
   static constexpr int MBC = TM / WC / 16;
-  static constexpr int RK = KC + 2;   // [row][k] staging stride (ld/2 odd)
+  // [row][k] staging stride: odd, so 16 consecutive rows hit 16 distinct bank pairs both for
+  // ds_read_b64 (banks mod 64) and for the ds_read2_b64 the compiler pairs them into (mod 32)
+  static constexpr int RK = KC + 1;
   static constexpr int KN = TM + 16;  // [k][col] staging stride (2*ld == 32 mod 64 dwords)
   static constexpr int SA = TM * RK;
   static constexpr int SB = (TM * RK > KC * KN) ? TM * RK : KC * KN;
@@ -170,9 +172,12 @@ __device__ __forceinline__ void stage_store(double* sA, double* sB, const d2 (&r
   for (int u = 0; u < Geo<TM>::NLD; ++u) {
     const int q = tid + Geo<TM>::NTH * u;
     const int row = q / (KC / 2), c2 = q % (KC / 2);
-    *reinterpret_cast<d2*>(sA + row * RK + 2 * c2) = NEG ? -ra[u] : ra[u];
+    const d2 va = NEG ? -ra[u] : ra[u];
+    sA[row * RK + 2 * c2] = va.x;  // odd stride: 8-byte aligned rows, two b64 stores
+    sA[row * RK + 2 * c2 + 1] = va.y;
     if (!NN) {
-      *reinterpret_cast<d2*>(sB + row * RK + 2 * c2) = rb[u];
+      sB[row * RK + 2 * c2] = rb[u].x;
+      sB[row * RK + 2 * c2 + 1] = rb[u].y;
     } else {
       const int kr = q / (TM / 2), cc = q % (TM / 2);
       *reinterpret_cast<d2*>(sB + kr * KN + 2 * cc) = rb[u];

@@ -288,13 +288,17 @@ __global__ __launch_bounds__(DNTH) void k_diag(int J, int nt, int Npad, double* 
 }
 
 // ----------------------------------------------------------------------------
-// Block column J for every particle. grid: (nt-1, P)
-//   blockIdx.x <  nt-1-J : L tile I = J+1+blockIdx.x; the workgroup with I = J+1
-//                          (dispatched first) then factors the now fully reduced
-//                          diagonal block J+1 while the rest of the grid runs
-//   blockIdx.x >= nt-1-J : U tile K = blockIdx.x-(nt-1-J)
+// Block column J for every particle. grid: (P, nt-1), particle fastest:
+//   w = blockIdx.y <  nt-1-J : L tile I = J+1+w; the workgroup with I = J+1
+//                              (dispatched first) then factors the now fully
+//                              reduced diagonal block J+1 while the rest runs
+//   w = blockIdx.y >= nt-1-J : U tile K = w-(nt-1-J)
+// Work per tile falls with w (L tiles and U_0 have depth J, U_K depth J-K), so
+// the dispatch order is longest-first over the whole launch; and with P a
+// multiple of 8 the round-robin dispatcher puts every workgroup of particle p
+// on XCD p mod 8, so a particle's shared B panel is fetched into one L2 only.
 // ----------------------------------------------------------------------------
-constexpr int STEP_SMEM = Geo<T>::STAGE;  // 9216 doubles = 72 KiB: two workgroups per CU
+constexpr int STEP_SMEM = (Geo<T>::STAGE > DIAG_BASE) ? Geo<T>::STAGE : DIAG_BASE;  // ~72 KiB: two workgroups per CU
 constexpr int STEP_SMALL = 5 * T;         // z_J + reduction scratch (also the diagonal's scratch)
 static_assert(DIAG_BASE <= STEP_SMEM && DIAG_SMALL <= STEP_SMALL, "fused diagonal fits the step's LDS");
 constexpr int STEP_NTH = Geo<T>::NTH;     // 512 threads: 8 waves, 64x32 per wave
@@ -307,7 +311,8 @@ __global__ __launch_bounds__(STEP_NTH, 4) void k_step(int J, int nt, int Npad, d
   __shared__ __attribute__((aligned(16))) double smem[STEP_SMEM];
   __shared__ double small[STEP_SMALL];
   const int tid = threadIdx.x;
-  const int p = blockIdx.y;
+  const int p = blockIdx.x;
+  const int w = blockIdx.y;
   const int nL = nt - 1 - J;
   const size_t ld = (size_t)Npad;
   double* Lp = Lb + (size_t)p * ld * ld;
@@ -318,8 +323,8 @@ __global__ __launch_bounds__(STEP_NTH, 4) void k_step(int J, int nt, int Npad, d
   double* zj = small;  // z_J (128), written by the previous launch's diagonal
   double* scratch = small + T;
 
-  if ((int)blockIdx.x < nL) {
-    const int I = J + 1 + blockIdx.x;
+  if (w < nL) {
+    const int I = J + 1 + w;
     double* Aij = Lp + (size_t)I * T * ld + (size_t)J * T;
     double* Aii = Lp + (size_t)I * T * ld + (size_t)I * T;
     Acc<T> acc;
@@ -357,7 +362,7 @@ __global__ __launch_bounds__(STEP_NTH, 4) void k_step(int J, int nt, int Npad, d
       factor128(Aii, Up + (size_t)I * T * ld + (size_t)I * T, ld, yp + I * T, s2p + poff, szp + poff, info + p, sm);
     }
   } else {
-    const int K = blockIdx.x - nL;
+    const int K = w - nL;
     double* Ujk = Up + (size_t)J * T * ld + (size_t)K * T;
     Acc<T> acc;
     acc.zero();

@@ -220,7 +220,7 @@ static int run_factor(gpf_ctx* c, int pc) {
     }
     if (J + 1 < nt) fl += (2.0 / 3.0) * t3;
     rc = launch(c, PC_PANEL, fl * pc, [&] {
-      hipLaunchKernelGGL(gpf::k_step, dim3(nt - 1, pc), dim3(gpf::STEP_NTH), 0, c->stream, J, nt, Np, c->d_L,
+      hipLaunchKernelGGL(gpf::k_step, dim3(pc, nt - 1), dim3(gpf::STEP_NTH), 0, c->stream, J, nt, Np, c->d_L,
                          c->d_U, c->d_yb, c->d_s2p, c->d_szp, c->d_info);
     });
     if (rc) return rc;

@@ -2,6 +2,7 @@
 cd "$GRAFT_REPO_ROOT"
 TAG=${TAG:-r1}
 export TMPDIR=/tmp
+python -c "import __graft_entry__ as g; g.build()" || exit 3
 mkdir -p gpurun_out/$TAG
 timeout -k 10 600 python -m pytest tests -q -m gpu -p no:cacheprovider > gpurun_out/$TAG/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/$TAG/pytest_gpu.log; tail -4 gpurun_out/$TAG/pytest_gpu.log
