@@ -8,6 +8,9 @@ What it executes from the reference:
   * ``GP_func`` is imported as shipped (numpy only).
   * ``read_in.read_data`` is imported as shipped (pandas/yaml) to load the
     bundled Test_file*.txt exactly as the reference does (read_in.py:204-239).
+  * ``convex_hull`` and ``calc_prob_surf`` are imported as shipped (scipy,
+    pandas) for the hull-grid (F6) and probability-surface (F7) fixtures.
+  * ``tests/golden/inputs/`` holds copies of the bundled input data files.
   * ``find_len_scales`` cannot be imported as shipped: its top-level
     ``from smt.sampling_methods import LHS`` (find_len_scales.py:11) names a
     package that is not installed and not available offline. The script parses
@@ -42,6 +45,8 @@ sys.path.insert(0, str(REF))
 
 import GP_func as ref_gp  # noqa: E402
 import read_in as ref_read  # noqa: E402
+import convex_hull as ref_hull  # noqa: E402
+import calc_prob_surf as ref_prob  # noqa: E402
 
 
 def load_find_len_scales():
@@ -252,9 +257,55 @@ def make_f4_f5(exps):
     np.savez_compressed(OUT / "f4_pso_trace.npz", **arrays)
 
 
+def make_f6(exps):
+    """F6: fill_convex_hull grids (convex_hull.py:203-224) for the bundled experiments and
+    synthetic 2-D / 3-D point sets at several resolutions."""
+    arrays = {}
+    cases = [(x.T.copy(), [0.01, 0.01]) for _, x, _, _ in exps]
+    cases += [(x.T.copy(), [0.05, 0.1]) for _, x, _, _ in exps[:2]]
+    rng = np.random.default_rng(7)
+    cases.append((np.round(rng.uniform(0, 1, size=(12, 2)), 2), [0.02, 0.05]))
+    cases.append((np.round(rng.uniform(0, 1, size=(10, 3)), 1), [0.1, 0.1, 0.1]))
+    cases.append((np.round(rng.uniform(-1, 2, size=(9, 3)), 1), [0.2, 0.1, 0.25]))
+    for i, (pts, res) in enumerate(cases):
+        grid = ref_hull.fill_convex_hull(pts, list(res))
+        arrays.update({f"c{i}_points": pts, f"c{i}_res": np.array(res), f"c{i}_grid": grid})
+        print(f"F6 case {i}: {pts.shape} res={res} -> grid {grid.shape}")
+    arrays["ncases"] = np.array(len(cases))
+    np.savez_compressed(OUT / "f6_hull.npz", **arrays)
+
+
+def make_f7():
+    """F7: generate_prob_surf (calc_prob_surf.py:39-88) on a small merged frame with inf gaps."""
+    rng = np.random.default_rng(3)
+    n = 40
+    df = pd.DataFrame({"Plab": np.round(rng.uniform(1, 2, n), 2), "cosTheta": np.round(rng.uniform(-1, 1, n), 2),
+                       "A": rng.normal(0.5, 0.2, n), "A_unc": rng.uniform(0.05, 0.2, n),
+                       "B": rng.normal(0.3, 0.2, n), "B_unc": rng.uniform(0.05, 0.2, n)})
+    df.loc[::3, ["B", "B_unc"]] = np.inf
+    df.loc[::7, ["A", "A_unc"]] = np.inf
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        out = Path(td) / "ps.txt"
+        opt = Path(td) / "options.yaml"
+        opt.write_text(f"out_file_name: '{out}'\n")
+        with contextlib.redirect_stdout(io.StringIO()):
+            ref_prob.generate_prob_surf(df, 2, options_path=str(opt))
+        res = pd.read_csv(out)
+    np.savez_compressed(OUT / "f7_prob_surf.npz", frame=df.values, columns=np.array(list(df.columns)),
+                        out=res.values, out_columns=np.array(list(res.columns)))
+    print(f"F7: {df.shape} -> {res.shape}")
+
+
 if __name__ == "__main__":
     exps = test_experiments()
+    if "--only-host" in sys.argv:
+        make_f6(exps)
+        make_f7()
+        sys.exit(0)
     make_f1(exps)
     make_f2(exps)
     make_f3()
     make_f4_f5(exps)
+    make_f6(exps)
+    make_f7()
