@@ -43,6 +43,17 @@ FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (dense), spec; see DESIGN.md
 HBM_PEAK_GBS = 8000.0
 
 
+def config_letter(N, d, swarm, hetero):
+    """BASELINE.json configs: B = N1024 d2 P32, C/D = N4096 d3 (64 / 32 per GPU), E = N16384 d4 hetero."""
+    if (N, d) == (1024, 2):
+        return "B"
+    if (N, d) == (4096, 3):
+        return "C" if swarm == 64 else "D"
+    if (N, d) == (16384, 4) and hetero:
+        return "E"
+    return "custom"
+
+
 def pmc_traffic(N, d, swarm):
     """HBM bytes per k_step launch from the committed rocprofv3 PMC passes
     (scripts/pmc_traffic.py writes profiles/<round>/k_step_traffic.json), or None."""
@@ -212,11 +223,12 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "PSO objective evals/sec (swarm x iters) at N=4096 d=3",
+            "metric": f"PSO objective evals/sec (swarm x iters) at N={N} d={d}",
             "value": value, "unit": "evals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": f"PSO objective, BASELINE config C: synthetic N={N} d={d}, swarm {args.swarm_per_gpu}/GPU",
+            "config": {"workload": f"PSO objective, BASELINE config {config_letter(N, d, args.swarm_per_gpu, args.hetero)}: "
+                                   f"synthetic N={N} d={d}, swarm {args.swarm_per_gpu}/GPU",
                        "N": N, "d": d, "swarm": P, "global_batch": P, "seq_len": N,
                        "parallelism": f"swarm-shard x{world}", "hetero_noise": bool(args.hetero),
                        "pso_iters_per_s": args.steps / dt, "particles": "interior l~U[0.05,0.6]^d (full work)"},
