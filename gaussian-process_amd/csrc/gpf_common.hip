@@ -33,8 +33,11 @@ __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
 // WR x WC; each wave holds a (TM/WR) x (TM/WC) sub-tile as MBR x MBC MFMA blocks
 // of 16x16 (accumulators: 4 doubles per lane per block).
 template <int TM> struct TileCfg;
+#ifndef GPF_STEP_KC
+#define GPF_STEP_KC 16  // K depth per LDS stage of the 128-tile GEMMs (build-time tuning knob)
+#endif
 template <> struct TileCfg<128> {  // the factorisation / prediction GEMMs: 8 waves, 64x32 per wave
-  static constexpr int KC = 16, NW = 8, WR = 2, WC = 4;
+  static constexpr int KC = GPF_STEP_KC, NW = 8, WR = 2, WC = 4;
 };
 template <> struct TileCfg<64> {   // LDS-resident 64x64 products inside the diagonal factor: 8 waves, 32x16 each
   static constexpr int KC = 32, NW = 8, WR = 2, WC = 4;

@@ -22,6 +22,26 @@
 
 namespace gpf {
 
+#ifdef GPF_DIAG_STAMPS
+// Diagnostic build only (-DGPF_DIAG_STAMPS): thread 0 of workgroup 0 records s_memtime at
+// phase boundaries of factor128 into a buffer nothing else reads.
+__device__ unsigned long long g_diag_stamps[32];
+#define DIAG_STAMP(i)                                                                              \
+  do {                                                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) {                                \
+      unsigned long long t_;                                                                     \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                  \
+      g_diag_stamps[i] = t_;                                                                     \
+    }                                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+  } while (0)
+#else
+#define DIAG_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+
 // The diagonal-block routines below run on all DNTH (= 512) threads of the
 // factorisation workgroups (k_diag and, fused, k_step).
 
@@ -175,6 +195,7 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
   double* const t0 = sm.t0;
   double* const t1 = sm.t1;
 
+  DIAG_STAMP(0);
   // (a) L11, U11, z1
   tile64_to_lds(t0, LDH, Lt, ld);
   if (tid < T) {
@@ -185,6 +206,7 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
   __syncthreads();
   bool bad = factor64(t0, LDH, t1, LDH, sm.xbuf);
   __syncthreads();
+  DIAG_STAMP(1);
   lds_to_tile64(Lt, ld, t0, LDH, true);
   zero_tile64(Lt + H, ld);
   lds_to_tile64(Ut, ld, t1, LDH, false);
@@ -192,6 +214,7 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
   rows_dot64(sm.z, t1, LDH, sm.y, sm.scratch, false);          // z1 = U11 y1
   cols_partial64(sm.ps2, sm.psz, t1, LDH, sm.z, sm.scratch);   // U11 columns
 
+  DIAG_STAMP(2);
   // (b) L21 = A21 U11^T
   tile64_to_lds(t0, LDH, Lt + (size_t)H * ld, ld);
   __syncthreads();
@@ -205,6 +228,7 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
     });
   __syncthreads();
 
+  DIAG_STAMP(3);
   // (c) A22 -= L21 L21^T ; y2 -= L21 z1 ; T = L21 U11 (to the U21 slot as scratch)
   acc.zero();
   gemm_lds64<false>(acc, t0, LDH, t0, LDH, qd);
@@ -219,13 +243,16 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
   acc.foreach(qd, [&](int r, int c, double v) { t0[r * LDH + c] = A22[(size_t)r * ld + c] - v; });
   __syncthreads();
 
+  DIAG_STAMP(4);
   // (d) L22, U22
   bad = factor64(t0, LDH, t1, LDH, sm.xbuf) || bad;
   __syncthreads();
+  DIAG_STAMP(5);
   lds_to_tile64(Lt + (size_t)H * ld + H, ld, t0, LDH, true);
   lds_to_tile64(Ut + (size_t)H * ld + H, ld, t1, LDH, false);
   __syncthreads();
 
+  DIAG_STAMP(6);
   // (e) U21 = -U22 T
   tile64_to_lds(t0, LDH, U21, ld);
   __syncthreads();
@@ -238,8 +265,10 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
     });
   __syncthreads();
 
+  DIAG_STAMP(7);
   // (f) forward substitution: z2 = U22 (y2 - L21 z1) (y2 already reduced in (c))
   rows_dot64(sm.z + H, t1, LDH, sm.y + H, sm.scratch, false);
+  DIAG_STAMP(8);
   // (g) partials: columns 0..63 get the U21 rows, columns 64..127 the U22 rows
   cols_partial64(sm.ps2, sm.psz, t0, LDH, sm.z + H, sm.scratch);
   cols_partial64(sm.ps2 + H, sm.psz + H, t1, LDH, sm.z + H, sm.scratch);
@@ -249,6 +278,7 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
     yseg[tid] = sm.z[tid];
   }
   if (bad && tid == 0 && *info == 0) *info = 1;
+  DIAG_STAMP(9);
 }
 
 // Shared-memory carve-up for the diagonal factor: two 64x64 tiles and the small
@@ -304,7 +334,10 @@ static_assert(DIAG_BASE <= STEP_SMEM && DIAG_SMALL <= STEP_SMALL, "fused diagona
 constexpr int STEP_NTH = Geo<T>::NTH;     // 512 threads: 8 waves, 64x32 per wave
 static_assert(STEP_NTH == DNTH, "the fused diagonal runs on the step workgroup");
 
-__global__ __launch_bounds__(STEP_NTH, 4) void k_step(int J, int nt, int Npad, double* __restrict__ Lb,
+#ifndef GPF_STEP_WAVES_PER_SIMD
+#define GPF_STEP_WAVES_PER_SIMD 4  // 2 workgroups of 8 waves per CU
+#endif
+__global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int J, int nt, int Npad, double* __restrict__ Lb,
                                                   double* __restrict__ Ub, double* __restrict__ yb,
                                                   double* __restrict__ s2p, double* __restrict__ szp,
                                                   int* __restrict__ info) {

@@ -614,4 +614,16 @@ int gpf_mfma_peak(gpf_ctx* c, int blocks, int iters, double* tflops) {
   return GPF_OK;
 }
 
+#ifdef GPF_DIAG_STAMPS
+// diagnostic builds only: phase timestamps of factor128 (workgroup 0 of the last k_diag launch)
+int gpf_debug_diag_stamps(unsigned long long* out, int n) {
+  if (!out || n <= 0) return GPF_BAD_ARG;
+  hipDeviceSynchronize();
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gpf::g_diag_stamps), sizeof(unsigned long long) * std::min(n, 32)) !=
+      hipSuccess)
+    return GPF_HIP_ERROR;
+  return GPF_OK;
+}
+#endif
+
 }  // extern "C"

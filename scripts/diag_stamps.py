@@ -1,0 +1,24 @@
+"""Diagnostic: phase timing of the 128x128 diagonal factor (stamped build)."""
+import ctypes, os, sys
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["GPFIT_LIB"] = os.path.join(ROOT, "gaussian-process_amd", "libgpfit_stamps.so")
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gaussian-process_amd")]
+import torch  # noqa
+import gpfit
+from oracle import ref_cpu
+ctx = gpfit.Context(0)
+names = ["factor64 #1", "store L11/U11, z1, partials", "L21 = A21 U11^T", "syrk, y2, T", "factor64 #2",
+         "store L22/U22", "U21 = -U22 T", "z2", "partials + out"]
+for N, P in [(128, 1), (128, 64), (4096, 64)]:
+    rng = np.random.default_rng(0)
+    x = rng.uniform(size=(3, N)); y = np.sin(6 * x[0]); e = np.full(N, 0.1)
+    lo, hi = ref_cpu.search_bounds(x); s, ex = ref_cpu.sigma_grid()
+    ctx.set_data(x, y, e); ctx.set_grid(s, ex, lo, hi)
+    for _ in range(3):
+        ctx.eval_batch(rng.uniform(0.1, 0.5, size=(P, 3)))
+    buf = (ctypes.c_ulonglong * 32)()
+    assert ctx.lib.gpf_debug_diag_stamps(buf, 32) == 0
+    st = np.array(buf[:10], dtype=np.float64)
+    d = np.diff(st)
+    print(f"N={N} P={P}: total {st[9]-st[0]:.0f} cycles; " + ", ".join(f"{n} {v:.0f}" for n, v in zip(names, d)))
