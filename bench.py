@@ -203,7 +203,9 @@ def main():
             "frac_of_measured_ceiling": (achieved / ceiling) if (achieved and ceiling) else None,
             "launches": prof["panel_launches"], "avg_launch_ms": prof["panel_ms"] / max(prof["panel_launches"], 1),
             "flops_per_launch": prof["panel_flops"] / max(prof["panel_launches"], 1),
-            "formulation": "potrf+trtri (2/3 N^3 per eval)"}
+            "formulation": "potrf+trtri (2/3 N^3 per eval)",
+            "factor_phase_tflops": (prof["factor_flops"] / (prof["factor_wall_ms"] * 1e-3) / 1e12)
+            if prof["factor_wall_ms"] > 0 else None}
     build_gbs = (prof["build_bytes"] / (prof["build_ms"] * 1e-3) / 1e9) if prof["build_ms"] > 0 else None
     breakdown = {k: prof[k] for k in ("panel_ms", "diag_ms", "build_ms", "loss_ms")}
     breakdown["k_build_cov_GBps"] = build_gbs

@@ -68,7 +68,7 @@ template <int TM> struct Quad {
   __device__ Quad() {
     const int tid = threadIdx.x;
     lane = tid & 63;
-    const int w = tid >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar) tile origin
     rb = (w / Geo<TM>::WC) * (TM / Geo<TM>::WR);
     cb = (w % Geo<TM>::WC) * (TM / Geo<TM>::WC);
   }
@@ -77,12 +77,17 @@ template <int TM> struct Quad {
   __device__ __forceinline__ int col(int ni) const { return cb + ni * 16 + (lane & 15); }
 };
 
-// Hide a pointer's value from the optimiser so addresses derived from it are
-// recomputed per use instead of being kept live (and spilled) across GEMMs.
+// Hide a global pointer's value from the optimiser so addresses derived from it
+// are recomputed per use instead of being kept live (and spilled) across GEMMs.
+// The pointer goes through the asm in the global address space, so accesses
+// through the result stay global_load/store: a generic (flat) access would also
+// count against lgkmcnt, and every LDS wait would then wait for HBM as well.
 template <typename P>
 __device__ __forceinline__ P* launder(P* p) {
-  asm volatile("" : "+v"(p));
-  return p;
+  using G = __attribute__((address_space(1))) P*;
+  G g = (G)p;
+  asm volatile("" : "+v"(g));
+  return (P*)g;
 }
 
 template <int TM> struct Acc {
@@ -188,8 +193,31 @@ __device__ __forceinline__ void stage_store(double* sA, double* sB, const d2 (&r
   }
 }
 
-template <int TM, bool NN>
-__device__ __forceinline__ void stage_mma(Acc<TM>& acc, const double* sA, const double* sB, const Quad<TM>& qd) {
+// Known-zero structure of a GEMM's operands or unneeded output: MFMAs whose
+// 16x16x4 block is entirely zero (or whose output block is never read) are
+// skipped by a wave-uniform branch. Skipping adds of exact zeros leaves every
+// result bit unchanged (up to the sign of a zero).
+enum Tri : int {
+  TRI_NONE = 0,
+  TRI_B_KLEC,   // B(k,c) = 0 for k > c   (B = U^T with U lower triangular)
+  TRI_B_KGEC,   // B(k,c) = 0 for k < c   (B = U with U lower triangular in its first T rows)
+  TRI_A_KLER,   // A(r,k) = 0 for k > r   (A = U lower triangular)
+  TRI_C_LOWER,  // only C(r,c) with c <= r is ever read (symmetric rank-k update)
+};
+
+// does the 16x16x4 MFMA block (rows R0.., cols C0.., depth k..k+3) contribute?
+template <int TRI>
+__device__ __forceinline__ bool tri_live(int R0, int C0, int k) {
+  if (TRI == TRI_B_KLEC) return k <= C0 + 15;
+  if (TRI == TRI_B_KGEC) return k + 3 >= C0;
+  if (TRI == TRI_A_KLER) return k <= R0 + 15;
+  if (TRI == TRI_C_LOWER) return C0 <= R0 + 15;
+  return true;
+}
+
+template <int TM, bool NN, int TRI = TRI_NONE>
+__device__ __forceinline__ void stage_mma(Acc<TM>& acc, const double* sA, const double* sB, const Quad<TM>& qd,
+                                          int k0 = 0) {
   constexpr int KC = Geo<TM>::KC, RK = Geo<TM>::RK, KN = Geo<TM>::KN;
   constexpr int MBR = Geo<TM>::MBR, MBC = Geo<TM>::MBC;
   const int lr = qd.lane & 15, lk = qd.lane >> 4;
@@ -208,11 +236,12 @@ __device__ __forceinline__ void stage_mma(Acc<TM>& acc, const double* sA, const 
 #pragma unroll
     for (int mi = 0; mi < MBR; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < MBC; ++ni) acc.v[mi][ni] = mfma(a[mi], b[ni], acc.v[mi][ni]);
+      for (int ni = 0; ni < MBC; ++ni)
+        if (tri_live<TRI>(qd.rb + mi * 16, qd.cb + ni * 16, k0 + ks)) acc.v[mi][ni] = mfma(a[mi], b[ni], acc.v[mi][ni]);
   }
 }
 
-template <int TM, bool NN, bool NEG = false>
+template <int TM, bool NN, bool NEG = false, int TRI = TRI_NONE>
 __device__ void gemm_stream(Acc<TM>& acc, const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
                             int ldb, int K, double* smem, const Quad<TM>& qd) {
   constexpr int KC = Geo<TM>::KC, SA = Geo<TM>::SA, SB = Geo<TM>::SB, NLD = Geo<TM>::NLD;
@@ -230,7 +259,7 @@ __device__ void gemm_stream(Acc<TM>& acc, const double* __restrict__ Ap, int lda
     const bool more = (t + 1) < nch;
     if (more) stage_load<TM, NN>(ra, rb, Ap, lda, Bp, ldb, (t + 1) * KC, tid);
     const double* cur = smem + (t & 1) * (SA + SB);
-    stage_mma<TM, NN>(acc, cur, cur + SA, qd);
+    stage_mma<TM, NN, TRI>(acc, cur, cur + SA, qd, t * KC);
     if (more) {
       double* nxt = smem + ((t + 1) & 1) * (SA + SB);
       stage_store<TM, NN, NEG>(nxt, nxt + SA, ra, rb, tid);

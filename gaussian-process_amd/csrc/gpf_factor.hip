@@ -29,7 +29,7 @@ __device__ unsigned long long g_diag_stamps[32];
 #define DIAG_STAMP(i)                                                                              \
   do {                                                                                           \
     __builtin_amdgcn_sched_barrier(0);                                                           \
-    if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) {                                \
+    if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) {  /* WG (p 0, w 0) */                                \
       unsigned long long t_;                                                                     \
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                  \
       g_diag_stamps[i] = t_;                                                                     \
@@ -318,16 +318,33 @@ __global__ __launch_bounds__(DNTH) void k_diag(int J, int nt, int Npad, double* 
 }
 
 // ----------------------------------------------------------------------------
-// Block column J for every particle. grid: (P, nt-1), particle fastest:
-//   w = blockIdx.y <  nt-1-J : L tile I = J+1+w; the workgroup with I = J+1
-//                              (dispatched first) then factors the now fully
-//                              reduced diagonal block J+1 while the rest runs
-//   w = blockIdx.y >= nt-1-J : U tile K = w-(nt-1-J)
-// Work per tile falls with w (L tiles and U_0 have depth J, U_K depth J-K), so
-// the dispatch order is longest-first over the whole launch; and with P a
-// multiple of 8 the round-robin dispatcher puts every workgroup of particle p
-// on XCD p mod 8, so a particle's shared B panel is fetched into one L2 only.
+// Block column J for every particle. 1-D grid of P*(nt-1) workgroups; a
+// workgroup's (particle p, tile w) comes from its linear id (step_tile):
+//   w <  nt-1-J : L tile I = J+1+w; the workgroup with I = J+1 (w = 0) then
+//                 factors the now fully reduced diagonal block J+1
+//   w >= nt-1-J : U tile K = w-(nt-1-J)
+// Work per tile falls with w (L tiles and U_0 have depth J, U_K depth J-K).
+// The dispatcher deals linear ids round-robin over the 8 XCDs, so with P a
+// multiple of 8 every workgroup of particle p lands on XCD p mod 8 (its shared
+// B panel is fetched into one L2 only). Within an XCD the ids run in groups of
+// `grp` particles, w-major inside a group (longest tile first): grp = P/8 is
+// longest-first over the whole launch; smaller groups keep fewer particles'
+// B panels live in the 4 MB L2 at a time.
 // ----------------------------------------------------------------------------
+__device__ __forceinline__ void step_tile(int b, int P, int ntl, int grp, int& p, int& w) {
+  if ((P & 7) != 0 || grp <= 0) {  // particle fastest
+    p = b % P;
+    w = b / P;
+    return;
+  }
+  const int xcd = b & 7, s = b >> 3, pq = P >> 3;
+  const int per = grp * ntl;
+  const int gi = s / per, r = s - gi * per;
+  const int gs = min(grp, pq - gi * grp);  // the last group may be smaller
+  w = r / gs;
+  p = (gi * grp + (r - w * gs)) * 8 + xcd;
+}
+
 constexpr int STEP_SMEM = (Geo<T>::STAGE > DIAG_BASE) ? Geo<T>::STAGE : DIAG_BASE;  // ~72 KiB: two workgroups per CU
 constexpr int STEP_SMALL = 5 * T;         // z_J + reduction scratch (also the diagonal's scratch)
 static_assert(DIAG_BASE <= STEP_SMEM && DIAG_SMALL <= STEP_SMALL, "fused diagonal fits the step's LDS");
@@ -340,12 +357,12 @@ static_assert(STEP_NTH == DNTH, "the fused diagonal runs on the step workgroup")
 __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int J, int nt, int Npad, double* __restrict__ Lb,
                                                   double* __restrict__ Ub, double* __restrict__ yb,
                                                   double* __restrict__ s2p, double* __restrict__ szp,
-                                                  int* __restrict__ info) {
+                                                  int* __restrict__ info, int P, int grp) {
   __shared__ __attribute__((aligned(16))) double smem[STEP_SMEM];
   __shared__ double small[STEP_SMALL];
   const int tid = threadIdx.x;
-  const int p = blockIdx.x;
-  const int w = blockIdx.y;
+  int p, w;
+  step_tile(blockIdx.x, P, nt - 1, grp, p, w);
   const int nL = nt - 1 - J;
   const size_t ld = (size_t)Npad;
   double* Lp = Lb + (size_t)p * ld * ld;
@@ -369,13 +386,13 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
     __syncthreads();
     // L_IJ = C U_JJ^T
     acc.zero();
-    gemm_stream<T, false>(acc, Aij, Npad, Ujj, Npad, T, smem, qd);
+    gemm_stream<T, false, false, TRI_B_KLEC>(acc, Aij, Npad, Ujj, Npad, T, smem, qd);
     acc.store(qd, Aij, ld);
     if (tid < T) zj[tid] = yp[J * T + tid];
     __syncthreads();
     // look-ahead: A_II -= L_IJ L_IJ^T (the full tile; only its lower half is ever read), y_I -= L_IJ z_J
     acc.load(qd, Aii, ld);
-    gemm_stream<T, false, true>(acc, Aij, Npad, Aij, Npad, T, smem, qd);
+    gemm_stream<T, false, true, TRI_C_LOWER>(acc, Aij, Npad, Aij, Npad, T, smem, qd);
     acc.store(qd, Aii, ld);
     {
       const int r = tid & (T - 1), h = tid >> 7;  // 4 quarter-row partial dot products
@@ -400,14 +417,14 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
     Acc<T> acc;
     acc.zero();
     // W = L_J,[K,J) U_[K,J),K, parked in the U_JK slot
-    gemm_stream<T, true>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad, Up + (size_t)K * T * ld + (size_t)K * T,
-                         Npad, (J - K) * T, smem, qd);
+    gemm_stream<T, true, false, TRI_B_KGEC>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
+                                            Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T, smem, qd);
     acc.store(qd, Ujk, ld);
     if (tid < T) zj[tid] = yp[J * T + tid];
     __syncthreads();
     // U_JK = -U_JJ W (A operand staged negated)
     acc.zero();
-    gemm_stream<T, true, true>(acc, Ujj, Npad, Ujk, Npad, T, smem, qd);
+    gemm_stream<T, true, true, TRI_A_KLER>(acc, Ujj, Npad, Ujk, Npad, T, smem, qd);
     acc.store(qd, Ujk, ld);
     // column partials straight from the accumulators: sum over this wave's rows,
     // then the 4 lane groups, then the two row-halves of the tile (fixed order)
@@ -445,6 +462,28 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
       }
     }
   }
+}
+
+// ----------------------------------------------------------------------------
+// Measurement hook (gpf_gemm_bench): the L-tile GEMM of k_step in isolation.
+// Workgroup b: particle p = b % P, tile w = b / P; C_w -= L_p[rows I, :D] L_p[rows J, :D]^T
+// with I = J+1+w, J = D/T (mode 0), or every workgroup on the same operands (mode 1:
+// L2-resident, isolates the core from HBM). The tile goes to C + b*T*T.
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_gemm_bench(int mode, int D, int Npad, int P,
+                                                                                   const double* __restrict__ Lb,
+                                                                                   double* __restrict__ C) {
+  __shared__ __attribute__((aligned(16))) double smem[STEP_SMEM];
+  const int b = blockIdx.x;
+  const int p = (mode == 1) ? 0 : b % P, w = (mode == 1) ? 0 : b / P;
+  const size_t ld = (size_t)Npad;
+  const int J = D / T, I = J + 1 + w;
+  const double* Lp = Lb + (size_t)p * ld * ld;
+  const Quad<T> qd;
+  Acc<T> acc;
+  acc.zero();
+  gemm_stream<T, false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, D, smem, qd);
+  acc.store(qd, C + (size_t)b * T * T, T);
 }
 
 }  // namespace gpf

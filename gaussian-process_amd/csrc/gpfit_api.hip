@@ -28,7 +28,9 @@ using gpf::T;
 
 namespace {
 
-enum ProfClass { PC_PANEL = 0, PC_DIAG = 1, PC_BUILD = 2, PC_LOSS = 3, PC_N = 4 };
+enum ProfClass { PC_PANEL = 0, PC_DIAG = 1, PC_BUILD = 2, PC_LOSS = 3, PC_FACTOR = 4, PC_N = 5 };
+
+constexpr int MAX_GROUPS = 4;  // particle groups factorised on concurrent streams
 
 struct Pending {
   hipEvent_t a, b;
@@ -41,6 +43,8 @@ struct Pending {
 struct gpf_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t sub[MAX_GROUPS] = {};  // one stream per particle group (run_factor)
+  hipEvent_t fork = nullptr, join[MAX_GROUPS] = {};
   std::string err;
 
   // training data
@@ -108,12 +112,12 @@ static hipEvent_t take_event(gpf_ctx* c) {
 
 // Launch helper: brackets the launch with events when profiling is on.
 template <typename F>
-static int launch(gpf_ctx* c, int cls, double work, F f) {
+static int launch_on(gpf_ctx* c, hipStream_t st, int cls, double work, F f) {
   hipEvent_t a = nullptr, b = nullptr;
   if (c->prof) {
     a = take_event(c);
     b = take_event(c);
-    if (a && b) hipEventRecord(a, c->stream);
+    if (a && b) hipEventRecord(a, st);
   }
   f();
   hipError_t e = hipGetLastError();
@@ -122,10 +126,15 @@ static int launch(gpf_ctx* c, int cls, double work, F f) {
     return GPF_HIP_ERROR;
   }
   if (c->prof && a && b) {
-    hipEventRecord(b, c->stream);
+    hipEventRecord(b, st);
     c->pend.push_back({a, b, cls, work});
   }
   return GPF_OK;
+}
+
+template <typename F>
+static int launch(gpf_ctx* c, int cls, double work, F f) {
+  return launch_on(c, c->stream, cls, work, f);
 }
 
 static void harvest(gpf_ctx* c) {
@@ -189,41 +198,108 @@ static int ensure_work(gpf_ctx* c, int want) {
   return GPF_OK;
 }
 
-// Factorise `pc` particles whose length scales are already in d_ls:
-// K build (lower 64x64 tiles), the first diagonal block (k_diag), then one
-// k_step per 128-wide block column (each also factors the next diagonal block).
+// Particle groups factorised on concurrent streams (GPF_GROUPS, default 1): meant to
+// fill the tail of each dependent block-column launch with another group's tiles.
+// Measured on MI355X (profiles/r1/groups_ab.txt): 2 groups +3% at N=4096 P=64 but
+// -19% at N=1024 P=32, 4 groups worse everywhere, so one group is the default.
+static int num_groups(int pc) {
+  int g = 1;
+  if (const char* s = getenv("GPF_GROUPS")) g = atoi(s);
+  g = std::max(1, std::min(g, MAX_GROUPS));
+  while (g > 1 && pc / g < 8) --g;  // keep >= 8 particles (one per XCD) per group
+  return g;
+}
+
+// Particles per XCD dispatch group of k_step (see gpf::step_tile); GPF_STEP_GROUP
+// overrides, 0 = particle fastest over the whole launch.
+static int step_group(int pc) {
+  int g = 0;
+  if (const char* s = getenv("GPF_STEP_GROUP")) g = atoi(s);
+  return std::max(0, std::min(g, pc / 8));
+}
+
+// Factorise `pc` particles whose length scales are already in d_ls, in particle
+// groups on their own streams: per group the K build (lower 64x64 tiles), the first
+// diagonal block (k_diag), then one k_step per 128-wide block column (each also
+// factors the next diagonal block). Joins back into c->stream.
 static int run_factor(gpf_ctx* c, int pc) {
   const int nt = c->nt, Np = (int)c->Npad, N = (int)c->N;
   const double Tf = (double)T, t3 = Tf * Tf * Tf;
   const int nb = Np / BT;
   const int ntri = nb * (nb + 1) / 2;
-  int rc = launch(c, PC_BUILD, 8.0 * ntri * BT * BT * (double)pc, [&] {
-    hipLaunchKernelGGL(gpf::k_build_cov, dim3(ntri, pc), dim3(NTHR), 0, c->stream, N, Np, c->d, c->d_x, c->d_y,
-                       c->d_e, c->d_ls, c->d_L, c->d_yb);
-  });
-  if (rc) return rc;
-  // potrf + trtri of the first 128 block: 2/3 T^3 (later blocks are fused into k_step)
-  rc = launch(c, PC_DIAG, (2.0 / 3.0) * t3 * pc, [&] {
-    hipLaunchKernelGGL(gpf::k_diag, dim3(pc), dim3(gpf::DNTH), 0, c->stream, 0, nt, Np, c->d_L, c->d_U, c->d_yb,
-                       c->d_s2p, c->d_szp, c->d_info);
-  });
-  if (rc) return rc;
-  for (int J = 0; nt > 1 && J < nt; ++J) {
-    // algorithmic flops on the potrf + trtri (2/3 N^3) formulation:
-    //   L tile: depth-128J GEMM 2 T^3 J + triangular multiply T^3 + look-ahead syrk share T^3
-    //   U tile: depth-128(J-K) GEMM with a triangular factor 2 T^3 (J-K) - T^3 + triangular multiply T^3
-    //   fused diagonal block J+1: 2/3 T^3
+  const size_t ld = (size_t)Np;
+  const int ng = num_groups(pc);
+  // algorithmic flops of block-column launch J per particle, potrf + trtri (2/3 N^3) formulation:
+  //   L tile: depth-128J GEMM 2 T^3 J + triangular multiply T^3 + look-ahead syrk share T^3
+  //   U tile: depth-128(J-K) GEMM with a triangular factor 2 T^3 (J-K) - T^3 + triangular multiply T^3
+  //   fused diagonal block J+1: 2/3 T^3
+  auto step_flops = [&](int J) {
     double fl = 0.0;
     for (int w = 0; w < nt - 1; ++w) {
       if (w < nt - 1 - J) fl += 2.0 * t3 * J + 2.0 * t3;
       else fl += 2.0 * t3 * (J - (w - (nt - 1 - J)));
     }
     if (J + 1 < nt) fl += (2.0 / 3.0) * t3;
-    rc = launch(c, PC_PANEL, fl * pc, [&] {
-      hipLaunchKernelGGL(gpf::k_step, dim3(pc, nt - 1), dim3(gpf::STEP_NTH), 0, c->stream, J, nt, Np, c->d_L,
-                         c->d_U, c->d_yb, c->d_s2p, c->d_szp, c->d_info);
+    return fl;
+  };
+  hipEvent_t wa = nullptr, wb = nullptr;
+  if (c->prof) {
+    wa = take_event(c);
+    wb = take_event(c);
+    if (wa && wb) hipEventRecord(wa, c->stream);
+  }
+  if (ng > 1) {
+    GPF_HIP(c, hipEventRecord(c->fork, c->stream));
+    for (int g = 0; g < ng; ++g) GPF_HIP(c, hipStreamWaitEvent(c->sub[g], c->fork, 0));
+  }
+  double total = 0.0;
+  for (int g = 0; g < ng; ++g) {
+    const int p0 = (int)((long long)pc * g / ng), gc = (int)((long long)pc * (g + 1) / ng) - p0;
+    hipStream_t st = (ng > 1) ? c->sub[g] : c->stream;
+    double* Lg = c->d_L + (size_t)p0 * ld * ld;
+    double* Ug = c->d_U + (size_t)p0 * ld * ld;
+    double* yg = c->d_yb + (size_t)p0 * ld;
+    double* s2g = c->d_s2p + (size_t)p0 * nt * ld;
+    double* szg = c->d_szp + (size_t)p0 * nt * ld;
+    int* ig = c->d_info + p0;
+    const double* lsg = c->d_ls + (size_t)p0 * c->d;
+    int rc = launch_on(c, st, PC_BUILD, 8.0 * ntri * BT * BT * (double)gc, [&] {
+      hipLaunchKernelGGL(gpf::k_build_cov, dim3(ntri, gc), dim3(NTHR), 0, st, N, Np, c->d, c->d_x, c->d_y, c->d_e,
+                         lsg, Lg, yg);
     });
     if (rc) return rc;
+    // potrf + trtri of the first 128 block: 2/3 T^3 (later blocks are fused into k_step)
+    rc = launch_on(c, st, PC_DIAG, (2.0 / 3.0) * t3 * gc, [&] {
+      hipLaunchKernelGGL(gpf::k_diag, dim3(gc), dim3(gpf::DNTH), 0, st, 0, nt, Np, Lg, Ug, yg, s2g, szg, ig);
+    });
+    if (rc) return rc;
+    total += (2.0 / 3.0) * t3 * gc;
+  }
+  // block columns interleaved across groups so every stream has work queued early
+  for (int J = 0; nt > 1 && J < nt; ++J) {
+    const double fl = step_flops(J);
+    for (int g = 0; g < ng; ++g) {
+      const int p0 = (int)((long long)pc * g / ng), gc = (int)((long long)pc * (g + 1) / ng) - p0;
+      hipStream_t st = (ng > 1) ? c->sub[g] : c->stream;
+      const int rc = launch_on(c, st, PC_PANEL, fl * gc, [&] {
+        hipLaunchKernelGGL(gpf::k_step, dim3(gc * (nt - 1)), dim3(gpf::STEP_NTH), 0, st, J, nt, Np,
+                           c->d_L + (size_t)p0 * ld * ld, c->d_U + (size_t)p0 * ld * ld, c->d_yb + (size_t)p0 * ld,
+                           c->d_s2p + (size_t)p0 * nt * ld, c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc,
+                           step_group(gc));
+      });
+      if (rc) return rc;
+      total += fl * gc;
+    }
+  }
+  if (ng > 1) {
+    for (int g = 0; g < ng; ++g) {
+      GPF_HIP(c, hipEventRecord(c->join[g], c->sub[g]));
+      GPF_HIP(c, hipStreamWaitEvent(c->stream, c->join[g], 0));
+    }
+  }
+  if (c->prof && wa && wb) {
+    hipEventRecord(wb, c->stream);
+    c->pend.push_back({wa, wb, PC_FACTOR, total});
   }
   return GPF_OK;
 }
@@ -242,8 +318,13 @@ int gpf_open(int device, gpf_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return GPF_HIP_ERROR;
   gpf_ctx* c = new gpf_ctx();
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete c;
+  bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
+  for (int g = 0; ok && g < MAX_GROUPS; ++g)
+    ok = hipStreamCreateWithFlags(&c->sub[g], hipStreamNonBlocking) == hipSuccess &&
+         hipEventCreateWithFlags(&c->join[g], hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    gpf_close(c);
     return GPF_HIP_ERROR;
   }
   *out = c;
@@ -259,7 +340,12 @@ void gpf_close(gpf_ctx* c) {
   hipFree(c->d_x); hipFree(c->d_y); hipFree(c->d_e);
   hipFree(c->d_sig); hipFree(c->d_exp); hipFree(c->d_lo); hipFree(c->d_hi);
   for (auto e : c->pool) hipEventDestroy(e);
-  hipStreamDestroy(c->stream);
+  for (int g = 0; g < MAX_GROUPS; ++g) {
+    if (c->sub[g]) hipStreamDestroy(c->sub[g]);
+    if (c->join[g]) hipEventDestroy(c->join[g]);
+  }
+  if (c->fork) hipEventDestroy(c->fork);
+  if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
 
@@ -551,10 +637,11 @@ int gpf_get_profile(gpf_ctx* c, double* out, int n) {
   if (!c || !out) return 0;
   hipStreamSynchronize(c->stream);
   harvest(c);
-  double v[12] = {c->acc[PC_PANEL][0], c->acc[PC_PANEL][1], c->acc[PC_PANEL][2], c->acc[PC_DIAG][0],
-                  c->acc[PC_DIAG][1],  c->acc[PC_DIAG][2],  c->acc[PC_BUILD][0], c->acc[PC_BUILD][1],
-                  c->acc[PC_BUILD][2], c->acc[PC_LOSS][0],  c->acc[PC_LOSS][1],  c->evals};
-  const int m = std::min(n, 12);
+  double v[15] = {c->acc[PC_PANEL][0],  c->acc[PC_PANEL][1],  c->acc[PC_PANEL][2], c->acc[PC_DIAG][0],
+                  c->acc[PC_DIAG][1],   c->acc[PC_DIAG][2],   c->acc[PC_BUILD][0], c->acc[PC_BUILD][1],
+                  c->acc[PC_BUILD][2],  c->acc[PC_LOSS][0],   c->acc[PC_LOSS][1],  c->evals,
+                  c->acc[PC_FACTOR][0], c->acc[PC_FACTOR][1], c->acc[PC_FACTOR][2]};
+  const int m = std::min(n, 15);
   for (int i = 0; i < m; ++i) out[i] = v[i];
   return m;
 }
@@ -611,6 +698,37 @@ int gpf_mfma_peak(gpf_ctx* c, int blocks, int iters, double* tflops) {
   hipEventDestroy(a);
   hipEventDestroy(b);
   hipFree(out);
+  return GPF_OK;
+}
+
+// Measurement hook: TF/s of the k_step L-tile GEMM core alone (k_gemm_bench) on
+// P random Npad x Npad matrices, tiles = workgroups per particle, depth D.
+int gpf_gemm_bench(gpf_ctx* c, int mode, int Npad, int P, int tiles, int D, int iters, double* tflops) {
+  if (!c || !tflops || Npad % T || D % T || P <= 0 || tiles <= 0 || iters <= 0) return GPF_BAD_ARG;
+  if ((D / T + 1 + tiles) * T > Npad) return bad_arg(c, "gpf_gemm_bench: tiles do not fit");
+  hipSetDevice(c->device);
+  double *L = nullptr, *C = nullptr;
+  const size_t n = (size_t)P * Npad * Npad;
+  GPF_HIP(c, hipMalloc(&L, n * 8));
+  GPF_HIP(c, hipMalloc(&C, (size_t)P * tiles * T * T * 8));
+  GPF_HIP(c, hipMemsetAsync(L, 0, n * 8, c->stream));
+  hipEvent_t a, b;
+  GPF_HIP(c, hipEventCreate(&a));
+  GPF_HIP(c, hipEventCreate(&b));
+  const int W = P * tiles;
+  hipLaunchKernelGGL(gpf::k_gemm_bench, dim3(W), dim3(gpf::STEP_NTH), 0, c->stream, mode, D, Npad, P, L, C);
+  GPF_HIP(c, hipEventRecord(a, c->stream));
+  for (int i = 0; i < iters; ++i)
+    hipLaunchKernelGGL(gpf::k_gemm_bench, dim3(W), dim3(gpf::STEP_NTH), 0, c->stream, mode, D, Npad, P, L, C);
+  GPF_HIP(c, hipEventRecord(b, c->stream));
+  GPF_HIP(c, hipEventSynchronize(b));
+  float ms = 0.f;
+  GPF_HIP(c, hipEventElapsedTime(&ms, a, b));
+  *tflops = 2.0 * T * T * (double)D * W * iters / (ms * 1e-3) / 1e12;
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  hipFree(L);
+  hipFree(C);
   return GPF_OK;
 }
 

@@ -41,6 +41,8 @@ SIGNATURES = {
     "gpf_selftest_mfma": (ctypes.c_int, [_vp, _dp, _dp, _dp]),
     "gpf_debug_factor": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _dp]),
     "gpf_mfma_peak": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _dp]),
+    "gpf_gemm_bench": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_int, _dp]),
 }
 
 _LIB = None
@@ -190,10 +192,11 @@ class Context:
         self._check(self.lib.gpf_reset_profile(self._h), "gpf_reset_profile")
 
     def profile(self):
-        buf = np.zeros(12)
-        self.lib.gpf_get_profile(self._h, _ptr(buf), 12)
+        buf = np.zeros(15)
+        self.lib.gpf_get_profile(self._h, _ptr(buf), 15)
         keys = ["panel_ms", "panel_launches", "panel_flops", "diag_ms", "diag_launches", "diag_flops",
-                "build_ms", "build_launches", "build_bytes", "loss_ms", "loss_launches", "evals"]
+                "build_ms", "build_launches", "build_bytes", "loss_ms", "loss_launches", "evals",
+                "factor_wall_ms", "factor_calls", "factor_flops"]
         return dict(zip(keys, buf.tolist()))
 
     def debug_factor(self, lengths):
@@ -211,6 +214,13 @@ class Context:
     def mfma_peak(self, blocks=1024, iters=4096):
         out = ctypes.c_double(0.0)
         self._check(self.lib.gpf_mfma_peak(self._h, int(blocks), int(iters), ctypes.byref(out)), "gpf_mfma_peak")
+        return out.value
+
+    def gemm_bench(self, mode=0, npad=4096, particles=64, tiles=15, depth=2048, iters=5):
+        """TF/s of the block-column GEMM core alone (gpf_gemm_bench)."""
+        out = ctypes.c_double(0.0)
+        self._check(self.lib.gpf_gemm_bench(self._h, int(mode), int(npad), int(particles), int(tiles), int(depth),
+                                            int(iters), ctypes.byref(out)), "gpf_gemm_bench")
         return out.value
 
     def selftest_mfma(self, a, b):

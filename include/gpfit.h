@@ -102,6 +102,8 @@ int gpf_set_profiling(gpf_ctx* ctx, int on);
  *  [3] diag kernel ms    [4] diag launches   [5] diag algorithmic flops
  *  [6] K-build ms        [7] K-build launches[8] K-build algorithmic bytes
  *  [9] loss kernel ms    [10] loss launches  [11] evals (non-sentinel)
+ *  [12] factorisation wall ms (K build + diag + steps of all particle groups, which run
+ *       on concurrent streams, so [0]/[3]/[6] may overlap)  [13] calls  [14] its flops
  * Returns the number of values written. */
 int gpf_get_profile(gpf_ctx* ctx, double* out, int n);
 int gpf_reset_profile(gpf_ctx* ctx);
@@ -122,6 +124,11 @@ int gpf_debug_factor(gpf_ctx* ctx, const double* ls, double* L, double* U, doubl
 /* Diagnostic: measured FP64 MFMA throughput (TFLOP/s) of a register-only
  * v_mfma_f64_16x16x4_f64 loop over `blocks` workgroups of 4 waves. */
 int gpf_mfma_peak(gpf_ctx* ctx, int blocks, int iters, double* tflops);
+
+/* Measurement hook: TF/s of the block-column GEMM core alone (no factorisation):
+ * P particles' Npad x Npad matrices, `tiles` workgroups per particle, depth D, `iters`
+ * timed launches; mode 0 = per-particle operands, mode 1 = one shared (L2-resident) pair. */
+int gpf_gemm_bench(gpf_ctx* ctx, int mode, int Npad, int P, int tiles, int D, int iters, double* tflops);
 
 #ifdef __cplusplus
 }

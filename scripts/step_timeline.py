@@ -1,0 +1,51 @@
+"""Per-block-column k_step durations from a rocprofv3 kernel-trace CSV.
+
+usage: python scripts/step_timeline.py <kernel_trace.csv> N
+Prints, per J, the mean launch time and the algorithmic TF/s of the launch
+(same flop formula as run_factor), and the gaps between consecutive launches."""
+import csv
+import sys
+from collections import defaultdict
+
+f, N = sys.argv[1], int(sys.argv[2])
+T = 128
+nt = -(-N // T)
+rows = [r for r in csv.DictReader(open(f)) if "k_step" in r["Kernel_Name"] or "k_diag" in r["Kernel_Name"]
+        or "k_build_cov" in r["Kernel_Name"] or "k_points" in r["Kernel_Name"]]
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+t3 = T ** 3
+
+
+def flops(J):
+    fl = 0.0
+    for w in range(nt - 1):
+        fl += (2 * t3 * J + 2 * t3) if w < nt - 1 - J else 2 * t3 * (J - (w - (nt - 1 - J)))
+    return fl + (2 / 3 * t3 if J + 1 < nt else 0)
+
+
+dur, gap = defaultdict(list), defaultdict(list)
+P = None
+J = 0
+prev_end = None
+for r in rows:
+    s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    name = r["Kernel_Name"]
+    if "k_build_cov" in name:
+        J = 0
+    if "k_step" in name:
+        P = int(r["Grid_Size_X"]) // (int(r["Workgroup_Size_X"]) * (nt - 1)) if int(r["Grid_Size_Y"]) == 1 \
+            else int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"])
+        dur[J].append((e - s) * 1e-6)
+        if prev_end is not None:
+            gap[J].append((s - prev_end) * 1e-6)
+        J += 1
+    prev_end = e
+tot_ms = tot_fl = 0.0
+for j in sorted(dur):
+    ms = sum(dur[j]) / len(dur[j])
+    g = sum(gap[j]) / max(1, len(gap[j]))
+    fl = flops(j) * P
+    tot_ms += ms
+    tot_fl += fl
+    print(f"J={j:3d}  {ms:8.3f} ms  {fl / ms / 1e9:6.1f} TF/s  gap {g * 1e3:6.1f} us")
+print(f"P={P} total {tot_ms:.2f} ms  {tot_fl / tot_ms / 1e9:.1f} TF/s")
