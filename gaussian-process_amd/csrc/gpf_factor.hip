@@ -46,27 +46,39 @@ __device__ unsigned long long g_diag_stamps[32];
 // factorisation workgroups (k_diag and, fused, k_step).
 
 // ----------------------------------------------------------------------------
-// Unblocked 64x64 Cholesky with the inverse riding along ([A | I] -> [L | L^-1]).
-// Thread (r = tid>>3, g = tid&7) keeps row r, columns s = g + 8m, of both the
-// trailing A and X in registers (8 + 8 doubles). Whoever updates element
-// (r, c+1) also publishes it to `nxt[r]`, so column c+1 (and its pivot
-// nxt[c+1]) is read from LDS, never picked out of the register row by a runtime
-// index (which would go to scratch). Finished columns of L are written to sA as
-// they are produced. The update is branch-free (masked multipliers), one
-// reciprocal per column, two barriers per column; the column loop stays rolled
-// (small code, I-cache resident).
+// 64x64 Cholesky with the inverse riding along ([A | I] -> [L | L^-1]), in
+// panels of 4 columns: 2 barriers per panel instead of 2 per column.
+// Thread (r = tid>>3, g = tid&7) keeps row r, columns s = g + 8m, of the
+// trailing A and of X in registers (8 + 8 doubles). Per panel cb:
+//   panel (wave 0 alone, lane = row for A, lane = column for X, no barrier):
+//     pin[l][q] holds A[l][cb+q] (l >= cb) or X[cb+q][l] (l < cb); the 4 columns
+//     are factored with pivots/multipliers broadcast by readlane, and the 4 X
+//     rows finished (their diagonal block is still the identity). Output
+//     pout[l][q] = L[l][cb+q] (l > cb+3) or X[cb+q][l] (l <= cb+3); L -> sA.
+//   update (all waves): a[r][s] -= L[r][cb+q] L[s][cb+q]  (s > cb+3, s <= r)
+//                       x[r][s] -= L[r][cb+q] X[cb+q][s]  (s <= cb+3 < r)
+//     one q at a time in ascending order, then the next panel goes to pin.
+// Every element sees exactly the operations of the column-by-column
+// elimination, in the same order (mul, then sub: -ffp-contract=off), so the
+// result is bitwise that of an unblocked right-looking Cholesky.
 //   in : sA[r*la + s] lower triangle of the tile
-//   out: sA = L (zeros above the diagonal), sX = L^-1; returns true if a pivot
-//        was not > 0 (numpy: LinAlgError, GP_func.py:22)
-// xbuf: >= 192 doubles of LDS scratch.
+//   out: sA = L (zeros above the diagonal), sX = L^-1; returns true (in thread 0)
+//        if a pivot was not > 0 (numpy: LinAlgError, GP_func.py:22)
+// buf: >= 512 doubles of LDS scratch.
 // ----------------------------------------------------------------------------
-__device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx, double* xbuf) {
-  constexpr int G = DNTH / 64, NM = 64 / G;  // 8 column groups, 8 columns per lane
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const long long i = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)i, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(i >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx, double* buf) {
+  constexpr int G = DNTH / 64, NM = 64 / G, PW = 4;  // 8 column groups, 8 columns per lane, panel width
   const int tid = threadIdx.x;
   const int r = tid / G, g = tid % G;
-  double* colbuf = xbuf;       // column c of L
-  double* rowbuf = xbuf + 64;  // row c of L^-1
-  double* nxt = xbuf + 128;    // column c+1 of the reduced A (its pivot included)
+  double* pin = buf;             // [64][4] panel input
+  double* pout = buf + 64 * PW;  // [64][4] panel output
   double a[NM], x[NM];
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
@@ -74,42 +86,90 @@ __device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx,
     a[m] = (s <= r) ? sA[r * la + s] : 0.0;
     x[m] = (s == r) ? 1.0 : 0.0;
   }
-  if (g == 0) {
-    nxt[r] = a[0];  // column 0
-    colbuf[r] = 0.0;
-    rowbuf[r] = 0.0;
+  // panel 0 input: A[r][0..3] (X rows 0..3 have no columns left of the panel)
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    const int s = g + G * m;
+    if (s < PW) pin[r * PW + s] = a[m];
   }
   bool bad = false;
+  const bool panel_wave = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;  // wave 0 (scalar branch)
 #pragma unroll 1
-  for (int c = 0; c < 64; ++c) {
+  for (int cb = 0; cb < 64; cb += PW) {
+    if (cb == 16) DIAG_STAMP(10);
     __syncthreads();
-    const double p = nxt[c];
-    bad = bad || !(p > 0.0);
-    const double dg = sqrt(p);
-    const double inv = 1.0 / dg;
-    if (g == 0 && r >= c) {
-      const double l = (r > c) ? nxt[r] * inv : dg;
-      colbuf[r] = l;
-      sA[r * la + c] = l;
-    }
-    if (r == c) {
+    if (cb == 16) DIAG_STAMP(11);
+    if (panel_wave) {
+      const int l = tid;
+      const d2 p01 = *reinterpret_cast<const d2*>(pin + l * PW);
+      const d2 p23 = *reinterpret_cast<const d2*>(pin + l * PW + 2);
+      double v[PW] = {p01.x, p01.y, p23.x, p23.y};  // A[l][cb+q] for l >= cb
+      double w[PW];                                  // X[cb+q][l] for l <= cb+3
 #pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        if (g + G * m <= c) x[m] = x[m] * inv;
-        rowbuf[g + G * m] = x[m];
+      for (int q = 0; q < PW; ++q) w[q] = (l < cb) ? v[q] : ((l == cb + q) ? 1.0 : 0.0);
+#pragma unroll
+      for (int q = 0; q < PW; ++q) {
+        const double p = readlane_f64(v[q], cb + q);
+        bad = bad | !(p > 0.0);
+        const double dg = sqrt(p);
+        const double inv = 1.0 / dg;
+        const double lq = (l > cb + q) ? v[q] * inv : dg;  // L[l][cb+q] (rows below cb+q matter)
+        v[q] = lq;
+        w[q] = w[q] * inv;
+#pragma unroll
+        for (int q2 = q + 1; q2 < PW; ++q2) {
+          const double ls = readlane_f64(lq, cb + q2);  // L[cb+q2][cb+q]
+          v[q2] = v[q2] - lq * ls;
+          w[q2] = w[q2] - ls * w[q];
+        }
+      }
+      if (l >= cb) {
+#pragma unroll
+        for (int q = 0; q < PW; ++q) sA[l * la + cb + q] = v[q];
+      }
+      const bool below = l > cb + PW - 1;
+      *reinterpret_cast<d2*>(pout + l * PW) = below ? d2{v[0], v[1]} : d2{w[0], w[1]};
+      *reinterpret_cast<d2*>(pout + l * PW + 2) = below ? d2{v[2], v[3]} : d2{w[2], w[3]};
+    }
+    if (cb == 16) DIAG_STAMP(12);
+    __syncthreads();
+    if (cb == 16) DIAG_STAMP(13);
+    const int ce = cb + PW;  // first column right of the panel
+    double lr[PW];
+    {
+      const d2 t01 = *reinterpret_cast<const d2*>(pout + r * PW);
+      const d2 t23 = *reinterpret_cast<const d2*>(pout + r * PW + 2);
+      lr[0] = t01.x; lr[1] = t01.y; lr[2] = t23.x; lr[3] = t23.y;  // L[r][cb+q] if r >= ce, else X[cb+q][r]
+    }
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      const int s = g + G * m;
+      const d2 o01 = *reinterpret_cast<const d2*>(pout + s * PW);
+      const d2 o23 = *reinterpret_cast<const d2*>(pout + s * PW + 2);
+      const double o[PW] = {o01.x, o01.y, o23.x, o23.y};
+      const bool right = s >= ce;
+      double t = right ? a[m] : x[m];
+#pragma unroll
+      for (int q = 0; q < PW; ++q) t = t - lr[q] * o[q];
+      if (r >= ce) {
+        if (right) {
+          if (s <= r) a[m] = t;
+        } else {
+          x[m] = t;
+        }
+      } else if (r >= cb && !right) {  // a panel row of X: take the finished values
+        const int q = r - cb;
+        x[m] = (q == 0) ? o[0] : (q == 1) ? o[1] : (q == 2) ? o[2] : o[3];
       }
     }
-    __syncthreads();
-    if (r > c) {
-      const double l = colbuf[r];
+    if (cb == 16) DIAG_STAMP(14);
+    // next panel's input
+    if (ce < 64) {
 #pragma unroll
       for (int m = 0; m < NM; ++m) {
         const int s = g + G * m;
-        const double la_ = (s > c && s <= r) ? l : 0.0;  // trailing update of A
-        const double lx_ = (s <= c) ? l : 0.0;           // elimination of X
-        a[m] = a[m] - la_ * colbuf[s];
-        x[m] = x[m] - lx_ * rowbuf[s];
-        if (s == c + 1) nxt[r] = a[m];
+        if (r >= ce && s >= ce && s < ce + PW) pin[r * PW + (s - ce)] = a[m];
+        if (r >= ce && r < ce + PW && s < ce) pin[s * PW + (r - ce)] = x[m];
       }
     }
   }
@@ -171,7 +231,6 @@ __device__ __forceinline__ void cols_partial64(double* s2, double* sz, const dou
 struct DiagSmem {
   double* t0;       // 64 x LDH
   double* t1;       // 64 x LDH
-  double* xbuf;     // 192
   double* y;        // 128
   double* z;        // 128
   double* ps2;      // 128
@@ -204,7 +263,7 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
     sm.psz[tid] = 0.0;
   }
   __syncthreads();
-  bool bad = factor64(t0, LDH, t1, LDH, sm.xbuf);
+  bool bad = factor64(t0, LDH, t1, LDH, sm.scratch);
   __syncthreads();
   DIAG_STAMP(1);
   lds_to_tile64(Lt, ld, t0, LDH, true);
@@ -245,7 +304,7 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
 
   DIAG_STAMP(4);
   // (d) L22, U22
-  bad = factor64(t0, LDH, t1, LDH, sm.xbuf) || bad;
+  bad = factor64(t0, LDH, t1, LDH, sm.scratch) | bad;
   __syncthreads();
   DIAG_STAMP(5);
   lds_to_tile64(Lt + (size_t)H * ld + H, ld, t0, LDH, true);
@@ -284,14 +343,13 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
 // Shared-memory carve-up for the diagonal factor: two 64x64 tiles and the small
 // vectors live in `base` (the GEMM staging area, DIAG_BASE doubles), the
 // 512-double reduction scratch in `small`.
-constexpr int DIAG_BASE = 2 * H * LDH + 192 + 4 * T;
+constexpr int DIAG_BASE = 2 * H * LDH + 4 * T;
 constexpr int DIAG_SMALL = 512;
 __device__ __forceinline__ DiagSmem carve_diag(double* base, double* small) {
   DiagSmem s;
   s.t0 = base;
   s.t1 = base + H * LDH;
-  s.xbuf = base + 2 * H * LDH;
-  s.y = s.xbuf + 192;
+  s.y = base + 2 * H * LDH;
   s.z = s.y + T;
   s.ps2 = s.z + T;
   s.psz = s.ps2 + T;
@@ -308,7 +366,7 @@ __global__ __launch_bounds__(DNTH) void k_diag(int J, int nt, int Npad, double* 
                                                   double* __restrict__ s2p, double* __restrict__ szp,
                                                   int* __restrict__ info) {
   __shared__ __attribute__((aligned(16))) double tiles[DIAG_BASE];
-  __shared__ double small[DIAG_SMALL];
+  __shared__ __attribute__((aligned(16))) double small[DIAG_SMALL];
   const int p = blockIdx.x;
   const size_t ld = (size_t)Npad;
   const size_t off = (size_t)p * ld * ld + (size_t)J * T * ld + (size_t)J * T;
@@ -359,7 +417,7 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
                                                   double* __restrict__ s2p, double* __restrict__ szp,
                                                   int* __restrict__ info, int P, int grp) {
   __shared__ __attribute__((aligned(16))) double smem[STEP_SMEM];
-  __shared__ double small[STEP_SMALL];
+  __shared__ __attribute__((aligned(16))) double small[STEP_SMALL];
   const int tid = threadIdx.x;
   int p, w;
   step_tile(blockIdx.x, P, nt - 1, grp, p, w);
@@ -461,6 +519,27 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
         szp[poff + c] = acc.v[0][ni][1] + half[T + c];
       }
     }
+  }
+}
+
+// Debug hook (gpf_debug_factor64): factor64 on two host-given 64x64 matrices in a row
+// (in: 2 x 64 x 64 row-major; out: L then X for each).
+__global__ __launch_bounds__(DNTH) void k_debug_factor64(const double* __restrict__ in, double* __restrict__ out,
+                                                         int* __restrict__ bad) {
+  __shared__ __attribute__((aligned(16))) double t[2 * H * LDH];
+  __shared__ __attribute__((aligned(16))) double scratch[512];
+  const int tid = threadIdx.x;
+  for (int k = 0; k < 2; ++k) {
+    for (int i = tid; i < H * H; i += DNTH) t[(i / H) * LDH + i % H] = in[k * H * H + i];
+    __syncthreads();
+    const bool b = factor64(t, LDH, t + H * LDH, LDH, scratch);
+    __syncthreads();
+    for (int i = tid; i < H * H; i += DNTH) {
+      out[(2 * k) * H * H + i] = t[(i / H) * LDH + i % H];
+      out[(2 * k + 1) * H * H + i] = t[H * LDH + (i / H) * LDH + i % H];
+    }
+    if (tid == 0) bad[k] = b;
+    __syncthreads();
   }
 }
 

@@ -675,7 +675,7 @@ int gpf_debug_factor(gpf_ctx* c, const double* ls, double* L, double* U, double*
   GPF_HIP(c, hipMemcpy(L, c->d_L, np * np * 8, hipMemcpyDeviceToHost));
   GPF_HIP(c, hipMemcpy(U, c->d_U, np * np * 8, hipMemcpyDeviceToHost));
   GPF_HIP(c, hipMemcpy(z, c->d_yb, np * 8, hipMemcpyDeviceToHost));
-  GPF_HIP(c, hipMemcpy(alpha, al, (size_t)c->N * 8, hipMemcpyDeviceToHost));
+  if (al) GPF_HIP(c, hipMemcpy(alpha, al, (size_t)c->N * 8, hipMemcpyDeviceToHost));
   return rc;
 }
 
@@ -729,6 +729,25 @@ int gpf_gemm_bench(gpf_ctx* c, int mode, int Npad, int P, int tiles, int D, int 
   hipEventDestroy(b);
   hipFree(L);
   hipFree(C);
+  return GPF_OK;
+}
+
+// Debug hook: the unblocked-panel 64x64 factor on two matrices (2*4096 in, 4*4096 out).
+int gpf_debug_factor64(gpf_ctx* c, const double* in, double* out, int* bad) {
+  if (!c || !in || !out || !bad) return GPF_BAD_ARG;
+  hipSetDevice(c->device);
+  double *di = nullptr, *dout = nullptr;
+  int* db = nullptr;
+  GPF_HIP(c, hipMalloc(&di, 2 * 4096 * 8));
+  GPF_HIP(c, hipMalloc(&dout, 4 * 4096 * 8));
+  GPF_HIP(c, hipMalloc(&db, 2 * 4));
+  GPF_HIP(c, hipMemcpy(di, in, 2 * 4096 * 8, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(gpf::k_debug_factor64, dim3(1), dim3(gpf::DNTH), 0, c->stream, di, dout, db);
+  GPF_HIP(c, hipGetLastError());
+  GPF_HIP(c, hipStreamSynchronize(c->stream));
+  GPF_HIP(c, hipMemcpy(out, dout, 4 * 4096 * 8, hipMemcpyDeviceToHost));
+  GPF_HIP(c, hipMemcpy(bad, db, 2 * 4, hipMemcpyDeviceToHost));
+  hipFree(di); hipFree(dout); hipFree(db);
   return GPF_OK;
 }
 
