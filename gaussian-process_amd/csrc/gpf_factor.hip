@@ -47,24 +47,27 @@ __device__ unsigned long long g_diag_stamps[32];
 
 // ----------------------------------------------------------------------------
 // 64x64 Cholesky with the inverse riding along ([A | I] -> [L | L^-1]), in
-// panels of 4 columns: 2 barriers per panel instead of 2 per column.
+// panels of 4 columns with a one-panel look-ahead: one barrier per panel.
 // Thread (r = tid>>3, g = tid&7) keeps row r, columns s = g + 8m, of the
-// trailing A and of X in registers (8 + 8 doubles). Per panel cb:
-//   panel (wave 0 alone, lane = row for A, lane = column for X, no barrier):
-//     pin[l][q] holds A[l][cb+q] (l >= cb) or X[cb+q][l] (l < cb); the 4 columns
-//     are factored with pivots/multipliers broadcast by readlane, and the 4 X
-//     rows finished (their diagonal block is still the identity). Output
-//     pout[l][q] = L[l][cb+q] (l > cb+3) or X[cb+q][l] (l <= cb+3); L -> sA.
-//   update (all waves): a[r][s] -= L[r][cb+q] L[s][cb+q]  (s > cb+3, s <= r)
-//                       x[r][s] -= L[r][cb+q] X[cb+q][s]  (s <= cb+3 < r)
-//     one q at a time in ascending order, then the next panel goes to pin.
+// trailing A and of X in registers (8 + 8 doubles). Iteration k (panel
+// cb = 4k, its factor already in pout[k&1]):
+//   waves 1..7 (and wave 0 while it still owns live rows): apply panel k
+//     a[r][s] -= L[r][cb+q] L[s][cb+q]  (s > cb+3, s <= r)
+//     x[r][s] -= L[r][cb+q] X[cb+q][s]  (s <= cb+3 < r)
+//   one q at a time in ascending order, take finished X rows of panel k, and
+//   hand strip k+2 (A columns cb+8.., X rows cb+8..) to the panel wave;
+//   wave 0 (lane = row for A, lane = column for X, no barrier): take strip k+1
+//   (through panel k-1), apply panel k to it from its own registers (multipliers
+//   by readlane), factor it (pivot, sqrt, reciprocal per column) and finish its
+//   4 X rows (their diagonal block is still the identity); L -> sA,
+//   pout[(k+1)&1][l][q] = L[l][cb'+q] (l > cb'+3) or X[cb'+q][l] (l <= cb'+3).
 // Every element sees exactly the operations of the column-by-column
 // elimination, in the same order (mul, then sub: -ffp-contract=off), so the
 // result is bitwise that of an unblocked right-looking Cholesky.
 //   in : sA[r*la + s] lower triangle of the tile
 //   out: sA = L (zeros above the diagonal), sX = L^-1; returns true (in thread 0)
 //        if a pivot was not > 0 (numpy: LinAlgError, GP_func.py:22)
-// buf: >= 512 doubles of LDS scratch.
+// buf: >= 1024 doubles of LDS scratch.
 // ----------------------------------------------------------------------------
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const long long i = __double_as_longlong(v);
@@ -73,112 +76,206 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-__device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx, double* buf) {
-  constexpr int G = DNTH / 64, NM = 64 / G, PW = 4;  // 8 column groups, 8 columns per lane, panel width
-  const int tid = threadIdx.x;
-  const int r = tid / G, g = tid % G;
-  double* pin = buf;             // [64][4] panel input
-  double* pout = buf + 64 * PW;  // [64][4] panel output
-  double a[NM], x[NM];
+constexpr int F64_PW = 4;            // panel width
+constexpr int F64_BUF = 4 * 64 * 4;  // LDS scratch of factor64: 2 strip + 2 panel buffers of [64][4]
+
+// Panel wave: factor the 4 columns held as v[q] = A[l][cb+q] (l >= cb) and finish
+// the 4 X rows held as w[q] = X[cb+q][l]; writes L to sA and the panel to pout.
+__device__ __forceinline__ void f64_factor_panel(double (&v)[F64_PW], double (&w)[F64_PW], int l, int cb,
+                                                 double* sA, int la, double* pout, bool& bad) {
+  constexpr int PW = F64_PW;
 #pragma unroll
-  for (int m = 0; m < NM; ++m) {
-    const int s = g + G * m;
-    a[m] = (s <= r) ? sA[r * la + s] : 0.0;
-    x[m] = (s == r) ? 1.0 : 0.0;
+  for (int q = 0; q < PW; ++q) {
+    const double p = readlane_f64(v[q], cb + q);
+    bad = bad | !(p > 0.0);
+    const double dg = sqrt(p);
+    const double inv = 1.0 / dg;
+    const double lq = (l > cb + q) ? v[q] * inv : dg;  // L[l][cb+q] (rows below cb+q matter)
+    v[q] = lq;
+    w[q] = w[q] * inv;
+#pragma unroll
+    for (int q2 = q + 1; q2 < PW; ++q2) {
+      const double ls = readlane_f64(lq, cb + q2);  // L[cb+q2][cb+q]
+      v[q2] = v[q2] - lq * ls;
+      w[q2] = w[q2] - ls * w[q];
+    }
   }
-  // panel 0 input: A[r][0..3] (X rows 0..3 have no columns left of the panel)
+  if (l >= cb) {
 #pragma unroll
-  for (int m = 0; m < NM; ++m) {
-    const int s = g + G * m;
-    if (s < PW) pin[r * PW + s] = a[m];
+    for (int q = 0; q < PW; ++q) sA[l * la + cb + q] = v[q];
+  }
+  const bool below = l > cb + PW - 1;
+  *reinterpret_cast<d2*>(pout + l * PW) = below ? d2{v[0], v[1]} : d2{w[0], w[1]};
+  *reinterpret_cast<d2*>(pout + l * PW + 2) = below ? d2{v[2], v[3]} : d2{w[2], w[3]};
+}
+
+// Block slots of the MFMA update: the 10 lower 16x16 blocks of A (slot ids 0..9) and
+// of X (10..19), in the order (0,0) (1,0) (1,1) (2,0) (2,1) (2,2) (3,0) .. (3,3);
+// waves 1..7 own ids wave-1, wave-1+7, wave-1+14 (wave 0 is the panel wave).
+__device__ __forceinline__ void f64_block(int id, bool& isx, int& bi, int& bj) {
+  isx = id >= 10;
+  const int t = isx ? id - 10 : id;
+  bi = (t >= 6) ? 3 : (t >= 3) ? 2 : (t >= 1) ? 1 : 0;
+  bj = t - bi * (bi + 1) / 2;
+}
+
+__device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx, double* buf) {
+  constexpr int PW = F64_PW, NS = 3;  // panel width, block slots per update wave
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 15, lk = lane >> 4;  // MFMA operand row/col and depth index; C row base
+  double* strip = buf;                // [2][64][4]: strip k goes to strip[k&1]
+  double* pout = buf + 2 * 64 * PW;   // [2][64][4]: panel k goes to pout[k&1]
+  // update waves: accumulators of the owned blocks, C layout (row lk + 4 reg, col lr)
+  d4 acc[NS];
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    const int id = wave - 1 + 7 * j;
+    acc[j] = d4{0.0, 0.0, 0.0, 0.0};
+    if (wave > 0 && id < 20) {
+      bool isx;
+      int bi, bj;
+      f64_block(id, isx, bi, bj);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = 16 * bi + lk + 4 * e, col = 16 * bj + lr;
+        acc[j][e] = isx ? ((row == col) ? 1.0 : 0.0) : ((col <= row) ? sA[row * la + col] : 0.0);
+      }
+    }
+  }
+  // strips 0 and 1: A[r][0..7] (no X columns left of them)
+  {
+    const int row = tid >> 3, c = tid & 7;
+    strip[(c / PW) * 64 * PW + row * PW + (c % PW)] = (c <= row) ? sA[row * la + c] : 0.0;
   }
   bool bad = false;
-  const bool panel_wave = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;  // wave 0 (scalar branch)
+  double v[PW], w[PW];  // panel wave: the current panel (L columns by row lane, X rows by column lane)
+  __syncthreads();
+  if (wave == 0) {
+    const int l = lane;
+    const d2 p01 = *reinterpret_cast<const d2*>(strip + l * PW);
+    const d2 p23 = *reinterpret_cast<const d2*>(strip + l * PW + 2);
+    v[0] = p01.x; v[1] = p01.y; v[2] = p23.x; v[3] = p23.y;
+#pragma unroll
+    for (int q = 0; q < PW; ++q) w[q] = (l == q) ? 1.0 : 0.0;
+    f64_factor_panel(v, w, l, 0, sA, la, pout, bad);
+  }
 #pragma unroll 1
-  for (int cb = 0; cb < 64; cb += PW) {
-    if (cb == 16) DIAG_STAMP(10);
+  for (int k = 0; k < 64 / PW; ++k) {
+    const int cb = k * PW, ce = cb + PW, pc = cb / 16;
+    if (k == 4) DIAG_STAMP(10);
     __syncthreads();
-    if (cb == 16) DIAG_STAMP(11);
-    if (panel_wave) {
-      const int l = tid;
-      const d2 p01 = *reinterpret_cast<const d2*>(pin + l * PW);
-      const d2 p23 = *reinterpret_cast<const d2*>(pin + l * PW + 2);
-      double v[PW] = {p01.x, p01.y, p23.x, p23.y};  // A[l][cb+q] for l >= cb
-      double w[PW];                                  // X[cb+q][l] for l <= cb+3
+    if (k == 4) DIAG_STAMP(11);
+    const double* pk = pout + (k & 1) * 64 * PW;
+    if (wave == 0) {
+      if (ce < 64) {
+        // look-ahead: strip k+1 through panel k, then factor it
+        const int l = lane, cn = ce;
+        const double* sb = strip + ((k + 1) & 1) * 64 * PW;
+        const d2 p01 = *reinterpret_cast<const d2*>(sb + l * PW);
+        const d2 p23 = *reinterpret_cast<const d2*>(sb + l * PW + 2);
+        double vn[PW] = {p01.x, p01.y, p23.x, p23.y};  // A[l][cn+q] for l >= cn; X[cn+q][l] for l < cb
+        double wn[PW];
 #pragma unroll
-      for (int q = 0; q < PW; ++q) w[q] = (l < cb) ? v[q] : ((l == cb + q) ? 1.0 : 0.0);
+        for (int q = 0; q < PW; ++q) wn[q] = (l < cb) ? vn[q] : ((l == cn + q) ? 1.0 : 0.0);
 #pragma unroll
-      for (int q = 0; q < PW; ++q) {
-        const double p = readlane_f64(v[q], cb + q);
-        bad = bad | !(p > 0.0);
-        const double dg = sqrt(p);
-        const double inv = 1.0 / dg;
-        const double lq = (l > cb + q) ? v[q] * inv : dg;  // L[l][cb+q] (rows below cb+q matter)
-        v[q] = lq;
-        w[q] = w[q] * inv;
+        for (int q = 0; q < PW; ++q)
 #pragma unroll
-        for (int q2 = q + 1; q2 < PW; ++q2) {
-          const double ls = readlane_f64(lq, cb + q2);  // L[cb+q2][cb+q]
-          v[q2] = v[q2] - lq * ls;
-          w[q2] = w[q2] - ls * w[q];
+          for (int q2 = 0; q2 < PW; ++q2) {
+            const double ls = readlane_f64(v[q], cn + q2);  // L[cn+q2][cb+q]
+            vn[q2] = vn[q2] - v[q] * ls;
+            wn[q2] = wn[q2] - ls * w[q];
+          }
+#pragma unroll
+        for (int q = 0; q < PW; ++q) {
+          v[q] = vn[q];
+          w[q] = wn[q];
         }
+        if (k == 4) DIAG_STAMP(12);
+        f64_factor_panel(v, w, l, cn, sA, la, pout + ((k + 1) & 1) * 64 * PW, bad);
+        if (k == 4) DIAG_STAMP(13);
       }
-      if (l >= cb) {
+    } else {
+      // rank-4 updates with one MFMA per owned live block (A operand staged negated):
+      //   A(bi,bj), bj >= pc:          C -= L[rows][cb..] L[cols][cb..]^T
+      //   X(bi,bj), bi >= pc >= bj:    C -= L[rows > cb+3][cb..] X[cb..][cols <= cb+3]
+      // entries of A left of / above the panel are dead (never read again).
+      const int c2 = cb + 2 * PW;
+      double* sb = strip + (k & 1) * 64 * PW;
 #pragma unroll
-        for (int q = 0; q < PW; ++q) sA[l * la + cb + q] = v[q];
-      }
-      const bool below = l > cb + PW - 1;
-      *reinterpret_cast<d2*>(pout + l * PW) = below ? d2{v[0], v[1]} : d2{w[0], w[1]};
-      *reinterpret_cast<d2*>(pout + l * PW + 2) = below ? d2{v[2], v[3]} : d2{w[2], w[3]};
-    }
-    if (cb == 16) DIAG_STAMP(12);
-    __syncthreads();
-    if (cb == 16) DIAG_STAMP(13);
-    const int ce = cb + PW;  // first column right of the panel
-    double lr[PW];
-    {
-      const d2 t01 = *reinterpret_cast<const d2*>(pout + r * PW);
-      const d2 t23 = *reinterpret_cast<const d2*>(pout + r * PW + 2);
-      lr[0] = t01.x; lr[1] = t01.y; lr[2] = t23.x; lr[3] = t23.y;  // L[r][cb+q] if r >= ce, else X[cb+q][r]
-    }
+      for (int j = 0; j < NS; ++j) {
+        const int id = wave - 1 + 7 * j;
+        if (id >= 20) continue;
+        bool isx;
+        int bi, bj;
+        f64_block(id, isx, bi, bj);
+        const int arow = 16 * bi + lr, bcol = 16 * bj + lr;
+        if (!isx) {
+          if (bj >= pc) {
+            const double av = -pk[arow * PW + lk];
+            const double bv = pk[bcol * PW + lk];
+            acc[j] = mfma(av, bv, acc[j]);
+          }
+          // strip k+2: A columns c2..c2+3 (rows >= c2) for the panel wave
+          if (c2 < 64 && bj == c2 / 16 && bi >= bj) {
+            const int q = lr - c2 % 16;
+            if (q >= 0 && q < PW) {
 #pragma unroll
-    for (int m = 0; m < NM; ++m) {
-      const int s = g + G * m;
-      const d2 o01 = *reinterpret_cast<const d2*>(pout + s * PW);
-      const d2 o23 = *reinterpret_cast<const d2*>(pout + s * PW + 2);
-      const double o[PW] = {o01.x, o01.y, o23.x, o23.y};
-      const bool right = s >= ce;
-      double t = right ? a[m] : x[m];
-#pragma unroll
-      for (int q = 0; q < PW; ++q) t = t - lr[q] * o[q];
-      if (r >= ce) {
-        if (right) {
-          if (s <= r) a[m] = t;
+              for (int e = 0; e < 4; ++e) {
+                const int row = 16 * bi + lk + 4 * e;
+                if (row >= c2) sb[row * PW + q] = acc[j][e];
+              }
+            }
+          }
         } else {
-          x[m] = t;
-        }
-      } else if (r >= cb && !right) {  // a panel row of X: take the finished values
-        const int q = r - cb;
-        x[m] = (q == 0) ? o[0] : (q == 1) ? o[1] : (q == 2) ? o[2] : o[3];
-      }
-    }
-    if (cb == 16) DIAG_STAMP(14);
-    // next panel's input
-    if (ce < 64) {
+          if (bi >= pc && bj <= pc) {
+            const double av = (arow > cb + PW - 1) ? -pk[arow * PW + lk] : 0.0;
+            const double bv = (bcol <= cb + PW - 1) ? pk[bcol * PW + lk] : 0.0;
+            acc[j] = mfma(av, bv, acc[j]);
+            if (bi == pc) {  // the panel's X rows cb+lk are finished: take them
+              const int e0 = (cb % 16) / 4;
+              const double xf = (bcol <= cb + PW - 1) ? pk[bcol * PW + lk] : 0.0;
 #pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        const int s = g + G * m;
-        if (r >= ce && s >= ce && s < ce + PW) pin[r * PW + (s - ce)] = a[m];
-        if (r >= ce && r < ce + PW && s < ce) pin[s * PW + (r - ce)] = x[m];
+              for (int e = 0; e < 4; ++e) acc[j][e] = (e == e0) ? xf : acc[j][e];
+            }
+          }
+          // strip k+2: X rows c2..c2+3 (columns < ce) for the panel wave
+          if (c2 < 64 && bi == c2 / 16 && bcol < ce) {
+            const int e0 = (c2 % 16) / 4;
+            double xv = acc[j][0];
+#pragma unroll
+            for (int e = 1; e < 4; ++e) xv = (e == e0) ? acc[j][e] : xv;
+            sb[bcol * PW + lk] = xv;
+          }
+        }
       }
     }
   }
   __syncthreads();
+  // outputs: X blocks from their owners, zeros above the diagonal of X (wave 0) and of L
 #pragma unroll
-  for (int m = 0; m < NM; ++m) {
-    const int s = g + G * m;
-    if (s > r) sA[r * la + s] = 0.0;
-    sX[r * lx + s] = x[m];
+  for (int j = 0; j < NS; ++j) {
+    const int id = wave - 1 + 7 * j;
+    if (wave > 0 && id >= 10 && id < 20) {
+      bool isx;
+      int bi, bj;
+      f64_block(id, isx, bi, bj);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sX[(16 * bi + lk + 4 * e) * lx + 16 * bj + lr] = acc[j][e];
+    }
+  }
+  if (wave == 0) {
+    for (int t = 0; t < 6; ++t) {  // upper blocks (0,1) (0,2) (0,3) (1,2) (1,3) (2,3)
+      const int bi = (t < 3) ? 0 : (t < 5) ? 1 : 2;
+      const int bj = (t < 3) ? t + 1 : (t < 5) ? t - 1 : 3;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sX[(16 * bi + lk + 4 * e) * lx + 16 * bj + lr] = 0.0;
+    }
+  }
+  for (int i = tid; i < 64 * 64; i += DNTH) {
+    const int row = i >> 6, col = i & 63;
+    if (col > row) sA[row * la + col] = 0.0;
   }
   return bad;
 }
@@ -235,7 +332,7 @@ struct DiagSmem {
   double* z;        // 128
   double* ps2;      // 128
   double* psz;      // 128
-  double* scratch;  // 512
+  double* scratch;  // DIAG_SMALL (>= 512)
 };
 
 // ----------------------------------------------------------------------------
@@ -344,7 +441,7 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
 // vectors live in `base` (the GEMM staging area, DIAG_BASE doubles), the
 // 512-double reduction scratch in `small`.
 constexpr int DIAG_BASE = 2 * H * LDH + 4 * T;
-constexpr int DIAG_SMALL = 512;
+constexpr int DIAG_SMALL = F64_BUF;  // factor64's buffers (also >= the 512-double reduction scratch)
 __device__ __forceinline__ DiagSmem carve_diag(double* base, double* small) {
   DiagSmem s;
   s.t0 = base;
@@ -404,11 +501,14 @@ __device__ __forceinline__ void step_tile(int b, int P, int ntl, int grp, int& p
 }
 
 constexpr int STEP_SMEM = (Geo<T>::STAGE > DIAG_BASE) ? Geo<T>::STAGE : DIAG_BASE;  // ~72 KiB: two workgroups per CU
-constexpr int STEP_SMALL = 5 * T;         // z_J + reduction scratch (also the diagonal's scratch)
+constexpr int STEP_SMALL = (5 * T > DIAG_SMALL) ? 5 * T : DIAG_SMALL;  // z_J + reduction scratch, or the diagonal's
 static_assert(DIAG_BASE <= STEP_SMEM && DIAG_SMALL <= STEP_SMALL, "fused diagonal fits the step's LDS");
 constexpr int STEP_NTH = Geo<T>::NTH;     // 512 threads: 8 waves, 64x32 per wave
 static_assert(STEP_NTH == DNTH, "the fused diagonal runs on the step workgroup");
 
+#ifndef GPF_DIAG_PRIO
+#define GPF_DIAG_PRIO 1
+#endif
 #ifndef GPF_STEP_WAVES_PER_SIMD
 #define GPF_STEP_WAVES_PER_SIMD 4  // 2 workgroups of 8 waves per CU
 #endif
@@ -467,6 +567,9 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
       __syncthreads();
       const DiagSmem sm = carve_diag(smem, small);
       const size_t poff = ((size_t)p * nt + I) * Npad + (size_t)I * T;
+#if GPF_DIAG_PRIO
+      __builtin_amdgcn_s_setprio(3);  // latency-critical: the next launch waits for this block
+#endif
       factor128(Aii, Up + (size_t)I * T * ld + (size_t)I * T, ld, yp + I * T, s2p + poff, szp + poff, info + p, sm);
     }
   } else {
@@ -527,7 +630,7 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
 __global__ __launch_bounds__(DNTH) void k_debug_factor64(const double* __restrict__ in, double* __restrict__ out,
                                                          int* __restrict__ bad) {
   __shared__ __attribute__((aligned(16))) double t[2 * H * LDH];
-  __shared__ __attribute__((aligned(16))) double scratch[512];
+  __shared__ __attribute__((aligned(16))) double scratch[F64_BUF];
   const int tid = threadIdx.x;
   for (int k = 0; k < 2; ++k) {
     for (int i = tid; i < H * H; i += DNTH) t[(i / H) * LDH + i % H] = in[k * H * H + i];

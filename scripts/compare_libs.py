@@ -55,6 +55,7 @@ else:
         x, y = a[k], b[k]
         same = np.array_equal(x, y)
         rel = float(np.max(np.abs(x - y) / np.maximum(np.abs(x), 1e-300))) if not same else 0.0
-        worst = max(worst, rel)
-        print(f"{k:14s} {'bitwise' if same else f'max rel diff {rel:.3e}'}")
-    print("worst", worst)
+        nrm = float(np.max(np.abs(x - y)) / max(np.max(np.abs(x)), 1e-300)) if not same else 0.0
+        worst = max(worst, nrm)
+        print(f"{k:14s} {'bitwise' if same else f'max elementwise rel {rel:.3e}  max|d|/max|x| {nrm:.3e}'}")
+    print("worst normwise", worst)

@@ -22,6 +22,6 @@ for N, P in [(128, 1), (128, 64), (4096, 64)]:
     st = np.array(buf[:10], dtype=np.float64)
     d = np.diff(st)
     print(f"N={N} P={P}: total {st[9]-st[0]:.0f} cycles; " + ", ".join(f"{n} {v:.0f}" for n, v in zip(names, d)))
-    p = np.array(buf[10:15], dtype=np.float64)
-    print(f"    panel cb=16 (last factor64): barrier-in {p[1]-p[0]:.0f}, panel wave {p[2]-p[1]:.0f}, "
-          f"barrier-mid {p[3]-p[2]:.0f}, update(thread 0) {p[4]-p[3]:.0f}")
+    p = np.array(buf[10:14], dtype=np.float64)
+    if p.any(): print(f"    iteration k=4 (last factor64, wave 0): barrier {p[1]-p[0]:.0f}, strip read+update {p[2]-p[1]:.0f}, "
+          f"factor panel {p[3]-p[2]:.0f}")

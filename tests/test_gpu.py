@@ -182,7 +182,10 @@ def test_pso_on_gpu_end_to_end(ctx, f4, k, capsys):
     from the reference's once a 1e-12-level score difference flips a stall
     counter (the loss is piecewise constant in l), so this checks the outcome:
     the optimum it reports is as good as the reference's (within 1%) and its
-    reported score is the objective at its reported position."""
+    reported score is the objective at its reported position, up to a coverage
+    tie: the swarm converges onto edges of the piecewise-constant loss, where a
+    pull sits within rounding of |pull| = 1 and two correct fp64 evaluations
+    may count it differently (pull_at_threshold)."""
     import find_len_scales as fls
     x, y, e = _fx(f4[f"c{k}_x"]), f4[f"c{k}_y"], f4[f"c{k}_e"]
     best = fls.len_scale_opt(x, y, e, True, init_positions=f4[f"c{k}_init"], seed=int(f4[f"c{k}_seed"]))
@@ -192,7 +195,9 @@ def test_pso_on_gpu_end_to_end(ctx, f4, k, capsys):
     assert got_score <= ref_score * 1.01
     lo, hi = ref_cpu.search_bounds(x)
     s, ex = ref_cpu.sigma_grid()
-    assert abs(ref_cpu.evaluate_loss(best, x, y, e, s, ex, lo, hi) - got_score) <= 1e-8 * got_score
+    ref_at_best = ref_cpu.evaluate_loss(best, x, y, e, s, ex, lo, hi)
+    if abs(ref_at_best - got_score) > 1e-8 * got_score:
+        assert pull_at_threshold(best, x, y, e, s), (ref_at_best, got_score)
 
 
 def test_not_positive_definite_raises_like_numpy(ctx):
