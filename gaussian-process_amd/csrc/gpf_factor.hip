@@ -26,10 +26,11 @@ namespace gpf {
 // Diagnostic build only (-DGPF_DIAG_STAMPS): thread 0 of workgroup 0 records s_memtime at
 // phase boundaries of factor128 into a buffer nothing else reads.
 __device__ unsigned long long g_diag_stamps[32];
-#define DIAG_STAMP(i)                                                                              \
+#define DIAG_STAMP(i) DIAG_STAMP_T(i, 0)
+#define DIAG_STAMP_T(i, thr)                                                                       \
   do {                                                                                           \
     __builtin_amdgcn_sched_barrier(0);                                                           \
-    if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) {  /* WG (p 0, w 0) */                                \
+    if (threadIdx.x == (thr) && blockIdx.x == 0 && blockIdx.y == 0) {  /* WG (p 0, w 0) */                                \
       unsigned long long t_;                                                                     \
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                  \
       g_diag_stamps[i] = t_;                                                                     \
@@ -39,6 +40,9 @@ __device__ unsigned long long g_diag_stamps[32];
 #else
 #define DIAG_STAMP(i) \
   do {               \
+  } while (0)
+#define DIAG_STAMP_T(i, thr) \
+  do {                      \
   } while (0)
 #endif
 
@@ -76,28 +80,59 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// 1/sqrt(p) for the pivots of the diagonal factor: v_rsq_f64 and two Newton steps
+// (y += y (1/2 - p/2 y^2)), a ~9-op dependent chain instead of the ~25 of a
+// correctly rounded sqrt followed by a division; within a few ulp of 1/sqrt(p).
+__device__ __forceinline__ double rsqrt_nr(double p) {
+  double y = __builtin_amdgcn_rsq(p);
+  const double h = 0.5 * p;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const double t = fma(-(h * y), y, 0.5);
+    y = fma(y, t, y);
+  }
+  return y;
+}
+
 constexpr int F64_PW = 4;            // panel width
 constexpr int F64_BUF = 4 * 64 * 4;  // LDS scratch of factor64: 2 strip + 2 panel buffers of [64][4]
 
 // Panel wave: factor the 4 columns held as v[q] = A[l][cb+q] (l >= cb) and finish
 // the 4 X rows held as w[q] = X[cb+q][l]; writes L to sA and the panel to pout.
+// The 4x4 diagonal block is broadcast once (10 readlanes) and factored redundantly
+// by every lane, so each lane's row needs no further cross-lane traffic. The
+// operations and their order are those of the column-by-column elimination.
 __device__ __forceinline__ void f64_factor_panel(double (&v)[F64_PW], double (&w)[F64_PW], int l, int cb,
                                                  double* sA, int la, double* pout, bool& bad) {
   constexpr int PW = F64_PW;
+  double d[PW][PW];  // d[i][j] = A[cb+i][cb+j], j <= i (then L of the block)
+#pragma unroll
+  for (int i = 0; i < PW; ++i)
+#pragma unroll
+    for (int j = 0; j <= i; ++j) d[i][j] = readlane_f64(v[j], cb + i);
+  double dg[PW], inv[PW];
 #pragma unroll
   for (int q = 0; q < PW; ++q) {
-    const double p = readlane_f64(v[q], cb + q);
+    const double p = d[q][q];
     bad = bad | !(p > 0.0);
-    const double dg = sqrt(p);
-    const double inv = 1.0 / dg;
-    const double lq = (l > cb + q) ? v[q] * inv : dg;  // L[l][cb+q] (rows below cb+q matter)
+    inv[q] = rsqrt_nr(p);
+    dg[q] = p * inv[q];
+#pragma unroll
+    for (int i = q + 1; i < PW; ++i) d[i][q] = d[i][q] * inv[q];  // L[cb+i][cb+q]
+#pragma unroll
+    for (int i = q + 1; i < PW; ++i)
+#pragma unroll
+      for (int j = q + 1; j <= i; ++j) d[i][j] = d[i][j] - d[i][q] * d[j][q];
+  }
+#pragma unroll
+  for (int q = 0; q < PW; ++q) {
+    const double lq = (l > cb + q) ? v[q] * inv[q] : dg[q];  // L[l][cb+q] (rows below cb+q matter)
     v[q] = lq;
-    w[q] = w[q] * inv;
+    w[q] = w[q] * inv[q];
 #pragma unroll
     for (int q2 = q + 1; q2 < PW; ++q2) {
-      const double ls = readlane_f64(lq, cb + q2);  // L[cb+q2][cb+q]
-      v[q2] = v[q2] - lq * ls;
-      w[q2] = w[q2] - ls * w[q];
+      v[q2] = v[q2] - lq * d[q2][q];
+      w[q2] = w[q2] - d[q2][q] * w[q];
     }
   }
   if (l >= cb) {
