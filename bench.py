@@ -96,6 +96,44 @@ def cpu_baseline(x, y, e, positions, lo, hi, workers):
     return len(args) / dt, np.array(out), dt
 
 
+def predict_line(ctx, x, y, e, N, d, args):
+    """Secondary measurement, SURVEY.md §8f row 1: GP(x, y, e, x_fit, l) at M query
+    points (GP_fit.py:32 -> GP_func.py:12-45): one factorisation, then the
+    cross-covariance build and V = U K_s reduced to column sums of squares."""
+    M = args.predict_points
+    rng = np.random.default_rng(args.seed + 99)
+    xf = rng.uniform(size=(d, M))
+    ls = np.full(d, 0.3)
+    ctx.predict(ls, xf)  # warm-up (workspace, code objects)
+    ctx.reset_profile()
+    ctx.set_profiling(True)
+    import torch
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ctx.predict(ls, xf)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    prof = ctx.profile()
+    ctx.set_profiling(False)
+    out = {"N": N, "d": d, "M": M, "ms": dt * 1e3, "points_per_s": M / dt,
+           "factor_ms": prof["factor_wall_ms"],
+           "k_predict_vsq_ms": prof["predict_ms"],
+           "k_predict_vsq_tflops": prof["predict_flops"] / (prof["predict_ms"] * 1e-3) / 1e12
+           if prof["predict_ms"] > 0 else None,
+           "k_cross_cov_GBps": prof["predict_cov_bytes"] / (prof["predict_cov_ms"] * 1e-3) / 1e9
+           if prof["predict_cov_ms"] > 0 else None,
+           "note": "wall time includes the single-particle factorisation and host<->device copies"}
+    if not args.no_cpu and args.cpu_predict_points > 0:
+        from oracle import ref_cpu  # CPU baseline leg only
+        m = args.cpu_predict_points
+        t1 = time.perf_counter()
+        ref_cpu.GP(x, y, e, xf[:, :m], ls, batch_size=10000)
+        cdt = time.perf_counter() - t1
+        out["cpu_baseline"] = {"points_per_s": m / cdt, "sample": f"oracle GP (GP_func.py:12-45 restated) on {m} "
+                               f"query points, host BLAS threads={os.environ.get('OMP_NUM_THREADS')}", "s": cdt}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -111,6 +149,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="do not bracket launches with HIP events")
     ap.add_argument("--pso-steps", type=int, default=3, help="secondary: real PSO iterations timed")
+    ap.add_argument("--predict-points", type=int, default=10000,
+                    help="secondary (SURVEY.md §8f row 1): GP prediction at this many query points, 0 = skip")
+    ap.add_argument("--cpu-predict-points", type=int, default=256, help="CPU GP sample for the prediction line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -212,6 +253,10 @@ def main():
     breakdown["evals_on_gpu"] = prof["evals"]
 
     cpu = None
+    predict = None
+    if rank == 0 and args.predict_points > 0:
+        predict = predict_line(ctx, x, y, e, N, d, args)
+
     if rank == 0 and not args.no_cpu and args.cpu_sample > 0:
         rng = np.random.default_rng(args.seed + 7)
         sample = lo + (hi - lo) * rng.uniform(0.2, 0.8, size=(args.cpu_sample, d))
@@ -235,6 +280,7 @@ def main():
                        "parallelism": f"swarm-shard x{world}", "hetero_noise": bool(args.hetero),
                        "pso_iters_per_s": args.steps / dt, "particles": "interior l~U[0.05,0.6]^d (full work)"},
             "pso_loop": pso,
+            "predict": predict,
             "roofline": roof,
             "cpu_baseline": cpu,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,

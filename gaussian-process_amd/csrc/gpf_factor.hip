@@ -547,10 +547,21 @@ static_assert(STEP_NTH == DNTH, "the fused diagonal runs on the step workgroup")
 #ifndef GPF_STEP_WAVES_PER_SIMD
 #define GPF_STEP_WAVES_PER_SIMD 4  // 2 workgroups of 8 waves per CU
 #endif
-__global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int J, int nt, int Npad, double* __restrict__ Lb,
-                                                  double* __restrict__ Ub, double* __restrict__ yb,
-                                                  double* __restrict__ s2p, double* __restrict__ szp,
-                                                  int* __restrict__ info, int P, int grp) {
+#ifdef GPF_WG_TRACE
+// Diagnostic build only (-DGPF_WG_TRACE): per-workgroup start/end (s_memrealtime, 100 MHz)
+// and hardware placement of every k_step workgroup, per block column J.
+constexpr int WG_TRACE_J = 64, WG_TRACE_N = 4096;
+__device__ unsigned long long g_wg_trace[WG_TRACE_J][WG_TRACE_N][3];
+__device__ __forceinline__ unsigned long long realtime() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+#endif
+
+__device__ __forceinline__ void k_step_body(int J, int nt, int Npad, double* __restrict__ Lb, double* __restrict__ Ub,
+                                            double* __restrict__ yb, double* __restrict__ s2p,
+                                            double* __restrict__ szp, int* __restrict__ info, int P, int grp) {
   __shared__ __attribute__((aligned(16))) double smem[STEP_SMEM];
   __shared__ __attribute__((aligned(16))) double small[STEP_SMALL];
   const int tid = threadIdx.x;
@@ -659,6 +670,28 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
     }
   }
 }
+
+__global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int J, int nt, int Npad, double* __restrict__ Lb,
+                                                  double* __restrict__ Ub, double* __restrict__ yb,
+                                                  double* __restrict__ s2p, double* __restrict__ szp,
+                                                  int* __restrict__ info, int P, int grp) {
+  const int tid = threadIdx.x;
+#ifdef GPF_WG_TRACE
+  if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_wg_trace[J][blockIdx.x][0] = realtime();
+    g_wg_trace[J][blockIdx.x][2] = ((unsigned long long)xcc << 32) | hw;
+  }
+#endif
+  k_step_body(J, nt, Npad, Lb, Ub, yb, s2p, szp, info, P, grp);
+#ifdef GPF_WG_TRACE
+  __syncthreads();
+  if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) g_wg_trace[J][blockIdx.x][1] = realtime();
+#endif
+}
+
 
 // Debug hook (gpf_debug_factor64): factor64 on two host-given 64x64 matrices in a row
 // (in: 2 x 64 x 64 row-major; out: L then X for each).

@@ -28,7 +28,7 @@ using gpf::T;
 
 namespace {
 
-enum ProfClass { PC_PANEL = 0, PC_DIAG = 1, PC_BUILD = 2, PC_LOSS = 3, PC_FACTOR = 4, PC_N = 5 };
+enum ProfClass { PC_PANEL = 0, PC_DIAG = 1, PC_BUILD = 2, PC_LOSS = 3, PC_FACTOR = 4, PC_PRED = 5, PC_PREDK = 6, PC_N = 7 };
 
 constexpr int MAX_GROUPS = 4;  // particle groups factorised on concurrent streams
 
@@ -542,14 +542,19 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
     }
     const int nqt = (int)((m + T - 1) / T);
     const int Cm = nqt * T;
-    rc = launch(c, PC_BUILD, 8.0 * Np * Cm, [&] {
+    rc = launch(c, PC_PREDK, 8.0 * Np * Cm, [&] {
       hipLaunchKernelGGL(gpf::k_cross_cov, dim3(Cm / BT, (unsigned)(Np / BT)), dim3(NTHR), 0, c->stream, (int)c->N,
                          (int)m, (int)Np, Cm, c->d, c->d_x, (int)c->N, d_xf, (int)Cp, c->d_ls, d_ks, (int64_t)Cp);
     });
     if (rc) break;
-    rc = launch(c, PC_PANEL, 0.0, [&] {
+    // V = U K_s: row tile t of U has (t+1) column tiles, the last one triangular
+    const double vflops = 2.0 * T * T * (double)Cm * (c->nt * (c->nt + 1) / 2) - (double)T * T * Cm * c->nt;
+    rc = launch(c, PC_PRED, vflops, [&] {
       hipLaunchKernelGGL(gpf::k_predict_vsq, dim3(nqt, c->nt), dim3(gpf::Geo<T>::NTH), 0, c->stream, (int)Np, c->d_U, d_ks,
                          (int)Cp, d_vsq);
+    });
+    if (rc) break;
+    rc = launch(c, PC_LOSS, 0.0, [&] {
       hipLaunchKernelGGL(gpf::k_predict_out, dim3((unsigned)((m + NTHR - 1) / NTHR)), dim3(NTHR), 0, c->stream,
                          (int)c->N, c->nt, (int)m, d_ks, (int)Cp, alpha, d_vsq, d_mu, d_sd);
     });
@@ -637,11 +642,13 @@ int gpf_get_profile(gpf_ctx* c, double* out, int n) {
   if (!c || !out) return 0;
   hipStreamSynchronize(c->stream);
   harvest(c);
-  double v[15] = {c->acc[PC_PANEL][0],  c->acc[PC_PANEL][1],  c->acc[PC_PANEL][2], c->acc[PC_DIAG][0],
+  double v[21] = {c->acc[PC_PANEL][0],  c->acc[PC_PANEL][1],  c->acc[PC_PANEL][2], c->acc[PC_DIAG][0],
                   c->acc[PC_DIAG][1],   c->acc[PC_DIAG][2],   c->acc[PC_BUILD][0], c->acc[PC_BUILD][1],
                   c->acc[PC_BUILD][2],  c->acc[PC_LOSS][0],   c->acc[PC_LOSS][1],  c->evals,
-                  c->acc[PC_FACTOR][0], c->acc[PC_FACTOR][1], c->acc[PC_FACTOR][2]};
-  const int m = std::min(n, 15);
+                  c->acc[PC_FACTOR][0], c->acc[PC_FACTOR][1], c->acc[PC_FACTOR][2],
+                  c->acc[PC_PRED][0],   c->acc[PC_PRED][1],   c->acc[PC_PRED][2],
+                  c->acc[PC_PREDK][0],  c->acc[PC_PREDK][1],  c->acc[PC_PREDK][2]};
+  const int m = std::min(n, 21);
   for (int i = 0; i < m; ++i) out[i] = v[i];
   return m;
 }
@@ -750,6 +757,19 @@ int gpf_debug_factor64(gpf_ctx* c, const double* in, double* out, int* bad) {
   hipFree(di); hipFree(dout); hipFree(db);
   return GPF_OK;
 }
+
+#ifdef GPF_WG_TRACE
+// diagnostic builds only: per-workgroup (start, end, placement) of k_step, [J][wg][3]
+int gpf_debug_wg_trace(unsigned long long* out, int nj, int nwg) {
+  if (!out || nj <= 0 || nwg <= 0 || nj > gpf::WG_TRACE_J || nwg > gpf::WG_TRACE_N) return GPF_BAD_ARG;
+  hipDeviceSynchronize();
+  std::vector<unsigned long long> h((size_t)gpf::WG_TRACE_J * gpf::WG_TRACE_N * 3);
+  if (hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(gpf::g_wg_trace), h.size() * 8) != hipSuccess) return GPF_HIP_ERROR;
+  for (int j = 0; j < nj; ++j)
+    std::memcpy(out + (size_t)j * nwg * 3, h.data() + (size_t)j * gpf::WG_TRACE_N * 3, (size_t)nwg * 3 * 8);
+  return GPF_OK;
+}
+#endif
 
 #ifdef GPF_DIAG_STAMPS
 // diagnostic builds only: phase timestamps of factor128 (workgroup 0 of the last k_diag launch)

@@ -192,11 +192,12 @@ class Context:
         self._check(self.lib.gpf_reset_profile(self._h), "gpf_reset_profile")
 
     def profile(self):
-        buf = np.zeros(15)
-        self.lib.gpf_get_profile(self._h, _ptr(buf), 15)
+        buf = np.zeros(21)
+        self.lib.gpf_get_profile(self._h, _ptr(buf), 21)
         keys = ["panel_ms", "panel_launches", "panel_flops", "diag_ms", "diag_launches", "diag_flops",
                 "build_ms", "build_launches", "build_bytes", "loss_ms", "loss_launches", "evals",
-                "factor_wall_ms", "factor_calls", "factor_flops"]
+                "factor_wall_ms", "factor_calls", "factor_flops", "predict_ms", "predict_launches",
+                "predict_flops", "predict_cov_ms", "predict_cov_launches", "predict_cov_bytes"]
         return dict(zip(keys, buf.tolist()))
 
     def debug_factor(self, lengths):

@@ -104,6 +104,8 @@ int gpf_set_profiling(gpf_ctx* ctx, int on);
  *  [9] loss kernel ms    [10] loss launches  [11] evals (non-sentinel)
  *  [12] factorisation wall ms (K build + diag + steps of all particle groups, which run
  *       on concurrent streams, so [0]/[3]/[6] may overlap)  [13] calls  [14] its flops
+ *  [15] prediction V = U K_s kernel ms  [16] launches  [17] algorithmic flops
+ *  [18] prediction cross-covariance ms  [19] launches  [20] algorithmic bytes
  * Returns the number of values written. */
 int gpf_get_profile(gpf_ctx* ctx, double* out, int n);
 int gpf_reset_profile(gpf_ctx* ctx);
