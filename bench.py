@@ -134,6 +134,42 @@ def predict_line(ctx, x, y, e, N, d, args):
     return out
 
 
+def psurf_line(ctx, args):
+    """Secondary measurement, SURVEY.md §8f row 4: probability surface of a merged frame of
+    `psurf_rows` grid rows x 4 experiments (calc_prob_surf.py:15-30,67-81), kernel time from
+    HIP events; HBM roofline on its algorithmic bytes (tails read + 2 x 100 doubles written)."""
+    M, E = args.psurf_rows, 8
+    rng = np.random.default_rng(args.seed + 5)
+    tails = np.empty((M, E))
+    tails[:, 0::2] = rng.normal(size=(M, E // 2))
+    tails[:, 1::2] = rng.uniform(0.05, 0.5, size=(M, E // 2))
+    tails[rng.uniform(size=M) < 0.1, 6:] = np.inf  # some rows miss an experiment
+    ctx.prob_surface(tails[:1000])
+    ctx.reset_profile()
+    ctx.set_profiling(True)
+    t0 = time.perf_counter()
+    _, p, ok = ctx.prob_surface(tails)
+    dt = time.perf_counter() - t0
+    prof = ctx.profile()
+    ctx.set_profiling(False)
+    kms = prof["psurf_ms"]
+    out = {"rows": M, "experiments": E // 2, "wall_ms": dt * 1e3, "kernel_ms": kms,
+           "rows_per_s_kernel": M / (kms * 1e-3) if kms > 0 else None, "rows_per_s_wall": M / dt,
+           "kernel_GBps": prof["psurf_bytes"] / (kms * 1e-3) / 1e9 if kms > 0 else None,
+           "hbm_peak_GBps": 8000.0,
+           "note": "wall includes host<->device copies of the tails and of y, p (PCIe)"}
+    if not args.no_cpu:
+        from oracle import ref_cpu  # CPU baseline leg only
+        m = 2000
+        vals = np.concatenate([np.zeros((m, 2)), tails[:m]], axis=1)
+        t1 = time.perf_counter()
+        ref_cpu.prob_surface(vals, 2)
+        cdt = time.perf_counter() - t1
+        out["cpu_baseline"] = {"rows_per_s": m / cdt, "sample": f"oracle prob_surface (calc_prob_surf.py "
+                               f"restated: numpy + scipy.stats.norm) on {m} rows, 1 core", "s": cdt}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -152,6 +188,8 @@ def main():
     ap.add_argument("--predict-points", type=int, default=10000,
                     help="secondary (SURVEY.md §8f row 1): GP prediction at this many query points, 0 = skip")
     ap.add_argument("--cpu-predict-points", type=int, default=256, help="CPU GP sample for the prediction line")
+    ap.add_argument("--psurf-rows", type=int, default=100000,
+                    help="secondary (SURVEY.md §8f row 4): probability-surface rows, 0 = skip")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -256,6 +294,9 @@ def main():
     predict = None
     if rank == 0 and args.predict_points > 0:
         predict = predict_line(ctx, x, y, e, N, d, args)
+    psurf = None
+    if rank == 0 and args.psurf_rows > 0:
+        psurf = psurf_line(ctx, args)
 
     if rank == 0 and not args.no_cpu and args.cpu_sample > 0:
         rng = np.random.default_rng(args.seed + 7)
@@ -281,6 +322,7 @@ def main():
                        "pso_iters_per_s": args.steps / dt, "particles": "interior l~U[0.05,0.6]^d (full work)"},
             "pso_loop": pso,
             "predict": predict,
+            "prob_surface": psurf,
             "roofline": roof,
             "cpu_baseline": cpu,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,

@@ -21,6 +21,7 @@
 #include "gpf_factor.hip"
 #include "gpf_objective.hip"
 #include "gpf_predict.hip"
+#include "gpf_probsurf.hip"
 
 using gpf::BT;
 using gpf::NTHR;
@@ -28,7 +29,7 @@ using gpf::T;
 
 namespace {
 
-enum ProfClass { PC_PANEL = 0, PC_DIAG = 1, PC_BUILD = 2, PC_LOSS = 3, PC_FACTOR = 4, PC_PRED = 5, PC_PREDK = 6, PC_N = 7 };
+enum ProfClass { PC_PANEL = 0, PC_DIAG = 1, PC_BUILD = 2, PC_LOSS = 3, PC_FACTOR = 4, PC_PRED = 5, PC_PREDK = 6, PC_PSURF = 7, PC_N = 8 };
 
 constexpr int MAX_GROUPS = 4;  // particle groups factorised on concurrent streams
 
@@ -642,13 +643,14 @@ int gpf_get_profile(gpf_ctx* c, double* out, int n) {
   if (!c || !out) return 0;
   hipStreamSynchronize(c->stream);
   harvest(c);
-  double v[21] = {c->acc[PC_PANEL][0],  c->acc[PC_PANEL][1],  c->acc[PC_PANEL][2], c->acc[PC_DIAG][0],
+  double v[24] = {c->acc[PC_PANEL][0],  c->acc[PC_PANEL][1],  c->acc[PC_PANEL][2], c->acc[PC_DIAG][0],
                   c->acc[PC_DIAG][1],   c->acc[PC_DIAG][2],   c->acc[PC_BUILD][0], c->acc[PC_BUILD][1],
                   c->acc[PC_BUILD][2],  c->acc[PC_LOSS][0],   c->acc[PC_LOSS][1],  c->evals,
                   c->acc[PC_FACTOR][0], c->acc[PC_FACTOR][1], c->acc[PC_FACTOR][2],
                   c->acc[PC_PRED][0],   c->acc[PC_PRED][1],   c->acc[PC_PRED][2],
-                  c->acc[PC_PREDK][0],  c->acc[PC_PREDK][1],  c->acc[PC_PREDK][2]};
-  const int m = std::min(n, 21);
+                  c->acc[PC_PREDK][0],  c->acc[PC_PREDK][1],  c->acc[PC_PREDK][2],
+                  c->acc[PC_PSURF][0],  c->acc[PC_PSURF][1],  c->acc[PC_PSURF][2]};
+  const int m = std::min(n, 24);
   for (int i = 0; i < m; ++i) out[i] = v[i];
   return m;
 }
@@ -706,6 +708,48 @@ int gpf_mfma_peak(gpf_ctx* c, int blocks, int iters, double* tflops) {
   hipEventDestroy(b);
   hipFree(out);
   return GPF_OK;
+}
+
+// Probability surface (calc_prob_surf.py:15-30,67-81) of M rows of E tail entries each.
+int gpf_prob_surface(gpf_ctx* c, const double* tails, int64_t M, int E, double* y, double* p, int* ok) {
+  if (!c) return GPF_BAD_ARG;
+  if (M < 0 || E < 0 || E > gpf::PS_EMAX || (M > 0 && (!tails || !y || !p || !ok)))
+    return bad_arg(c, "gpf_prob_surface: bad arguments");
+  if (M == 0) return GPF_OK;
+  hipSetDevice(c->device);
+  const int64_t chunk = std::min<int64_t>(M, 1 << 20);
+  double *dt = nullptr, *dy = nullptr, *dp = nullptr;
+  int* dok = nullptr;
+  GPF_HIP(c, hipMalloc(&dt, (size_t)chunk * std::max(E, 1) * 8));
+  GPF_HIP(c, hipMalloc(&dy, (size_t)chunk * gpf::PS_POINTS * 8));
+  GPF_HIP(c, hipMalloc(&dp, (size_t)chunk * gpf::PS_POINTS * 8));
+  GPF_HIP(c, hipMalloc(&dok, (size_t)chunk * 4));
+  int rc = GPF_OK;
+  for (int64_t s = 0; s < M && rc == GPF_OK; s += chunk) {
+    const int64_t m = std::min<int64_t>(chunk, M - s);
+    if (hipMemcpyAsync(dt, tails + s * E, (size_t)m * E * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+      rc = GPF_HIP_ERROR;
+      break;
+    }
+    // algorithmic bytes: the tails read, y and p written, the row flags
+    const double bytes = (double)m * (E * 8.0 + 2.0 * gpf::PS_POINTS * 8.0 + 4.0);
+    rc = launch(c, PC_PSURF, bytes, [&] {
+      hipLaunchKernelGGL(gpf::k_prob_surf, dim3((unsigned)m), dim3(gpf::PS_NTH), 0, c->stream, dt, m, E, dy, dp, dok);
+    });
+    if (rc) break;
+    if (hipMemcpyAsync(y + s * gpf::PS_POINTS, dy, (size_t)m * gpf::PS_POINTS * 8, hipMemcpyDeviceToHost, c->stream) !=
+            hipSuccess ||
+        hipMemcpyAsync(p + s * gpf::PS_POINTS, dp, (size_t)m * gpf::PS_POINTS * 8, hipMemcpyDeviceToHost, c->stream) !=
+            hipSuccess ||
+        hipMemcpyAsync(ok + s, dok, (size_t)m * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+      rc = GPF_HIP_ERROR;
+      c->err = "gpf_prob_surface: copy failed";
+    }
+  }
+  if (rc == GPF_HIP_ERROR && c->err.empty()) c->err = "gpf_prob_surface: HIP error";
+  hipFree(dt); hipFree(dy); hipFree(dp); hipFree(dok);
+  return rc;
 }
 
 // Measurement hook: TF/s of the k_step L-tile GEMM core alone (k_gemm_bench) on

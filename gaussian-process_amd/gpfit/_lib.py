@@ -41,6 +41,8 @@ SIGNATURES = {
     "gpf_selftest_mfma": (ctypes.c_int, [_vp, _dp, _dp, _dp]),
     "gpf_debug_factor": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _dp]),
     "gpf_mfma_peak": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _dp]),
+    "gpf_prob_surface": (ctypes.c_int, [_vp, _dp, ctypes.c_int64, ctypes.c_int, _dp, _dp,
+                                        ctypes.POINTER(ctypes.c_int)]),
     "gpf_gemm_bench": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_int, _dp]),
 }
@@ -192,12 +194,13 @@ class Context:
         self._check(self.lib.gpf_reset_profile(self._h), "gpf_reset_profile")
 
     def profile(self):
-        buf = np.zeros(21)
-        self.lib.gpf_get_profile(self._h, _ptr(buf), 21)
+        buf = np.zeros(24)
+        self.lib.gpf_get_profile(self._h, _ptr(buf), 24)
         keys = ["panel_ms", "panel_launches", "panel_flops", "diag_ms", "diag_launches", "diag_flops",
                 "build_ms", "build_launches", "build_bytes", "loss_ms", "loss_launches", "evals",
                 "factor_wall_ms", "factor_calls", "factor_flops", "predict_ms", "predict_launches",
-                "predict_flops", "predict_cov_ms", "predict_cov_launches", "predict_cov_bytes"]
+                "predict_flops", "predict_cov_ms", "predict_cov_launches", "predict_cov_bytes",
+                "psurf_ms", "psurf_launches", "psurf_bytes"]
         return dict(zip(keys, buf.tolist()))
 
     def debug_factor(self, lengths):
@@ -216,6 +219,18 @@ class Context:
         out = ctypes.c_double(0.0)
         self._check(self.lib.gpf_mfma_peak(self._h, int(blocks), int(iters), ctypes.byref(out)), "gpf_mfma_peak")
         return out.value
+
+    def prob_surface(self, tails):
+        """(y (M,100), p (M,100), ok (M,) bool) for each row of tail entries (gpf_prob_surface)."""
+        t = _f64(tails)
+        if t.ndim != 2:
+            raise ValueError("tails must be (M, E)")
+        m, e = t.shape
+        y, p = np.empty((m, 100)), np.empty((m, 100))
+        ok = np.empty(m, dtype=np.int32)
+        self._check(self.lib.gpf_prob_surface(self._h, _ptr(t), m, e, _ptr(y), _ptr(p),
+                                              ok.ctypes.data_as(ctypes.POINTER(ctypes.c_int))), "gpf_prob_surface")
+        return y, p, ok.astype(bool)
 
     def gemm_bench(self, mode=0, npad=4096, particles=64, tiles=15, depth=2048, iters=5):
         """TF/s of the block-column GEMM core alone (gpf_gemm_bench)."""

@@ -92,6 +92,13 @@ int gpf_kernel(gpf_ctx* ctx, const double* x1_dN1, int64_t N1,
  * none): -1/2 y^T alpha - sum log L_ii - N/2 log(2 pi). */
 int gpf_log_marginal_likelihood(gpf_ctx* ctx, const double* ls, double* out);
 
+/* Probability surface of merged GP results (replaces calc_prob_surf.py:15-30,67-81; SURVEY.md
+ * §8f row 4). tails: M rows x E entries (row-major) = each merged-frame row after its kinematic
+ * columns, non-finite = missing. Per row: y[100] (the numpy.linspace grid), p[100] (bin
+ * probabilities of the equal-weight Gaussian mixture), ok = 0 if the row is skipped (fewer than
+ * 2 or an odd number of finite entries, calc_prob_surf.py:71-73), else 1. E <= 1024. */
+int gpf_prob_surface(gpf_ctx* ctx, const double* tails, int64_t M, int E, double* y, double* p, int* ok);
+
 /* ---- measurement hooks (bench.py) ---- */
 
 /* Enable per-kernel-class HIP event timing on the context's stream. */
@@ -106,6 +113,7 @@ int gpf_set_profiling(gpf_ctx* ctx, int on);
  *       on concurrent streams, so [0]/[3]/[6] may overlap)  [13] calls  [14] its flops
  *  [15] prediction V = U K_s kernel ms  [16] launches  [17] algorithmic flops
  *  [18] prediction cross-covariance ms  [19] launches  [20] algorithmic bytes
+ *  [21] probability-surface kernel ms  [22] launches  [23] algorithmic bytes
  * Returns the number of values written. */
 int gpf_get_profile(gpf_ctx* ctx, double* out, int n);
 int gpf_reset_profile(gpf_ctx* ctx);

@@ -315,3 +315,38 @@ def len_scale_opt(x_known, y_known, e_known, PSO_progress, *,
         print(g_score)
         print(f"Total soft restarts: {restarts}")
     return g_pos
+
+
+# ---------------------------------------------------------------------------
+# Probability surface  (calc_prob_surf.py) — host restatement, checker of gpf_prob_surface
+# ---------------------------------------------------------------------------
+
+def sum_gaussians(temp_y, temp_gaus):
+    """Mean bin probability under the Gaussians (mu_0, sd_0, mu_1, ...), calc_prob_surf.py:15-30."""
+    from scipy.stats import norm
+    temp_y = np.asarray(temp_y)
+    k = len(temp_gaus) // 2
+    dy = abs(max(temp_y) - min(temp_y)) / len(temp_y)
+    z = np.zeros(len(temp_y))
+    for i in range(k):
+        mu, sd = temp_gaus[2 * i], temp_gaus[2 * i + 1]
+        z += norm.cdf(temp_y + dy / 2, loc=mu, scale=sd)
+        z -= norm.cdf(temp_y - dy / 2, loc=mu, scale=sd)
+    return z / k
+
+
+def prob_surface(values, ndims, points=100):
+    """Per-row (y, p) of calc_prob_surf.py:67-81: rows whose finite tail has fewer than 2 or an
+    odd number of entries are skipped. Returns (row indices, y (R, points), p (R, points))."""
+    rows, ys, ps = [], [], []
+    for r, row in enumerate(values):
+        tail = row[ndims:]
+        gaus = tail[np.isfinite(tail)]
+        if len(gaus) < 2 or len(gaus) % 2:
+            continue
+        mus, sds = gaus[::2], gaus[1::2]
+        y = np.linspace(min(mus - 3 * sds), max(mus + 3 * sds), points)
+        rows.append(r)
+        ys.append(y)
+        ps.append(sum_gaussians(y, gaus))
+    return np.array(rows, dtype=np.int64), np.array(ys).reshape(-1, points), np.array(ps).reshape(-1, points)

@@ -31,8 +31,26 @@ def test_round_to_res_quirks():
     assert round_to_res(7.0, 2) == 8
 
 
-def test_prob_surface_matches_reference(tmp_path):
-    from calc_prob_surf import generate_prob_surf
+def test_prob_surface_oracle_matches_reference(tmp_path):
+    """The host restatement (checker of the GPU kernel), written through the same object-frame
+    to_csv as calc_prob_surf.py:84-86, equals the reference's output file F7 bit for bit."""
+    from oracle import ref_cpu
+    f7 = load_golden("f7_prob_surf.npz")
+    rows, ys, ps = ref_cpu.prob_surface(f7["frame"], 2)
+    data = np.empty((len(rows) * 100, 4), dtype=object)
+    data[:, :2] = np.repeat(f7["frame"][rows, :2], 100, axis=0)
+    data[:, 2] = ys.reshape(-1)
+    data[:, 3] = ps.reshape(-1)
+    pd.DataFrame(data.tolist(), columns=[str(c) for c in f7["out_columns"]]).to_csv(tmp_path / "o.csv", index=False)
+    np.testing.assert_array_equal(pd.read_csv(tmp_path / "o.csv").values, f7["out"])
+
+
+@pytest.mark.gpu
+def test_prob_surface_on_gpu_matches_reference(tmp_path):
+    """generate_prob_surf (k_prob_surf on the MI355X) vs the reference's output F7: same rows,
+    columns and grid (bitwise: same linspace arithmetic), probabilities to 1e-12 (erf/erfc are
+    not scipy's implementations)."""
+    from calc_prob_surf import generate_prob_surf, sum_gaussians
     f7 = load_golden("f7_prob_surf.npz")
     df = pd.DataFrame(f7["frame"], columns=[str(c) for c in f7["columns"]])
     out = tmp_path / "ps.txt"
@@ -41,7 +59,38 @@ def test_prob_surface_matches_reference(tmp_path):
     generate_prob_surf(df, 2, options_path=str(opt))
     got = pd.read_csv(out)
     assert list(got.columns) == [str(c) for c in f7["out_columns"]]
-    np.testing.assert_array_equal(got.values, f7["out"])
+    ref = f7["out"]
+    assert got.values.shape == ref.shape
+    np.testing.assert_array_equal(got.values[:, :3], ref[:, :3])
+    np.testing.assert_allclose(got.values[:, 3], ref[:, 3], rtol=1e-12, atol=1e-15)
+    # the scalar helper on one row, and its argument checks
+    row = next(r for r in f7["frame"] if np.isfinite(r[2:]).sum() >= 2 and np.isfinite(r[2:]).sum() % 2 == 0)
+    gaus = row[2:][np.isfinite(row[2:])]
+    y = np.linspace(min(gaus[::2] - 3 * gaus[1::2]), max(gaus[::2] + 3 * gaus[1::2]), 100)
+    from oracle import ref_cpu
+    np.testing.assert_allclose(sum_gaussians(y, gaus), ref_cpu.sum_gaussians(y, gaus), rtol=1e-12, atol=1e-15)
+    with pytest.raises(ValueError):
+        sum_gaussians(y[:50], gaus)
+
+
+@pytest.mark.gpu
+def test_prob_surface_on_gpu_edge_rows():
+    """Skipped rows (no finite pair, odd count), misaligned compaction, a single Gaussian, zero span."""
+    import gpfit
+    from oracle import ref_cpu
+    inf = np.inf
+    tails = np.array([[0.5, 0.1, inf, inf],      # one experiment
+                      [inf, inf, inf, inf],      # nothing finite: skipped
+                      [0.5, inf, 0.7, 0.2],      # odd count: skipped
+                      [0.5, 0.1, 0.7, 0.2],      # two experiments
+                      [inf, 0.3, 0.4, inf],      # compaction pairs (0.3, 0.4)
+                      [1e3, 1e-3, -2.0, 5.0]])   # wide span
+    vals = np.concatenate([np.zeros((len(tails), 2)), tails], axis=1)
+    rows, ys, ps = ref_cpu.prob_surface(vals, 2)
+    y, p, ok = gpfit.default_context().prob_surface(tails)
+    assert list(np.nonzero(ok)[0]) == list(rows)
+    np.testing.assert_array_equal(y[ok], ys)
+    np.testing.assert_allclose(p[ok], ps, rtol=1e-12, atol=1e-15)
 
 
 def test_read_in_matches_reference_loader(f2, tmp_path, monkeypatch):
