@@ -268,6 +268,107 @@ __device__ void gemm_stream(Acc<TM>& acc, const double* __restrict__ Ap, int lda
   }
 }
 
+// ----------------------------------------------------------------------------
+// Direct-to-LDS streaming GEMM, TM = 128: acc (+/-)= A(128 x K) B(K x 128) with
+//   A (r,k) at Ap[r*lda + k]                 (row panel, k contiguous)
+//   B (k,c) at Bp[c*ldb + k]   (!NN: B^T given as a row panel, stored like A)
+//           at Bp[k*ldb + c]   ( NN: B given as a row panel)
+// Chunks of KC = 16 go global -> LDS by global_load_lds_dwordx4 (no VGPR staging, no
+// ds_write; the loads of chunk t+1 stay in flight across the chunk-t MFMAs); one barrier per
+// chunk. Each wave instruction fills one 1 KiB block with 16 B per lane in lane order, so the
+// bank-conflict-free layout is made by choosing which global pair each lane fetches (XOR
+// swizzles):
+//   [r][k] panels: 8 rows x 8 k-pairs per block; pair kp of row r sits in slot kp ^ (r % 8),
+//                  so the 16 rows of an MFMA operand read spread over the banks;
+//   [k][c] panels: one k-row per block; column pair cp of row k sits in slot cp ^ 8 (k % 4),
+//                  so the 4 k-rows of an operand read land 128 B apart.
+// NEG negates through the MFMA's own A-negate modifier. LDS: 2 x 2 x 128 x 16 doubles = 64 KiB.
+// ----------------------------------------------------------------------------
+constexpr int DL_KC = 16;
+constexpr int DL_BUF = 2 * 128 * DL_KC;  // one stage (A + B), doubles
+constexpr int DL_STAGE = 2 * DL_BUF;     // double-buffered
+
+__device__ __forceinline__ d4 mfma_neg_a(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 1);  // blgp bit 0 = negate A (f64)
+}
+
+__device__ __forceinline__ void dl_load(const double* g, double* l) {
+  __builtin_amdgcn_global_load_lds((const void*)g, (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+template <bool NN>
+__device__ __forceinline__ void dl_issue(const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
+                                         int ldb, int k0, double* sbuf, int wave, int lane) {
+  // 16 blocks of 1 KiB per operand per chunk; wave w issues blocks 2w and 2w+1 of each
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int blk = 2 * wave + u;
+    {
+      const int row = 8 * blk + (lane >> 3), kp = (lane & 7) ^ (row & 7);
+      dl_load(Ap + (size_t)row * lda + k0 + 2 * kp, sbuf + blk * 8 * DL_KC);
+    }
+    double* sB = sbuf + 128 * DL_KC;
+    if (!NN) {
+      const int row = 8 * blk + (lane >> 3), kp = (lane & 7) ^ (row & 7);
+      dl_load(Bp + (size_t)row * ldb + k0 + 2 * kp, sB + blk * 8 * DL_KC);
+    } else {
+      const int k = blk, cp = lane ^ (8 * (k & 3));
+      dl_load(Bp + (size_t)(k0 + k) * ldb + 2 * cp, sB + k * 128);
+    }
+  }
+}
+
+template <bool NN, bool NEG, int TRI>
+__device__ __forceinline__ void dl_mma(Acc<128>& acc, const double* sA, const double* sB, const Quad<128>& qd, int k0) {
+  constexpr int MBR = Geo<128>::MBR, MBC = Geo<128>::MBC;
+  const int lr = qd.lane & 15, lk = qd.lane >> 4;
+#pragma unroll
+  for (int ks = 0; ks < DL_KC; ks += 4) {
+    const int k = ks + lk, kp = k >> 1, ko = k & 1;
+    double a[MBR], b[MBC];
+#pragma unroll
+    for (int mi = 0; mi < MBR; ++mi) {
+      const int row = qd.rb + mi * 16 + lr;
+      a[mi] = sA[row * DL_KC + 2 * (kp ^ (row & 7)) + ko];
+    }
+#pragma unroll
+    for (int ni = 0; ni < MBC; ++ni) {
+      const int col = qd.cb + ni * 16 + lr;
+      if (!NN)
+        b[ni] = sB[col * DL_KC + 2 * (kp ^ (col & 7)) + ko];
+      else
+        b[ni] = sB[k * 128 + 2 * ((col >> 1) ^ (8 * (k & 3))) + (col & 1)];
+    }
+#pragma unroll
+    for (int mi = 0; mi < MBR; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < MBC; ++ni)
+        if (tri_live<TRI>(qd.rb + mi * 16, qd.cb + ni * 16, k0 + ks))
+          acc.v[mi][ni] = NEG ? mfma_neg_a(a[mi], b[ni], acc.v[mi][ni]) : mfma(a[mi], b[ni], acc.v[mi][ni]);
+  }
+}
+
+template <bool NN, bool NEG = false, int TRI = TRI_NONE>
+__device__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
+                               int ldb, int K, double* smem, const Quad<128>& qd) {
+  const int nch = K / DL_KC;
+  if (nch <= 0) return;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  Ap = launder(Ap);
+  Bp = launder(Bp);
+  dl_issue<NN>(Ap, lda, Bp, ldb, 0, smem, wave, qd.lane);
+#pragma unroll 1
+  for (int t = 0; t < nch; ++t) {
+    // chunk t landed (own loads; barriers do not drain LDS-DMA) and everyone's are visible
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 < nch) dl_issue<NN>(Ap, lda, Bp, ldb, (t + 1) * DL_KC, smem + ((t + 1) & 1) * DL_BUF, wave, qd.lane);
+    const double* cur = smem + (t & 1) * DL_BUF;
+    dl_mma<NN, NEG, TRI>(acc, cur, cur + 128 * DL_KC, qd, t * DL_KC);
+  }
+  __syncthreads();
+}
+
 // 64x64x64 GEMM with both operands resident in LDS (8 waves, 32x16 each):
 //   A (r,k) at sA[r*la + k];  B (k,c) at sB[c*lb + k] (!NN) or sB[k*lb + c] (NN).
 template <bool NN>

@@ -535,7 +535,8 @@ __device__ __forceinline__ void step_tile(int b, int P, int ntl, int grp, int& p
   p = (gi * grp + (r - w * gs)) * 8 + xcd;
 }
 
-constexpr int STEP_SMEM = (Geo<T>::STAGE > DIAG_BASE) ? Geo<T>::STAGE : DIAG_BASE;  // ~72 KiB: two workgroups per CU
+constexpr int STEP_STAGE = (Geo<T>::STAGE > DL_STAGE) ? Geo<T>::STAGE : DL_STAGE;
+constexpr int STEP_SMEM = (STEP_STAGE > DIAG_BASE) ? STEP_STAGE : DIAG_BASE;  // ~72 KiB: two workgroups per CU
 constexpr int STEP_SMALL = (5 * T > DIAG_SMALL) ? 5 * T : DIAG_SMALL;  // z_J + reduction scratch, or the diagonal's
 static_assert(DIAG_BASE <= STEP_SMEM && DIAG_SMALL <= STEP_SMALL, "fused diagonal fits the step's LDS");
 constexpr int STEP_NTH = Geo<T>::NTH;     // 512 threads: 8 waves, 64x32 per wave
@@ -558,6 +559,19 @@ __device__ __forceinline__ unsigned long long realtime() {
   return t;
 }
 #endif
+
+#ifndef GPF_DL
+#define GPF_DL 1  // direct-to-LDS staging in the block-column GEMMs (build-time A/B knob)
+#endif
+template <bool NN, bool NEG = false, int TRI = TRI_NONE>
+__device__ __forceinline__ void step_gemm(Acc<T>& acc, const double* Ap, int lda, const double* Bp, int ldb, int K,
+                                          double* smem, const Quad<T>& qd) {
+#if GPF_DL
+  gemm_stream_dl<NN, NEG, TRI>(acc, Ap, lda, Bp, ldb, K, smem, qd);
+#else
+  gemm_stream<T, NN, NEG, TRI>(acc, Ap, lda, Bp, ldb, K, smem, qd);
+#endif
+}
 
 __device__ __forceinline__ void k_step_body(int J, int nt, int Npad, double* __restrict__ Lb, double* __restrict__ Ub,
                                             double* __restrict__ yb, double* __restrict__ s2p,
@@ -585,18 +599,18 @@ __device__ __forceinline__ void k_step_body(int J, int nt, int Npad, double* __r
     // C = A_IJ - L_I,<J L_J,<J^T (accumulator seeded with A_IJ, A operand staged negated)
     acc.load(qd, Aij, ld);
     if (J > 0)
-      gemm_stream<T, false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, J * T, smem, qd);
+      step_gemm<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, J * T, smem, qd);
     acc.store(qd, Aij, ld);
     __syncthreads();
     // L_IJ = C U_JJ^T
     acc.zero();
-    gemm_stream<T, false, false, TRI_B_KLEC>(acc, Aij, Npad, Ujj, Npad, T, smem, qd);
+    step_gemm<false, false, TRI_B_KLEC>(acc, Aij, Npad, Ujj, Npad, T, smem, qd);
     acc.store(qd, Aij, ld);
     if (tid < T) zj[tid] = yp[J * T + tid];
     __syncthreads();
     // look-ahead: A_II -= L_IJ L_IJ^T (the full tile; only its lower half is ever read), y_I -= L_IJ z_J
     acc.load(qd, Aii, ld);
-    gemm_stream<T, false, true, TRI_C_LOWER>(acc, Aij, Npad, Aij, Npad, T, smem, qd);
+    step_gemm<false, true, TRI_C_LOWER>(acc, Aij, Npad, Aij, Npad, T, smem, qd);
     acc.store(qd, Aii, ld);
     {
       const int r = tid & (T - 1), h = tid >> 7;  // 4 quarter-row partial dot products
@@ -624,14 +638,14 @@ __device__ __forceinline__ void k_step_body(int J, int nt, int Npad, double* __r
     Acc<T> acc;
     acc.zero();
     // W = L_J,[K,J) U_[K,J),K, parked in the U_JK slot
-    gemm_stream<T, true, false, TRI_B_KGEC>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
+    step_gemm<true, false, TRI_B_KGEC>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
                                             Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T, smem, qd);
     acc.store(qd, Ujk, ld);
     if (tid < T) zj[tid] = yp[J * T + tid];
     __syncthreads();
     // U_JK = -U_JJ W (A operand staged negated)
     acc.zero();
-    gemm_stream<T, true, true, TRI_A_KLER>(acc, Ujj, Npad, Ujk, Npad, T, smem, qd);
+    step_gemm<true, true, TRI_A_KLER>(acc, Ujj, Npad, Ujk, Npad, T, smem, qd);
     acc.store(qd, Ujk, ld);
     // column partials straight from the accumulators: sum over this wave's rows,
     // then the 4 lane groups, then the two row-halves of the tile (fixed order)
@@ -725,14 +739,18 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_gemm_benc
                                                                                    double* __restrict__ C) {
   __shared__ __attribute__((aligned(16))) double smem[STEP_SMEM];
   const int b = blockIdx.x;
-  const int p = (mode == 1) ? 0 : b % P, w = (mode == 1) ? 0 : b / P;
+  const bool shared = (mode & 1) != 0, direct = (mode & 2) != 0;  // 1/3: shared operands; 2/3: direct-to-LDS
+  const int p = shared ? 0 : b % P, w = shared ? 0 : b / P;
   const size_t ld = (size_t)Npad;
   const int J = D / T, I = J + 1 + w;
   const double* Lp = Lb + (size_t)p * ld * ld;
   const Quad<T> qd;
   Acc<T> acc;
   acc.zero();
-  gemm_stream<T, false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, D, smem, qd);
+  if (direct)
+    gemm_stream_dl<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, D, smem, qd);
+  else
+    gemm_stream<T, false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, D, smem, qd);
   acc.store(qd, C + (size_t)b * T * T, T);
 }
 

@@ -13,14 +13,14 @@ namespace gpf {
 __global__ __launch_bounds__(Geo<T>::NTH, 4) void k_predict_vsq(int Npad, const double* __restrict__ U,
                                                          const double* __restrict__ Ks, int ldks,
                                                          double* __restrict__ vsq) {
-  __shared__ __attribute__((aligned(16))) double smem[Geo<T>::STAGE];
+  __shared__ __attribute__((aligned(16))) double smem[DL_STAGE];
   __shared__ double half[T];
   const int q = blockIdx.x, t = blockIdx.y;
   const Quad<T> qd;
   Acc<T> acc;
   acc.zero();
   // U is lower triangular: row tile t needs columns [0, (t+1) * 128)
-  gemm_stream<T, true>(acc, U + (size_t)t * T * Npad, Npad, Ks + (size_t)q * T, ldks, (t + 1) * T, smem, qd);
+  gemm_stream_dl<true>(acc, U + (size_t)t * T * Npad, Npad, Ks + (size_t)q * T, ldks, (t + 1) * T, smem, qd);
   constexpr int MBR = Geo<T>::MBR, MBC = Geo<T>::MBC;
   const int wr = qd.wrow();
   double part[MBC];
