@@ -284,6 +284,9 @@ __device__ void gemm_stream(Acc<TM>& acc, const double* __restrict__ Ap, int lda
 //                  so the 4 k-rows of an operand read land 128 B apart.
 // NEG negates through the MFMA's own A-negate modifier. LDS: 2 x 2 x 128 x 16 doubles = 64 KiB.
 // ----------------------------------------------------------------------------
+#ifndef GPF_DL_PRIO
+#define GPF_DL_PRIO 0
+#endif
 constexpr int DL_KC = 16;
 constexpr int DL_BUF = 2 * 128 * DL_KC;  // one stage (A + B), doubles
 constexpr int DL_STAGE = 2 * DL_BUF;     // double-buffered
@@ -357,6 +360,9 @@ __device__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int
   Ap = launder(Ap);
   Bp = launder(Bp);
   dl_issue<NN>(Ap, lda, Bp, ldb, 0, smem, wave, qd.lane);
+#if GPF_DL_PRIO
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half (guide: 2 waves/SIMD)
+#endif
 #pragma unroll 1
   for (int t = 0; t < nch; ++t) {
     // chunk t landed (own loads; barriers do not drain LDS-DMA) and everyone's are visible
@@ -366,6 +372,9 @@ __device__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int
     const double* cur = smem + (t & 1) * DL_BUF;
     dl_mma<NN, NEG, TRI>(acc, cur, cur + 128 * DL_KC, qd, t * DL_KC);
   }
+#if GPF_DL_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
   __syncthreads();
 }
 

@@ -380,7 +380,8 @@ struct DiagSmem {
 // ----------------------------------------------------------------------------
 __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __restrict__ Ut, size_t ld,
                                           double* __restrict__ yseg, double* __restrict__ s2o,
-                                          double* __restrict__ szo, int* __restrict__ info, const DiagSmem& sm) {
+                                          double* __restrict__ szo, int* __restrict__ info, const DiagSmem& sm,
+                                          bool pad2) {
   const int tid = threadIdx.x;
   const Quad<64> qd;
   double* const t0 = sm.t0;
@@ -404,6 +405,26 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
   zero_tile64(Ut + H, ld);
   rows_dot64(sm.z, t1, LDH, sm.y, sm.scratch, false);          // z1 = U11 y1
   cols_partial64(sm.ps2, sm.psz, t1, LDH, sm.z, sm.scratch);   // U11 columns
+
+  if (pad2) {
+    // rows/columns 64..127 of this block are all padding (A21 = 0, A22 = I from the K build and
+    // no earlier column touches them): L21 = U21 = 0, L22 = U22 = I, z2 = 0 — exactly what the
+    // general path computes, without the second 64x64 factor
+    zero_tile64(Lt + (size_t)H * ld, ld);
+    zero_tile64(Ut + (size_t)H * ld, ld);
+    for (int i = tid; i < H * H; i += DNTH) {
+      const int r = i >> 6, c = i & 63;
+      Lt[(size_t)(H + r) * ld + H + c] = (r == c) ? 1.0 : 0.0;
+      Ut[(size_t)(H + r) * ld + H + c] = (r == c) ? 1.0 : 0.0;
+    }
+    if (tid < T) {
+      s2o[tid] = (tid < H) ? sm.ps2[tid] : 1.0;
+      szo[tid] = (tid < H) ? sm.psz[tid] : 0.0;
+      yseg[tid] = (tid < H) ? sm.z[tid] : 0.0;
+    }
+    if (bad && tid == 0 && *info == 0) *info = 1;
+    return;
+  }
 
   DIAG_STAMP(2);
   // (b) L21 = A21 U11^T
@@ -493,7 +514,7 @@ __device__ __forceinline__ DiagSmem carve_diag(double* base, double* small) {
 // all earlier block columns). Launched for J = 0 only; every later diagonal
 // block is factored inside k_step by the workgroup that finishes reducing it.
 // grid: (P)
-__global__ __launch_bounds__(DNTH) void k_diag(int J, int nt, int Npad, double* __restrict__ Lb,
+__global__ __launch_bounds__(DNTH) void k_diag(int J, int nt, int N, int Npad, double* __restrict__ Lb,
                                                   double* __restrict__ Ub, double* __restrict__ yb,
                                                   double* __restrict__ s2p, double* __restrict__ szp,
                                                   int* __restrict__ info) {
@@ -504,7 +525,8 @@ __global__ __launch_bounds__(DNTH) void k_diag(int J, int nt, int Npad, double* 
   const size_t off = (size_t)p * ld * ld + (size_t)J * T * ld + (size_t)J * T;
   const DiagSmem sm = carve_diag(tiles, small);
   const size_t poff = ((size_t)p * nt + J) * Npad + (size_t)J * T;
-  factor128(Lb + off, Ub + off, ld, yb + (size_t)p * Npad + J * T, s2p + poff, szp + poff, info + p, sm);
+  factor128(Lb + off, Ub + off, ld, yb + (size_t)p * Npad + J * T, s2p + poff, szp + poff, info + p, sm,
+            J * T + H >= N);
 }
 
 // ----------------------------------------------------------------------------
@@ -575,7 +597,8 @@ __device__ __forceinline__ void step_gemm(Acc<T>& acc, const double* Ap, int lda
 
 __device__ __forceinline__ void k_step_body(int J, int nt, int Npad, double* __restrict__ Lb, double* __restrict__ Ub,
                                             double* __restrict__ yb, double* __restrict__ s2p,
-                                            double* __restrict__ szp, int* __restrict__ info, int P, int grp) {
+                                            double* __restrict__ szp, int* __restrict__ info, int P, int grp,
+                                            int N) {
   __shared__ __attribute__((aligned(16))) double smem[STEP_SMEM];
   __shared__ __attribute__((aligned(16))) double small[STEP_SMALL];
   const int tid = threadIdx.x;
@@ -630,7 +653,8 @@ __device__ __forceinline__ void k_step_body(int J, int nt, int Npad, double* __r
 #if GPF_DIAG_PRIO
       __builtin_amdgcn_s_setprio(3);  // latency-critical: the next launch waits for this block
 #endif
-      factor128(Aii, Up + (size_t)I * T * ld + (size_t)I * T, ld, yp + I * T, s2p + poff, szp + poff, info + p, sm);
+      factor128(Aii, Up + (size_t)I * T * ld + (size_t)I * T, ld, yp + I * T, s2p + poff, szp + poff, info + p, sm,
+                I * T + H >= N);
     }
   } else {
     const int K = w - nL;
@@ -688,7 +712,7 @@ __device__ __forceinline__ void k_step_body(int J, int nt, int Npad, double* __r
 __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int J, int nt, int Npad, double* __restrict__ Lb,
                                                   double* __restrict__ Ub, double* __restrict__ yb,
                                                   double* __restrict__ s2p, double* __restrict__ szp,
-                                                  int* __restrict__ info, int P, int grp) {
+                                                  int* __restrict__ info, int P, int grp, int N) {
   const int tid = threadIdx.x;
 #ifdef GPF_WG_TRACE
   if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) {
@@ -699,7 +723,7 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
     g_wg_trace[J][blockIdx.x][2] = ((unsigned long long)xcc << 32) | hw;
   }
 #endif
-  k_step_body(J, nt, Npad, Lb, Ub, yb, s2p, szp, info, P, grp);
+  k_step_body(J, nt, Npad, Lb, Ub, yb, s2p, szp, info, P, grp, N);
 #ifdef GPF_WG_TRACE
   __syncthreads();
   if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) g_wg_trace[J][blockIdx.x][1] = realtime();

@@ -69,9 +69,11 @@ __device__ double pairwise_leaf(const double* a, int len) {
   return r;
 }
 
-__device__ double pairwise_sum_seq(const double* a, int n) {
-  // numpy recurses: n <= 128 is a leaf, else split at (n/2) rounded down to a
-  // multiple of 8 and return left + right. Explicit stack, same order.
+// numpy's recursion: n <= 128 is a leaf, else split at (n/2) rounded down to a multiple
+// of 8 and return left + right. Explicit stack, same order; `leaf(off, len)` supplies
+// the value of each leaf, visited left to right.
+template <typename Leaf>
+__device__ double pairwise_tree(int n, Leaf leaf) {
   int off[32], len[32], stage[32];
   double left[32];
   int sp = 0;
@@ -84,7 +86,7 @@ __device__ double pairwise_sum_seq(const double* a, int n) {
       off[sp + 1] = off[sp]; len[sp + 1] = half; stage[sp + 1] = 0;
       ++sp;
     }
-    double v = pairwise_leaf(a + off[sp], len[sp]);
+    double v = leaf(off[sp], len[sp]);
     for (;;) {
       if (sp == 0) return v;
       --sp;
@@ -102,6 +104,37 @@ __device__ double pairwise_sum_seq(const double* a, int n) {
   }
 }
 
+__device__ double pairwise_sum_seq(const double* a, int n) {
+  return pairwise_tree(n, [&](int off, int len) { return pairwise_leaf(a + off, len); });
+}
+
+// Same sum, leaves in parallel: thread 0 lists the leaves, one thread per leaf sums it,
+// thread 0 combines them in the tree's order. Block-wide (all threads call); the result
+// is returned in thread 0. Scratch: leaf tables of PW_LEAVES entries.
+constexpr int PW_LEAVES = 64;  // K <= KGRID_MAX = 4096 -> at most 64 leaves of >= 64
+__device__ double pairwise_sum_block(const double* a, int n, int* loff, int* llen, double* lsum, int* nleaf) {
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    int cnt = 0;
+    pairwise_tree(n, [&](int off, int len) {
+      loff[cnt] = off;
+      llen[cnt] = len;
+      ++cnt;
+      return 0.0;
+    });
+    *nleaf = cnt;
+  }
+  __syncthreads();
+  if (tid < *nleaf) lsum[tid] = pairwise_leaf(a + loff[tid], llen[tid]);
+  __syncthreads();
+  double r = 0.0;
+  if (tid == 0) {
+    int idx = 0;
+    r = pairwise_tree(n, [&](int, int) { return lsum[idx++]; });
+  }
+  return r;
+}
+
 // ----------------------------------------------------------------------------
 // Per particle score (find_len_scales.py:163-177, negated like evaluate_loss :182):
 //   coverage_k = count_k / N, W = trapz(|coverage - expected|, s) with numpy's
@@ -110,7 +143,7 @@ __device__ double pairwise_sum_seq(const double* a, int n) {
 // grid: (P)
 // ----------------------------------------------------------------------------
 __global__ __launch_bounds__(NTHR) void k_score(int N, int K, int d, const double* __restrict__ sig,
-                                                const double* __restrict__ expct, const int* __restrict__ hist,
+                                                const double* __restrict__ expct, int* __restrict__ hist,
                                                 const double* __restrict__ ls, const double* __restrict__ lo,
                                                 const double* __restrict__ hi, double* __restrict__ loss) {
   __shared__ int cnt[KGRID_MAX + 1];
@@ -118,12 +151,26 @@ __global__ __launch_bounds__(NTHR) void k_score(int N, int K, int d, const doubl
   __shared__ double term[KGRID_MAX];
   const int p = blockIdx.x;
   const int tid = threadIdx.x;
-  const int* h = hist + (size_t)p * (K + 1);
-  if (tid == 0) {
+  int* h = hist + (size_t)p * (K + 1);
+  // coverage counts = inclusive prefix sums of the histogram (exact integers: a block scan)
+  __shared__ int seg[NTHR];
+  {
+    const int per = (K + NTHR - 1) / NTHR, k0 = tid * per, k1 = min(K, k0 + per);
     int run = 0;
-    for (int k = 0; k < K; ++k) { run += h[k]; cnt[k] = run; }
+    for (int k = k0; k < k1; ++k) { run += h[k]; cnt[k] = run; }
+    seg[tid] = run;
+    __syncthreads();
+    for (int o = 1; o < NTHR; o <<= 1) {  // Hillis-Steele inclusive scan of the segment totals
+      const int v = (tid >= o) ? seg[tid - o] : 0;
+      __syncthreads();
+      seg[tid] += v;
+      __syncthreads();
+    }
+    const int base = (tid > 0) ? seg[tid - 1] : 0;
+    for (int k = k0; k < k1; ++k) cnt[k] += base;
   }
   __syncthreads();
+  for (int k = tid; k <= K; k += NTHR) h[k] = 0;  // leave the histogram zeroed for the next batch
   for (int k = tid; k < K; k += NTHR) {
     const double cov = (double)cnt[k] / (double)N;
     gap[k] = fabs(cov - expct[k]);
@@ -132,8 +179,11 @@ __global__ __launch_bounds__(NTHR) void k_score(int N, int K, int d, const doubl
   // trapezoid terms (np.trapezoid): (s[k+1]-s[k]) * (gap[k+1]+gap[k]) / 2
   for (int k = tid; k < K - 1; k += NTHR) term[k] = ((sig[k + 1] - sig[k]) * (gap[k + 1] + gap[k])) / 2.0;
   __syncthreads();
+  __shared__ int loff[PW_LEAVES], llen[PW_LEAVES], nleaf;
+  __shared__ double lsum[PW_LEAVES];
+  const double Wsum = pairwise_sum_block(term, K - 1, loff, llen, lsum, &nleaf);
   if (tid == 0) {
-    const double W = pairwise_sum_seq(term, K - 1);
+    const double W = Wsum;
     const double* l = ls + (size_t)p * d;
     double dmin = 0.0;
     for (int k = 0; k < d; ++k) {

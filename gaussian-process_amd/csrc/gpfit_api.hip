@@ -32,6 +32,7 @@ namespace {
 enum ProfClass { PC_PANEL = 0, PC_DIAG = 1, PC_BUILD = 2, PC_LOSS = 3, PC_FACTOR = 4, PC_PRED = 5, PC_PREDK = 6, PC_PSURF = 7, PC_N = 8 };
 
 constexpr int MAX_GROUPS = 4;  // particle groups factorised on concurrent streams
+constexpr int GRAPH_NT_MAX = 2;  // eval batches with N <= 256 run as a replayed HIP graph
 
 struct Pending {
   hipEvent_t a, b;
@@ -77,6 +78,12 @@ struct gpf_ctx {
   double* d_loss = nullptr;
   int* d_info = nullptr;
   int* d_hist = nullptr;
+  // pinned host staging for the per-batch transfers (async DMA, capturable in graphs)
+  double* h_ls = nullptr;
+  double* h_loss = nullptr;
+  int* h_info = nullptr;
+  // small-problem path: one captured graph per batch size (launch-latency bound regime)
+  std::vector<std::pair<int, hipGraphExec_t>> graphs;
 
   // profiling
   bool prof = false;
@@ -152,7 +159,16 @@ static void harvest(gpf_ctx* c) {
   c->pend.clear();
 }
 
+static void clear_graphs(gpf_ctx* c) {
+  for (auto& g : c->graphs) hipGraphExecDestroy(g.second);
+  c->graphs.clear();
+}
+
 static void free_work(gpf_ctx* c) {
+  clear_graphs(c);
+  hipHostFree(c->h_ls); hipHostFree(c->h_loss); hipHostFree(c->h_info);
+  c->h_ls = c->h_loss = nullptr;
+  c->h_info = nullptr;
   hipFree(c->d_L); hipFree(c->d_U); hipFree(c->d_yb); hipFree(c->d_s2p); hipFree(c->d_szp);
   hipFree(c->d_ls); hipFree(c->d_mu); hipFree(c->d_sd); hipFree(c->d_loss); hipFree(c->d_info);
   hipFree(c->d_hist);
@@ -195,6 +211,10 @@ static int ensure_work(gpf_ctx* c, int want) {
   GPF_HIP(c, hipMalloc(&c->d_loss, (size_t)cap * 8));
   GPF_HIP(c, hipMalloc(&c->d_info, (size_t)cap * 4));
   GPF_HIP(c, hipMalloc(&c->d_hist, (size_t)cap * (c->K + 1) * 4));
+  GPF_HIP(c, hipMemset(c->d_hist, 0, (size_t)cap * (c->K + 1) * 4));  // k_score re-zeroes what it read
+  GPF_HIP(c, hipHostMalloc((void**)&c->h_ls, (size_t)cap * std::max(c->d, 1) * 8, hipHostMallocDefault));
+  GPF_HIP(c, hipHostMalloc((void**)&c->h_loss, (size_t)cap * 8, hipHostMallocDefault));
+  GPF_HIP(c, hipHostMalloc((void**)&c->h_info, (size_t)cap * 4, hipHostMallocDefault));
   c->cap = cap;
   return GPF_OK;
 }
@@ -266,12 +286,12 @@ static int run_factor(gpf_ctx* c, int pc) {
     const double* lsg = c->d_ls + (size_t)p0 * c->d;
     int rc = launch_on(c, st, PC_BUILD, 8.0 * ntri * BT * BT * (double)gc, [&] {
       hipLaunchKernelGGL(gpf::k_build_cov, dim3(ntri, gc), dim3(NTHR), 0, st, N, Np, c->d, c->d_x, c->d_y, c->d_e,
-                         lsg, Lg, yg);
+                         lsg, Lg, yg, ig);
     });
     if (rc) return rc;
     // potrf + trtri of the first 128 block: 2/3 T^3 (later blocks are fused into k_step)
     rc = launch_on(c, st, PC_DIAG, (2.0 / 3.0) * t3 * gc, [&] {
-      hipLaunchKernelGGL(gpf::k_diag, dim3(gc), dim3(gpf::DNTH), 0, st, 0, nt, Np, Lg, Ug, yg, s2g, szg, ig);
+      hipLaunchKernelGGL(gpf::k_diag, dim3(gc), dim3(gpf::DNTH), 0, st, 0, nt, N, Np, Lg, Ug, yg, s2g, szg, ig);
     });
     if (rc) return rc;
     total += (2.0 / 3.0) * t3 * gc;
@@ -286,7 +306,7 @@ static int run_factor(gpf_ctx* c, int pc) {
         hipLaunchKernelGGL(gpf::k_step, dim3(gc * (nt - 1)), dim3(gpf::STEP_NTH), 0, st, J, nt, Np,
                            c->d_L + (size_t)p0 * ld * ld, c->d_U + (size_t)p0 * ld * ld, c->d_yb + (size_t)p0 * ld,
                            c->d_s2p + (size_t)p0 * nt * ld, c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc,
-                           step_group(gc));
+                           step_group(gc), N);
       });
       if (rc) return rc;
       total += fl * gc;
@@ -429,33 +449,79 @@ int gpf_eval_batch(gpf_ctx* c, const double* ls, int P, double* loss, double* mu
     }
   }
   if (act.empty()) return GPF_OK;
-  int rc = ensure_work(c, (int)act.size());
-  if (rc) return rc;
-  const int cap = c->cap;
-  std::vector<double> hls((size_t)cap * d), hloss(cap);
-  std::vector<int> hinfo(cap);
-  std::vector<double> hmu, hsd;
-  if (mu) hmu.resize((size_t)cap * Np);
-  if (sd) hsd.resize((size_t)cap * Np);
-  for (size_t s = 0; s < act.size(); s += cap) {
-    const int pc = (int)std::min<size_t>(cap, act.size() - s);
-    for (int q = 0; q < pc; ++q)
-      for (int k = 0; k < d; ++k) hls[(size_t)q * d + k] = ls[(size_t)act[s + q] * d + k];
-    GPF_HIP(c, hipMemcpyAsync(c->d_ls, hls.data(), (size_t)pc * d * 8, hipMemcpyHostToDevice, c->stream));
-    GPF_HIP(c, hipMemsetAsync(c->d_info, 0, (size_t)pc * 4, c->stream));
-    GPF_HIP(c, hipMemsetAsync(c->d_hist, 0, (size_t)pc * (c->K + 1) * 4, c->stream));
-    rc = run_factor(c, pc);
-    if (rc) return rc;
-    rc = launch(c, PC_LOSS, 0.0, [&] {
+  // Enqueue one chunk of pc particles whose length scales are staged in c->h_ls.
+  auto enqueue = [&](int pc) -> int {
+    GPF_HIP(c, hipMemcpyAsync(c->d_ls, c->h_ls, (size_t)pc * d * 8, hipMemcpyHostToDevice, c->stream));
+    int r = run_factor(c, pc);
+    if (r) return r;
+    r = launch(c, PC_LOSS, 0.0, [&] {
       hipLaunchKernelGGL(gpf::k_points, dim3((unsigned)((N + NTHR - 1) / NTHR), pc), dim3(NTHR), 0, c->stream,
                          (int)N, (int)Np, c->nt, c->K, c->d_y, c->d_e, c->d_sig, c->d_s2p, c->d_szp, c->d_mu,
                          c->d_sd, c->d_hist);
       hipLaunchKernelGGL(gpf::k_score, dim3(pc), dim3(NTHR), 0, c->stream, (int)N, c->K, d, c->d_sig, c->d_exp,
                          c->d_hist, c->d_ls, c->d_lo, c->d_hi, c->d_loss);
     });
+    if (r) return r;
+    GPF_HIP(c, hipMemcpyAsync(c->h_loss, c->d_loss, (size_t)pc * 8, hipMemcpyDeviceToHost, c->stream));
+    GPF_HIP(c, hipMemcpyAsync(c->h_info, c->d_info, (size_t)pc * 4, hipMemcpyDeviceToHost, c->stream));
+    return GPF_OK;
+  };
+  // Small problems are launch-latency bound: the whole batch (copies + ~5 kernels) is
+  // captured once per batch size as a HIP graph and replayed. The batch is padded to all P
+  // slots (spare slots repeat an active particle) so one graph serves every PSO iteration.
+  const bool graph = !c->prof && !mu && !sd && c->nt <= GRAPH_NT_MAX && getenv("GPF_NO_GRAPH") == nullptr;
+  if (graph) {
+    int rc = ensure_work(c, P);
     if (rc) return rc;
-    GPF_HIP(c, hipMemcpyAsync(hloss.data(), c->d_loss, (size_t)pc * 8, hipMemcpyDeviceToHost, c->stream));
-    GPF_HIP(c, hipMemcpyAsync(hinfo.data(), c->d_info, (size_t)pc * 4, hipMemcpyDeviceToHost, c->stream));
+    if (c->cap >= P) {
+      for (int q = 0; q < P; ++q) {
+        const int src = act[q < (int)act.size() ? q : 0];
+        for (int k = 0; k < d; ++k) c->h_ls[(size_t)q * d + k] = ls[(size_t)src * d + k];
+      }
+      hipGraphExec_t ge = nullptr;
+      for (auto& g : c->graphs)
+        if (g.first == P) ge = g.second;
+      if (!ge) {
+        GPF_HIP(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        const int rq = enqueue(P);
+        hipGraph_t gr = nullptr;
+        const hipError_t ec = hipStreamEndCapture(c->stream, &gr);
+        if (rq) {
+          if (gr) hipGraphDestroy(gr);
+          return rq;
+        }
+        GPF_HIP(c, ec);
+        const hipError_t ei = hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0);
+        hipGraphDestroy(gr);
+        GPF_HIP(c, ei);
+        c->graphs.push_back({P, ge});
+      }
+      GPF_HIP(c, hipGraphLaunch(ge, c->stream));
+      GPF_HIP(c, hipStreamSynchronize(c->stream));
+      c->evals += (double)act.size();
+      for (size_t q = 0; q < act.size(); ++q) {
+        if (c->h_info[q] != 0) {
+          if (bad_idx) *bad_idx = act[q];
+          c->err = "Matrix is not positive definite";
+          return GPF_NOT_PD;
+        }
+        loss[act[q]] = c->h_loss[q];
+      }
+      return GPF_OK;
+    }
+  }
+  int rc = ensure_work(c, (int)act.size());
+  if (rc) return rc;
+  const int cap = c->cap;
+  std::vector<double> hmu, hsd;
+  if (mu) hmu.resize((size_t)cap * Np);
+  if (sd) hsd.resize((size_t)cap * Np);
+  for (size_t s = 0; s < act.size(); s += cap) {
+    const int pc = (int)std::min<size_t>(cap, act.size() - s);
+    for (int q = 0; q < pc; ++q)
+      for (int k = 0; k < d; ++k) c->h_ls[(size_t)q * d + k] = ls[(size_t)act[s + q] * d + k];
+    rc = enqueue(pc);
+    if (rc) return rc;
     if (mu) GPF_HIP(c, hipMemcpyAsync(hmu.data(), c->d_mu, (size_t)pc * Np * 8, hipMemcpyDeviceToHost, c->stream));
     if (sd) GPF_HIP(c, hipMemcpyAsync(hsd.data(), c->d_sd, (size_t)pc * Np * 8, hipMemcpyDeviceToHost, c->stream));
     GPF_HIP(c, hipStreamSynchronize(c->stream));
@@ -463,12 +529,12 @@ int gpf_eval_batch(gpf_ctx* c, const double* ls, int P, double* loss, double* mu
     c->evals += pc;
     for (int q = 0; q < pc; ++q) {
       const int p = act[s + q];
-      if (hinfo[q] != 0) {
+      if (c->h_info[q] != 0) {
         if (bad_idx) *bad_idx = p;
         c->err = "Matrix is not positive definite";
         return GPF_NOT_PD;
       }
-      loss[p] = hloss[q];
+      loss[p] = c->h_loss[q];
       if (mu) std::memcpy(mu + (size_t)p * N, hmu.data() + (size_t)q * Np, (size_t)N * 8);
       if (sd) std::memcpy(sd + (size_t)p * N, hsd.data() + (size_t)q * Np, (size_t)N * 8);
     }
@@ -626,7 +692,7 @@ int gpf_log_marginal_likelihood(gpf_ctx* c, const double* ls, double* out) {
 
 int gpf_set_profiling(gpf_ctx* c, int on) {
   if (!c) return GPF_BAD_ARG;
-  c->prof = on != 0;
+  c->prof = on != 0;  // (profiled batches take the plain launch path, never a graph)
   return GPF_OK;
 }
 
