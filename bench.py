@@ -134,6 +134,34 @@ def predict_line(ctx, x, y, e, N, d, args):
     return out
 
 
+def hull_line(ctx, args):
+    """Secondary measurement, SURVEY.md §8f row 3: the prediction grid of GP_fit.py:31
+    (convex_hull.fill_convex_hull) for 2-D and 3-D hulls; the facet rasterisation stays on
+    the host, the d fill passes run on the GPU (gpf_hull_fill)."""
+    sys.path.insert(0, str(ROOT / "gaussian-process_amd"))
+    import convex_hull
+    rng = np.random.default_rng(args.seed + 3)
+    cases = [("2-D, 21 points, res 0.005", rng.uniform([1.2, -1.0], [2.0, 1.0], size=(21, 2)), [0.005, 0.005]),
+             ("3-D, 12 points, res 0.02", rng.uniform(0.0, 1.0, size=(12, 3)), [0.02, 0.02, 0.02])]
+    out = []
+    for name, pts, res in cases:
+        convex_hull.fill_convex_hull(pts, res)  # warm-up
+        t0 = time.perf_counter()
+        g = convex_hull.fill_convex_hull(pts, res)
+        dt = time.perf_counter() - t0
+        item = {"case": name, "grid_points": int(g.shape[0]), "ms": dt * 1e3, "points_per_s": g.shape[0] / dt}
+        if not args.no_cpu:
+            from oracle import ref_hull  # CPU baseline leg only
+            t1 = time.perf_counter()
+            ref = ref_hull.fill_convex_hull(pts, res)
+            cdt = time.perf_counter() - t1
+            item["cpu_baseline"] = {"ms": cdt * 1e3, "kind": "port", "cores": 1,
+                                    "sample": "oracle/ref_hull.py (convex_hull.py restated, pure Python), full case"}
+            item["identical"] = bool(np.array_equal(ref, g))
+        out.append(item)
+    return out
+
+
 def psurf_line(ctx, args):
     """Secondary measurement, SURVEY.md §8f row 4: probability surface of a merged frame of
     `psurf_rows` grid rows x 4 experiments (calc_prob_surf.py:15-30,67-81), kernel time from
@@ -188,6 +216,7 @@ def main():
     ap.add_argument("--predict-points", type=int, default=10000,
                     help="secondary (SURVEY.md §8f row 1): GP prediction at this many query points, 0 = skip")
     ap.add_argument("--cpu-predict-points", type=int, default=256, help="CPU GP sample for the prediction line")
+    ap.add_argument("--no-hull", action="store_true", help="skip the convex-hull grid line (SURVEY.md §8f row 3)")
     ap.add_argument("--psurf-rows", type=int, default=100000,
                     help="secondary (SURVEY.md §8f row 4): probability-surface rows, 0 = skip")
     args = ap.parse_args()
@@ -297,6 +326,9 @@ def main():
     psurf = None
     if rank == 0 and args.psurf_rows > 0:
         psurf = psurf_line(ctx, args)
+    hull = None
+    if rank == 0 and not args.no_hull:
+        hull = hull_line(ctx, args)
 
     if rank == 0 and not args.no_cpu and args.cpu_sample > 0:
         rng = np.random.default_rng(args.seed + 7)
@@ -323,6 +355,7 @@ def main():
             "pso_loop": pso,
             "predict": predict,
             "prob_surface": psurf,
+            "hull_grid": hull,
             "roofline": roof,
             "cpu_baseline": cpu,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,

@@ -22,6 +22,7 @@
 #include "gpf_objective.hip"
 #include "gpf_predict.hip"
 #include "gpf_probsurf.hip"
+#include "gpf_hull.hip"
 
 using gpf::BT;
 using gpf::NTHR;
@@ -82,6 +83,9 @@ struct gpf_ctx {
   double* h_ls = nullptr;
   double* h_loss = nullptr;
   int* h_info = nullptr;
+  // last convex-hull grid (gpf_hull_fill -> gpf_hull_fetch)
+  std::vector<double> hull_rows;
+  int hull_d = 0;
   // small-problem path: one captured graph per batch size (launch-latency bound regime)
   std::vector<std::pair<int, hipGraphExec_t>> graphs;
 
@@ -322,6 +326,58 @@ static int run_factor(gpf_ctx* c, int pc) {
     hipEventRecord(wb, c->stream);
     c->pend.push_back({wa, wb, PC_FACTOR, total});
   }
+  return GPF_OK;
+}
+
+// ---- convex-hull grid fill helpers (convex_hull.py:122-155,203-224) ----
+namespace {
+struct DevBuf {  // owning device allocation
+  void* p = nullptr;
+  ~DevBuf() { if (p) hipFree(p); }
+  template <typename V> V* as() { return static_cast<V*>(p); }
+};
+inline unsigned blocks_for(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + NTHR - 1) / NTHR); }
+}  // namespace
+
+// Sort rows (n x d, device) lexicographically by columns order[0], order[1], ... (stable LSD
+// sequence of radix sorts) and drop repeated rows; rows/n are replaced by the result.
+static int hull_sort_unique(gpf_ctx* c, DevBuf& rows, int64_t& n, int d, const int* order) {
+  hipStream_t st = c->stream;
+  DevBuf perm, perm2, key, key2, flag, pos, temp, out;
+  GPF_HIP(c, hipMalloc(&perm.p, std::max<int64_t>(n, 1) * 8));
+  GPF_HIP(c, hipMalloc(&perm2.p, std::max<int64_t>(n, 1) * 8));
+  GPF_HIP(c, hipMalloc(&key.p, std::max<int64_t>(n, 1) * 8));
+  GPF_HIP(c, hipMalloc(&key2.p, std::max<int64_t>(n, 1) * 8));
+  hipLaunchKernelGGL(gpf::k_hull_iota, dim3(blocks_for(n)), dim3(NTHR), 0, st, perm.as<int64_t>(), n);
+  size_t tb = 0, tb2 = 0;
+  GPF_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key.as<uint64_t>(), key2.as<uint64_t>(),
+                                                perm.as<int64_t>(), perm2.as<int64_t>(), n, 0, 64, st));
+  GPF_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, perm.as<int64_t>(), perm2.as<int64_t>(), n, st));
+  GPF_HIP(c, hipMalloc(&temp.p, std::max<size_t>(std::max(tb, tb2), 16)));
+  for (int q = d - 1; q >= 0; --q) {
+    hipLaunchKernelGGL(gpf::k_hull_key, dim3(blocks_for(n)), dim3(NTHR), 0, st, rows.as<double>(),
+                       perm.as<int64_t>(), n, d, order[q], key.as<uint64_t>());
+    GPF_HIP(c, hipcub::DeviceRadixSort::SortPairs(temp.p, tb, key.as<uint64_t>(), key2.as<uint64_t>(),
+                                                  perm.as<int64_t>(), perm2.as<int64_t>(), n, 0, 64, st));
+    std::swap(perm.p, perm2.p);
+  }
+  GPF_HIP(c, hipMalloc(&flag.p, std::max<int64_t>(n, 1) * 8));
+  GPF_HIP(c, hipMalloc(&pos.p, std::max<int64_t>(n, 1) * 8));
+  hipLaunchKernelGGL(gpf::k_hull_flag, dim3(blocks_for(n)), dim3(NTHR), 0, st, rows.as<double>(), perm.as<int64_t>(),
+                     n, d, flag.as<int64_t>());
+  GPF_HIP(c, hipcub::DeviceScan::ExclusiveSum(temp.p, tb2, flag.as<int64_t>(), pos.as<int64_t>(), n, st));
+  int64_t last[2] = {0, 0};
+  GPF_HIP(c, hipMemcpyAsync(&last[0], pos.as<int64_t>() + (n - 1), 8, hipMemcpyDeviceToHost, st));
+  GPF_HIP(c, hipMemcpyAsync(&last[1], flag.as<int64_t>() + (n - 1), 8, hipMemcpyDeviceToHost, st));
+  GPF_HIP(c, hipStreamSynchronize(st));
+  const int64_t m = last[0] + last[1];
+  GPF_HIP(c, hipMalloc(&out.p, std::max<int64_t>(m, 1) * d * 8));
+  hipLaunchKernelGGL(gpf::k_hull_compact, dim3(blocks_for(n)), dim3(NTHR), 0, st, rows.as<double>(),
+                     perm.as<int64_t>(), flag.as<int64_t>(), pos.as<int64_t>(), n, d, out.as<double>());
+  GPF_HIP(c, hipGetLastError());
+  GPF_HIP(c, hipStreamSynchronize(st));
+  std::swap(rows.p, out.p);
+  n = m;
   return GPF_OK;
 }
 
@@ -816,6 +872,69 @@ int gpf_prob_surface(gpf_ctx* c, const double* tails, int64_t M, int E, double* 
   if (rc == GPF_HIP_ERROR && c->err.empty()) c->err = "gpf_prob_surface: HIP error";
   hipFree(dt); hipFree(dy); hipFree(dp); hipFree(dok);
   return rc;
+}
+
+// ---- convex-hull grid fill (convex_hull.py:122-155,203-224; helpers above the C-ABI block) ----
+int gpf_hull_fill(gpf_ctx* c, const double* shell, int64_t n, int d, const double* res, const int* decimals,
+                  int64_t* m_out) {
+  if (!c) return GPF_BAD_ARG;
+  if (n <= 0 || d <= 0 || d > gpf::DMAX || !shell || !res || !decimals || !m_out)
+    return bad_arg(c, "gpf_hull_fill: bad arguments");
+  hipSetDevice(c->device);
+  gpf::HullDims hd{};
+  hd.d = d;
+  for (int j = 0; j < d; ++j) {
+    if (!(res[j] > 0.0)) return bad_arg(c, "gpf_hull_fill: resolution must be > 0");
+    hd.res[j] = res[j];
+    hd.p10[j] = (res[j] < 1.0 && decimals[j] >= 0) ? std::pow(10.0, decimals[j]) : 0.0;
+  }
+  hipStream_t st = c->stream;
+  DevBuf rows;
+  GPF_HIP(c, hipMalloc(&rows.p, (size_t)n * d * 8));
+  GPF_HIP(c, hipMemcpyAsync(rows.p, shell, (size_t)n * d * 8, hipMemcpyHostToDevice, st));
+  std::vector<int> order(d);
+  for (int j = 0; j < d; ++j) order[j] = j;
+  int rc = hull_sort_unique(c, rows, n, d, order.data());
+  if (rc) return rc;
+  for (int i = 0; i < d; ++i) {
+    // pass i: the grid is sorted by columns i, i+1, .., i-1 (mod d); fill along the last of them
+    hd.axis = (d - 1 + i) % d;
+    DevBuf cnt, off, temp, grown;
+    GPF_HIP(c, hipMalloc(&cnt.p, (size_t)n * 8));
+    GPF_HIP(c, hipMalloc(&off.p, (size_t)n * 8));
+    hipLaunchKernelGGL(gpf::k_hull_count, dim3(blocks_for(n)), dim3(NTHR), 0, st, rows.as<double>(), n, hd,
+                       cnt.as<int64_t>());
+    size_t tb = 0;
+    GPF_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt.as<int64_t>(), off.as<int64_t>(), n, st));
+    GPF_HIP(c, hipMalloc(&temp.p, std::max<size_t>(tb, 16)));
+    GPF_HIP(c, hipcub::DeviceScan::ExclusiveSum(temp.p, tb, cnt.as<int64_t>(), off.as<int64_t>(), n, st));
+    int64_t last[2] = {0, 0};
+    GPF_HIP(c, hipMemcpyAsync(&last[0], off.as<int64_t>() + (n - 1), 8, hipMemcpyDeviceToHost, st));
+    GPF_HIP(c, hipMemcpyAsync(&last[1], cnt.as<int64_t>() + (n - 1), 8, hipMemcpyDeviceToHost, st));
+    GPF_HIP(c, hipStreamSynchronize(st));
+    const int64_t add = last[0] + last[1];
+    GPF_HIP(c, hipMalloc(&grown.p, (size_t)(n + add) * d * 8));
+    GPF_HIP(c, hipMemcpyAsync(grown.p, rows.p, (size_t)n * d * 8, hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(gpf::k_hull_emit, dim3(blocks_for(n)), dim3(NTHR), 0, st, rows.as<double>(), n, hd,
+                       off.as<int64_t>(), grown.as<double>() + (size_t)n * d);
+    GPF_HIP(c, hipGetLastError());
+    std::swap(rows.p, grown.p);
+    n += add;
+    for (int j = 0; j < d; ++j) order[j] = (i + 1 + j) % d;
+    rc = hull_sort_unique(c, rows, n, d, order.data());
+    if (rc) return rc;
+  }
+  c->hull_rows.resize((size_t)n * d);
+  GPF_HIP(c, hipMemcpy(c->hull_rows.data(), rows.p, (size_t)n * d * 8, hipMemcpyDeviceToHost));
+  c->hull_d = d;
+  *m_out = n;
+  return GPF_OK;
+}
+
+int gpf_hull_fetch(gpf_ctx* c, double* out) {
+  if (!c || !out) return GPF_BAD_ARG;
+  if (!c->hull_rows.empty()) std::memcpy(out, c->hull_rows.data(), c->hull_rows.size() * 8);
+  return GPF_OK;
 }
 
 // Measurement hook: TF/s of the k_step L-tile GEMM core alone (k_gemm_bench) on

@@ -43,6 +43,9 @@ SIGNATURES = {
     "gpf_mfma_peak": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _dp]),
     "gpf_prob_surface": (ctypes.c_int, [_vp, _dp, ctypes.c_int64, ctypes.c_int, _dp, _dp,
                                         ctypes.POINTER(ctypes.c_int)]),
+    "gpf_hull_fill": (ctypes.c_int, [_vp, _dp, ctypes.c_int64, ctypes.c_int, _dp, ctypes.POINTER(ctypes.c_int),
+                                     ctypes.POINTER(ctypes.c_int64)]),
+    "gpf_hull_fetch": (ctypes.c_int, [_vp, _dp]),
     "gpf_gemm_bench": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_int, _dp]),
 }
@@ -231,6 +234,23 @@ class Context:
         self._check(self.lib.gpf_prob_surface(self._h, _ptr(t), m, e, _ptr(y), _ptr(p),
                                               ok.ctypes.data_as(ctypes.POINTER(ctypes.c_int))), "gpf_prob_surface")
         return y, p, ok.astype(bool)
+
+    def hull_fill(self, shell_rows, res, decimals):
+        """The d sort + scan-fill passes of fill_convex_hull on the GPU (gpf_hull_fill): rows
+        (m, d) sorted lexicographically."""
+        rows = _f64(shell_rows)
+        n, d = rows.shape
+        r = _f64(res).reshape(-1)
+        dec = np.ascontiguousarray(decimals, dtype=np.int32).reshape(-1)
+        if r.shape[0] != d or dec.shape[0] != d:
+            raise ValueError("res and decimals need one entry per dimension")
+        m = ctypes.c_int64(0)
+        self._check(self.lib.gpf_hull_fill(self._h, _ptr(rows), n, d, _ptr(r),
+                                           dec.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), ctypes.byref(m)),
+                    "gpf_hull_fill")
+        out = np.empty((m.value, d))
+        self._check(self.lib.gpf_hull_fetch(self._h, _ptr(out)), "gpf_hull_fetch")
+        return out
 
     def gemm_bench(self, mode=0, npad=4096, particles=64, tiles=15, depth=2048, iters=5):
         """TF/s of the block-column GEMM core alone (gpf_gemm_bench)."""

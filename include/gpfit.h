@@ -99,6 +99,16 @@ int gpf_log_marginal_likelihood(gpf_ctx* ctx, const double* ls, double* out);
  * 2 or an odd number of finite entries, calc_prob_surf.py:71-73), else 1. E <= 1024. */
 int gpf_prob_surface(gpf_ctx* ctx, const double* tails, int64_t M, int E, double* y, double* p, int* ok);
 
+/* Convex-hull grid fill (replaces the fill passes of convex_hull.py:122-155,203-224; SURVEY.md
+ * §8f row 3). shell: n x d rows (row-major) = the rasterised hull facets (the reference's
+ * concatenated facet surfaces, convex_hull.py:215-217); res: the d resolutions; decimals: the
+ * digits after the point of str(res[j]) (numpy.around in round_to_res, convex_hull.py:13-24).
+ * Runs the d sort + scan-fill passes and keeps the grid; *m = its row count. gpf_hull_fetch
+ * copies it (m x d, rows sorted lexicographically, as fill_convex_hull returns them). */
+int gpf_hull_fill(gpf_ctx* ctx, const double* shell, int64_t n, int d, const double* res, const int* decimals,
+                  int64_t* m);
+int gpf_hull_fetch(gpf_ctx* ctx, double* out);
+
 /* ---- measurement hooks (bench.py) ---- */
 
 /* Enable per-kernel-class HIP event timing on the context's stream. */

@@ -1,16 +1,12 @@
-"""Drop-in for the reference's convex_hull.py: the prediction grid of GP_fit.py:31.
+"""CPU oracle for the convex-hull grid — TEST INFRASTRUCTURE ONLY.
 
-SURVEY.md §8f row 3. The Qhull facets are rasterised onto the per-dimension resolution
-grid on the host (short sequential walks, convex_hull.py:38-174); the d sort + scan-fill
-passes over the whole grid, where the reference spends ~95% of its time, run on the
-MI355X (gpf_hull_fill, csrc/gpf_hull.hip). Same snapping rule and traversal order as
-convex_hull.py:13-224, so the grid is identical point for point (tests/test_host_glue.py,
-fixtures F6).
+A restatement of convex_hull.py:13-224: Qhull facets rasterised onto the resolution grid,
+then the hull filled by scan lines, one dimension at a time, with the reference's snapping
+rule and traversal order. Pinned to fixtures F6 (the reference's own output, point for
+point); the checker of gpf_hull_fill. Only tests/ and bench.py's CPU baseline leg use it.
 """
 import numpy as np
 from scipy.spatial import ConvexHull
-
-from gpfit import default_context
 
 __all__ = ["fill_convex_hull", "round_to_res"]
 
@@ -100,9 +96,13 @@ def fill_convex_hull(points, step):
     """Grid points (rows) filling the convex hull of `points` (n, d) at resolution `step`
     (convex_hull.py:203-224)."""
     points = np.asarray(points)
-    res = np.asarray(step, dtype=np.float64).reshape(-1)
+    res = step
     hull = ConvexHull(points)
-    shells = np.concatenate([_facet_surface(points[list(simplex)], res) for simplex in hull.simplices])
-    decimals = [_decimals(r) for r in res]
-    # d passes: fill along the last column, rotate the columns left by one (convex_hull.py:218-223)
-    return default_context().hull_fill(shells.astype(np.float64), res, decimals)
+    shells = [_facet_surface(points[list(simplex)], res) for simplex in hull.simplices]
+    grid = _unique_rows(np.concatenate(shells))
+    for _ in range(grid.shape[1]):
+        # fill along the last column, then rotate the columns left by one (and the steps with them)
+        grid = _scanfill(grid.shape[1] - 1, grid, res)
+        grid = _unique_rows(np.concatenate((grid[:, 1:].T, grid[:, :1].T)).T)
+        res = np.concatenate((res[1:], res[:1]))
+    return grid

@@ -13,7 +13,22 @@ from conftest import GOLDEN, load_golden
 INPUTS = GOLDEN / "inputs"
 
 
-def test_fill_convex_hull_matches_reference_grids():
+def test_hull_oracle_matches_reference_grids():
+    """The host restatement (checker of gpf_hull_fill) reproduces the reference's grids F6."""
+    from oracle.ref_hull import fill_convex_hull
+    f6 = load_golden("f6_hull.npz")
+    for i in range(int(f6["ncases"])):
+        pts, res = f6[f"c{i}_points"], list(f6[f"c{i}_res"])
+        got = fill_convex_hull(pts, res)
+        want = f6[f"c{i}_grid"]
+        assert got.shape == want.shape, i
+        assert np.array_equal(got, want), i
+
+
+@pytest.mark.gpu
+def test_fill_convex_hull_on_gpu_matches_reference_grids():
+    """fill_convex_hull with the fill passes on the MI355X: the reference's grids F6 point for
+    point, same order (2-D and 3-D cases)."""
     from convex_hull import fill_convex_hull
     f6 = load_golden("f6_hull.npz")
     for i in range(int(f6["ncases"])):
@@ -22,6 +37,21 @@ def test_fill_convex_hull_matches_reference_grids():
         want = f6[f"c{i}_grid"]
         assert got.shape == want.shape, i
         assert np.array_equal(got, want), i
+
+
+@pytest.mark.gpu
+def test_fill_convex_hull_on_gpu_matches_oracle_off_grid():
+    """Off-grid hull vertices (raw values that round_to_res moves, resolutions >= 1 and with
+    different decimals, 3-D and 4-D): GPU fill == host restatement."""
+    from convex_hull import fill_convex_hull
+    from oracle.ref_hull import fill_convex_hull as ref_fill
+    rng = np.random.default_rng(5)
+    for d, res in [(2, [0.05, 0.1]), (2, [0.25, 2.0]), (3, [0.1, 0.2, 0.15]), (4, [0.5, 0.5, 0.5, 0.5])]:
+        pts = rng.uniform(-1.3, 2.7, size=(12, d)) * np.array([1, 2, 1, 3][:d])
+        got = fill_convex_hull(pts, res)
+        want = ref_fill(pts, res)
+        assert got.shape == want.shape, (d, res)
+        assert np.array_equal(got, want), (d, res)
 
 
 def test_round_to_res_quirks():
