@@ -321,16 +321,19 @@ def main():
 
     cpu = None
     predict = None
-    if rank == 0 and args.predict_points > 0:
+    # secondary lines and the CPU baseline: single-GPU runs only (rank 0 at N=1); a multi-GPU
+    # run reports the headline metric alone
+    solo = world == 1
+    if solo and args.predict_points > 0:
         predict = predict_line(ctx, x, y, e, N, d, args)
     psurf = None
-    if rank == 0 and args.psurf_rows > 0:
+    if solo and args.psurf_rows > 0:
         psurf = psurf_line(ctx, args)
     hull = None
-    if rank == 0 and not args.no_hull:
+    if solo and not args.no_hull:
         hull = hull_line(ctx, args)
 
-    if rank == 0 and not args.no_cpu and args.cpu_sample > 0:
+    if solo and not args.no_cpu and args.cpu_sample > 0:
         rng = np.random.default_rng(args.seed + 7)
         sample = lo + (hi - lo) * rng.uniform(0.2, 0.8, size=(args.cpu_sample, d))
         workers = max(1, min(args.cpu_workers, args.cpu_sample))
