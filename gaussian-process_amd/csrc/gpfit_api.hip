@@ -550,6 +550,10 @@ int gpf_eval_batch(gpf_ctx* c, const double* ls, int P, double* loss, double* mu
         const hipError_t ei = hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0);
         hipGraphDestroy(gr);
         GPF_HIP(c, ei);
+        if (c->graphs.size() >= 8) {  // bounded cache: drop the oldest batch size
+          hipGraphExecDestroy(c->graphs.front().second);
+          c->graphs.erase(c->graphs.begin());
+        }
         c->graphs.push_back({P, ge});
       }
       GPF_HIP(c, hipGraphLaunch(ge, c->stream));
