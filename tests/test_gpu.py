@@ -248,6 +248,32 @@ def test_chunked_batches_equal_single_batch(f3, monkeypatch):
     np.testing.assert_array_equal(full, chunked)
 
 
+def test_graph_replay_equals_plain_launches(f2, monkeypatch):
+    """Small batches (N <= 256) replay a captured HIP graph padded to all P slots; the scores
+    equal the plain launch path bit for bit, across changing sentinel patterns and reuse."""
+    import gpfit
+    x, y, e = _fx(f2["c0_x"]), f2["c0_y"], f2["c0_e"]
+    lo, hi = ref_cpu.search_bounds(x)
+    s, ex = ref_cpu.sigma_grid()
+    rng = np.random.default_rng(11)
+    batches = []
+    for _ in range(4):
+        pos = lo + (hi - lo) * rng.uniform(-0.2, 1.2, size=(40, x.shape[0]))  # some land outside: sentinels
+        batches.append(pos)
+    a = gpfit.Context(0)
+    a.set_data(x, y, e); a.set_grid(s, ex, lo, hi)
+    with_graph = [a.eval_batch(p) for p in batches]
+    a.close()
+    monkeypatch.setenv("GPF_NO_GRAPH", "1")
+    b = gpfit.Context(0)
+    b.set_data(x, y, e); b.set_grid(s, ex, lo, hi)
+    plain = [b.eval_batch(p) for p in batches]
+    b.close()
+    for g, q in zip(with_graph, plain):
+        np.testing.assert_array_equal(g, q)
+    assert any((g == 1e13).any() for g in with_graph) and any((g < 1e13).any() for g in with_graph)
+
+
 def test_log_marginal_likelihood_vs_oracle(ctx, f3):
     for i in [0, 4]:
         x, y, e, P = f3[f"c{i}_x"], f3[f"c{i}_y"], f3[f"c{i}_e"], f3[f"c{i}_P"]
