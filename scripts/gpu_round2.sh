@@ -13,3 +13,7 @@ for v in $VARIANTS; do
     python -c "import json; d=json.loads(open('$O/b.log').read().strip().splitlines()[-1]); print('$v', d['config']['N'], round(d['value'],1), 'evals/s', round(d['roofline']['achieved'],1), 'TF')"
   done
 done
+for v in $VARIANTS; do
+  GPFIT_LIB=$PWD/gaussian-process_amd/libgpfit_$v.so timeout -k 10 200 python bench.py --n 4096 --d 3 --swarm-per-gpu 32 --steps 5 --warmup 1 --no-cpu --pso-steps 0 --predict-points 0 --psurf-rows 0 --no-hull > $O/b.log 2>&1 || exit $?
+  python -c "import json; d=json.loads(open('$O/b.log').read().strip().splitlines()[-1]); print('$v', d['config']['N'], 'P32', round(d['value'],1), 'evals/s', round(d['roofline']['achieved'],1), 'TF')"
+done
