@@ -620,10 +620,11 @@ __device__ __forceinline__ void k_step_body(int J, int nt, int Npad, double* __r
     double* Aii = Lp + (size_t)I * T * ld + (size_t)I * T;
     Acc<T> acc;
     // C = A_IJ - L_I,<J L_J,<J^T (accumulator seeded with A_IJ, A operand staged negated)
-    acc.load(qd, Aij, ld);
-    if (J > 0)
+    if (J > 0) {  // (at J = 0, C = A_IJ is already in place)
+      acc.load(qd, Aij, ld);
       step_gemm<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, J * T, smem, qd);
-    acc.store(qd, Aij, ld);
+      acc.store(qd, Aij, ld);
+    }
     __syncthreads();
     // L_IJ = C U_JJ^T
     acc.zero();
