@@ -13,9 +13,12 @@
 //   L tiles (I > J):  L_IJ = (A_IJ - L_I,<J L_J,<J^T) U_JJ^T       streamed MFMA GEMM, depth 128 J
 //                     A_II -= L_IJ L_IJ^T ; y_I -= L_IJ z_J         look-ahead (keeps A_II and y current)
 //   U tiles (K < J):  U_JK = -U_JJ (L_J,[K,J) U_[K,J),K)           streamed MFMA GEMM, depth 128 (J-K)
-// and k_diag factors the next diagonal block (L_JJ, U_JJ = L_JJ^-1, z_J) in between.
+// and the workgroup that finishes A_{J+1,J+1} factors it in the same launch (factor128:
+// L, U = L^-1 and z of the diagonal block); k_diag does block 0 before the first launch.
 // A left-looking step streams each factored panel once per 128 output columns,
 // so the GEMMs run at ~32 flop per HBM byte (64-wide columns: ~16, HBM-bound).
+// GEMM operands go global -> LDS by direct-to-LDS loads (gemm_stream_dl), and MFMAs on
+// known-zero triangles are skipped (Tri in gpf_common.hip).
 
 #pragma once
 #include "gpf_common.hip"
