@@ -63,14 +63,26 @@ template <int TM> struct Geo {
   static_assert(WR * WC == NW, "wave grid");
 };
 
+// Wave -> sub-tile map. The waves of a workgroup are dealt round-robin over the CU's 4
+// SIMDs (wave w on SIMD w % 4), so with WC = 4 the two waves sharing a SIMD own the
+// same column slab in the two row halves. Under a triangular operand (TRI_B_*) or a
+// lower-only output (TRI_C_LOWER) the skipped MFMAs then pile onto the same SIMDs:
+// in the 128-wide TRMM one SIMD issues all of its blocks while another issues an
+// eighth. GPF_BAL mirrors the column slabs of the second row half (wc -> WC-1-wc), so
+// each SIMD pairs a light slab with a heavy one. Any map is a permutation of the same
+// per-element work: results are bitwise unchanged.
+#ifndef GPF_BAL
+#define GPF_BAL 1
+#endif
 template <int TM> struct Quad {
   int lane, rb, cb;
   __device__ Quad() {
     const int tid = threadIdx.x;
     lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar) tile origin
-    rb = (w / Geo<TM>::WC) * (TM / Geo<TM>::WR);
-    cb = (w % Geo<TM>::WC) * (TM / Geo<TM>::WC);
+    const int wr = w / Geo<TM>::WC, wc = w % Geo<TM>::WC;
+    rb = wr * (TM / Geo<TM>::WR);
+    cb = ((GPF_BAL && (wr & 1)) ? (Geo<TM>::WC - 1 - wc) : wc) * (TM / Geo<TM>::WC);
   }
   __device__ __forceinline__ int wrow() const { return (threadIdx.x >> 6) / Geo<TM>::WC; }
   __device__ __forceinline__ int row(int mi, int r) const { return rb + mi * 16 + (lane >> 4) + 4 * r; }
