@@ -598,15 +598,12 @@ __device__ __forceinline__ void step_gemm(Acc<T>& acc, const double* Ap, int lda
 #endif
 }
 
-__device__ __forceinline__ void k_step_body(int J, int nt, int Npad, double* __restrict__ Lb, double* __restrict__ Ub,
-                                            double* __restrict__ yb, double* __restrict__ s2p,
-                                            double* __restrict__ szp, int* __restrict__ info, int P, int grp,
-                                            int N) {
-  __shared__ __attribute__((aligned(16))) double smem[STEP_SMEM];
-  __shared__ __attribute__((aligned(16))) double small[STEP_SMALL];
+// Tile w of block column J of particle p (the unit of work of k_step).
+__device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad, double* __restrict__ Lb,
+                                          double* __restrict__ Ub, double* __restrict__ yb,
+                                          double* __restrict__ s2p, double* __restrict__ szp,
+                                          int* __restrict__ info, int N, double* smem, double* small) {
   const int tid = threadIdx.x;
-  int p, w;
-  step_tile(blockIdx.x, P, nt - 1, grp, p, w);
   const int nL = nt - 1 - J;
   const size_t ld = (size_t)Npad;
   double* Lp = Lb + (size_t)p * ld * ld;
@@ -727,7 +724,11 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
     g_wg_trace[J][blockIdx.x][2] = ((unsigned long long)xcc << 32) | hw;
   }
 #endif
-  k_step_body(J, nt, Npad, Lb, Ub, yb, s2p, szp, info, P, grp, N);
+  __shared__ __attribute__((aligned(16))) double smem[STEP_SMEM];
+  __shared__ __attribute__((aligned(16))) double small[STEP_SMALL];
+  int p, w;
+  step_tile(blockIdx.x, P, nt - 1, grp, p, w);
+  step_item(J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, smem, small);
 #ifdef GPF_WG_TRACE
   __syncthreads();
   if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) g_wg_trace[J][blockIdx.x][1] = realtime();
@@ -767,7 +768,7 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_gemm_benc
                                                                                    double* __restrict__ C) {
   __shared__ __attribute__((aligned(16))) double smem[STEP_SMEM];
   const int b = blockIdx.x;
-  const bool shared = (mode & 1) != 0, direct = (mode & 2) != 0;  // 1/3: shared operands; 2/3: direct-to-LDS
+  const bool shared = (mode & 1) != 0, direct = (mode & 2) != 0;  // 1/3: shared operands; 2/3: direct-to-LDS; +4: NN
   const int p = shared ? 0 : b % P, w = shared ? 0 : b / P;
   const size_t ld = (size_t)Npad;
   const int J = D / T, I = J + 1 + w;
@@ -775,7 +776,9 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_gemm_benc
   const Quad<T> qd;
   Acc<T> acc;
   acc.zero();
-  if (direct)
+  if (direct && (mode & 4))  // U-tile shape: B given as a [k][c] row panel (NN)
+    gemm_stream_dl<true, false>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)w * T, Npad, D, smem, qd);
+  else if (direct)
     gemm_stream_dl<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, D, smem, qd);
   else
     gemm_stream<T, false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, D, smem, qd);
