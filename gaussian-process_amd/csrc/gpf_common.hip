@@ -390,6 +390,101 @@ __device__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int
   __syncthreads();
 }
 
+// ----------------------------------------------------------------------------
+// Staggered variant (experiment): 8-deep chunks in a ring of 4 LDS buffers (same 64 KiB),
+// prefetch distance 2 chunks, one raw s_barrier per chunk with counted vmcnt, and waves 4-7
+// (the SIMD partners of waves 0-3) computing one chunk behind waves 0-3, so the two waves
+// sharing a SIMD never reach their LDS reads and MFMA bursts together.
+//   buffer of chunk c: read in phase c (waves 0-3) and c+1 (waves 4-7); chunk c+2 is issued at
+//   the start of phase c into buffer (c+2)%4, last read in phase c-1; each wave waits for its
+//   own loads of chunk c before the barrier that opens phase c.
+// [r][k] layout: a 1 KiB block holds 16 rows x 4 k-pairs; pair kp of row r sits in slot
+// kp ^ ((r >> 2) & 3). [k][c] layout as in gemm_stream_dl.
+// ----------------------------------------------------------------------------
+constexpr int D8_KC = 8;
+constexpr int D8_BUF = 2 * 128 * D8_KC;  // one chunk (A + B), doubles
+
+template <bool NN>
+__device__ __forceinline__ void d8_issue(const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
+                                         int ldb, int k0, double* sbuf, int wave, int lane) {
+  {
+    const int row = 16 * wave + (lane >> 2), kp = (lane & 3) ^ ((row >> 2) & 3);
+    dl_load(Ap + (size_t)row * lda + k0 + 2 * kp, sbuf + wave * 128);
+  }
+  double* sB = sbuf + 128 * D8_KC;
+  if (!NN) {
+    const int row = 16 * wave + (lane >> 2), kp = (lane & 3) ^ ((row >> 2) & 3);
+    dl_load(Bp + (size_t)row * ldb + k0 + 2 * kp, sB + wave * 128);
+  } else {
+    const int k = wave, cp = lane ^ (8 * (k & 3));
+    dl_load(Bp + (size_t)(k0 + k) * ldb + 2 * cp, sB + k * 128);
+  }
+}
+
+template <bool NN, bool NEG, int TRI>
+__device__ __forceinline__ void d8_mma(Acc<128>& acc, const double* sA, const double* sB, const Quad<128>& qd, int k0) {
+  constexpr int MBR = Geo<128>::MBR, MBC = Geo<128>::MBC;
+  const int lr = qd.lane & 15, lk = qd.lane >> 4;
+#pragma unroll
+  for (int ks = 0; ks < D8_KC; ks += 4) {
+    const int k = ks + lk, kp = k >> 1, ko = k & 1;
+    double a[MBR], b[MBC];
+#pragma unroll
+    for (int mi = 0; mi < MBR; ++mi) {
+      const int row = qd.rb + mi * 16 + lr;
+      a[mi] = sA[row * D8_KC + 2 * (kp ^ ((row >> 2) & 3)) + ko];
+    }
+#pragma unroll
+    for (int ni = 0; ni < MBC; ++ni) {
+      const int col = qd.cb + ni * 16 + lr;
+      if (!NN)
+        b[ni] = sB[col * D8_KC + 2 * (kp ^ ((col >> 2) & 3)) + ko];
+      else
+        b[ni] = sB[k * 128 + 2 * ((col >> 1) ^ (8 * (k & 3))) + (col & 1)];
+    }
+#pragma unroll
+    for (int mi = 0; mi < MBR; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < MBC; ++ni)
+        if (tri_live<TRI>(qd.rb + mi * 16, qd.cb + ni * 16, k0 + ks))
+          acc.v[mi][ni] = NEG ? mfma_neg_a(a[mi], b[ni], acc.v[mi][ni]) : mfma(a[mi], b[ni], acc.v[mi][ni]);
+  }
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <bool NN, bool NEG = false, int TRI = TRI_NONE>
+__device__ void gemm_stream_d8(Acc<128>& acc, const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
+                               int ldb, int K, double* smem, const Quad<128>& qd) {
+  const int nch = K / D8_KC;
+  if (nch <= 0) return;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = wave >> 2;
+  Ap = launder(Ap);
+  Bp = launder(Bp);
+  d8_issue<NN>(Ap, lda, Bp, ldb, 0, smem, wave, qd.lane);
+  if (nch > 1) d8_issue<NN>(Ap, lda, Bp, ldb, D8_KC, smem + D8_BUF, wave, qd.lane);
+#pragma unroll 1
+  for (int ph = 0; ph <= nch; ++ph) {
+    if (ph + 1 < nch)
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // chunk ph landed, chunk ph+1 may be in flight
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (ph + 2 < nch) d8_issue<NN>(Ap, lda, Bp, ldb, (ph + 2) * D8_KC, smem + ((ph + 2) & 3) * D8_BUF, wave, qd.lane);
+    const int c = ph - g;
+    if (c >= 0 && c < nch) {
+      const double* cur = smem + (c & 3) * D8_BUF;
+      d8_mma<NN, NEG, TRI>(acc, cur, cur + 128 * D8_KC, qd, c * D8_KC);
+    }
+  }
+  __syncthreads();
+}
+
 // 64x64x64 GEMM with both operands resident in LDS (8 waves, 32x16 each):
 //   A (r,k) at sA[r*la + k];  B (k,c) at sB[c*lb + k] (!NN) or sB[k*lb + c] (NN).
 template <bool NN>

@@ -585,13 +585,18 @@ __device__ __forceinline__ unsigned long long realtime() {
 }
 #endif
 
+#ifndef GPF_D8
+#define GPF_D8 0  // staggered 8-deep ring (gemm_stream_d8) in the block-column GEMMs (build-time A/B knob)
+#endif
 #ifndef GPF_DL
 #define GPF_DL 1  // direct-to-LDS staging in the block-column GEMMs (build-time A/B knob)
 #endif
 template <bool NN, bool NEG = false, int TRI = TRI_NONE>
 __device__ __forceinline__ void step_gemm(Acc<T>& acc, const double* Ap, int lda, const double* Bp, int ldb, int K,
                                           double* smem, const Quad<T>& qd) {
-#if GPF_DL
+#if GPF_D8
+  gemm_stream_d8<NN, NEG, TRI>(acc, Ap, lda, Bp, ldb, K, smem, qd);
+#elif GPF_DL
   gemm_stream_dl<NN, NEG, TRI>(acc, Ap, lda, Bp, ldb, K, smem, qd);
 #else
   gemm_stream<T, NN, NEG, TRI>(acc, Ap, lda, Bp, ldb, K, smem, qd);
@@ -776,7 +781,12 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_gemm_benc
   const Quad<T> qd;
   Acc<T> acc;
   acc.zero();
-  if (direct && (mode & 4))  // U-tile shape: B given as a [k][c] row panel (NN)
+  if (mode & 8) {  // staggered 8-deep ring (gemm_stream_d8)
+    if (mode & 4)
+      gemm_stream_d8<true, false>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)w * T, Npad, D, smem, qd);
+    else
+      gemm_stream_d8<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, D, smem, qd);
+  } else if (direct && (mode & 4))  // U-tile shape: B given as a [k][c] row panel (NN)
     gemm_stream_dl<true, false>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)w * T, Npad, D, smem, qd);
   else if (direct)
     gemm_stream_dl<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, D, smem, qd);
