@@ -296,9 +296,6 @@ __device__ void gemm_stream(Acc<TM>& acc, const double* __restrict__ Ap, int lda
 //                  so the 4 k-rows of an operand read land 128 B apart.
 // NEG negates through the MFMA's own A-negate modifier. LDS: 2 x 2 x 128 x 16 doubles = 64 KiB.
 // ----------------------------------------------------------------------------
-#ifndef GPF_DL_PRIO
-#define GPF_DL_PRIO 0
-#endif
 constexpr int DL_KC = 16;
 constexpr int DL_BUF = 2 * 128 * DL_KC;  // one stage (A + B), doubles
 constexpr int DL_STAGE = 2 * DL_BUF;     // double-buffered
@@ -333,8 +330,52 @@ __device__ __forceinline__ void dl_issue(const double* __restrict__ Ap, int lda,
   }
 }
 
+// One 16-deep chunk of MFMAs on the LDS stage. Block (mi, ni) of the wave's 64x32 sub-tile is
+// issued iff mi >= M0 (ni = 0) / mi >= M1 (ni = 1); 4 = the whole column is dead. Straight-line
+// code: operand reads of the next k-step can be scheduled across this one's MFMAs.
+template <bool NN, bool NEG, int M0, int M1>
+__device__ __forceinline__ void dl_mma_live(Acc<128>& acc, const double* sA, const double* sB, const Quad<128>& qd) {
+  constexpr int MBR = Geo<128>::MBR, MBC = Geo<128>::MBC;
+  static_assert(MBR == 4 && MBC == 2, "wave sub-tile geometry");
+  constexpr int MLO = M0 < M1 ? M0 : M1;
+  // Partial patterns (the triangular runs): the per-lane swizzled offsets are made opaque per
+  // chunk, so they are recomputed (a few VALU ops) instead of being hoisted out of the K loop
+  // once per variant, which overflows 128 VGPRs. The dense pattern keeps them hoisted: VALU
+  // work does not overlap the FP64 MFMAs of the same SIMD, so every op in the loop costs.
+  int lane = qd.lane;
+  if constexpr (M0 != 0 || M1 != 0) asm volatile("" : "+v"(lane));
+  const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int ks = 0; ks < DL_KC; ks += 4) {
+    const int k = ks + lk, kp = k >> 1, ko = k & 1;
+    double a[MBR], b[MBC];
+#pragma unroll
+    for (int mi = MLO; mi < MBR; ++mi) {
+      const int row = qd.rb + mi * 16 + lr;
+      a[mi] = sA[row * DL_KC + 2 * (kp ^ (row & 7)) + ko];
+    }
+#pragma unroll
+    for (int ni = 0; ni < MBC; ++ni) {
+      if ((ni == 0 ? M0 : M1) >= MBR) continue;
+      const int col = qd.cb + ni * 16 + lr;
+      if (!NN)
+        b[ni] = sB[col * DL_KC + 2 * (kp ^ (col & 7)) + ko];
+      else
+        b[ni] = sB[k * 128 + 2 * ((col >> 1) ^ (8 * (k & 3))) + (col & 1)];
+    }
+#pragma unroll
+    for (int mi = MLO; mi < MBR; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < MBC; ++ni)
+        if (mi >= (ni == 0 ? M0 : M1))
+          acc.v[mi][ni] = NEG ? mfma_neg_a(a[mi], b[ni], acc.v[mi][ni]) : mfma(a[mi], b[ni], acc.v[mi][ni]);
+  }
+}
+
+// One chunk with a per-MFMA-block wave-uniform skip (tri_live).
 template <bool NN, bool NEG, int TRI>
-__device__ __forceinline__ void dl_mma(Acc<128>& acc, const double* sA, const double* sB, const Quad<128>& qd, int k0) {
+__device__ __forceinline__ void dl_mma_blocks(Acc<128>& acc, const double* sA, const double* sB, const Quad<128>& qd,
+                                              int k0) {
   constexpr int MBR = Geo<128>::MBR, MBC = Geo<128>::MBC;
   const int lr = qd.lane & 15, lk = qd.lane >> 4;
 #pragma unroll
@@ -363,6 +404,31 @@ __device__ __forceinline__ void dl_mma(Acc<128>& acc, const double* sA, const do
   }
 }
 
+// Chunks [t0, t1) of the direct-to-LDS pipeline with one fixed MFMA pattern (M0, M1 as in
+// dl_mma_live; <4, 4> issues none but keeps the loads and barriers of its chunks).
+template <bool NN, bool NEG, int M0, int M1>
+__device__ __forceinline__ void dl_run(Acc<128>& acc, const double* __restrict__ Ap, int lda,
+                                       const double* __restrict__ Bp, int ldb, int t0, int t1, int nch, double* smem,
+                                       const Quad<128>& qd, int wave) {
+#pragma unroll 1
+  for (int t = t0; t < t1; ++t) {
+    // chunk t landed (own loads; barriers do not drain LDS-DMA) and everyone's are visible
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 < nch) dl_issue<NN>(Ap, lda, Bp, ldb, (t + 1) * DL_KC, smem + ((t + 1) & 1) * DL_BUF, wave, qd.lane);
+    if constexpr (M0 < 4 || M1 < 4) {
+      const double* cur = smem + (t & 1) * DL_BUF;
+      dl_mma_live<NN, NEG, M0, M1>(acc, cur, cur + 128 * DL_KC, qd);
+    }
+  }
+}
+
+// Known-zero skipping (Tri) at chunk granularity: every Tri boundary sits on a multiple of 16
+// in k, rows and columns, so whether an MFMA block contributes (tri_live) is the same for the
+// 4 k-steps of a 16-deep chunk, and per wave the chunks fall into a few contiguous runs with one
+// pattern each. Each run is its own straight-line loop (one pattern per loop keeps the register
+// allocation of the dense loop); exactly the MFMAs tri_live admits are issued, so results are
+// bitwise those of per-block skipping. Every wave still passes one barrier per chunk.
 template <bool NN, bool NEG = false, int TRI = TRI_NONE>
 __device__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
                                int ldb, int K, double* smem, const Quad<128>& qd) {
@@ -372,32 +438,53 @@ __device__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int
   Ap = launder(Ap);
   Bp = launder(Bp);
   dl_issue<NN>(Ap, lda, Bp, ldb, 0, smem, wave, qd.lane);
-#if GPF_DL_PRIO
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half (guide: 2 waves/SIMD)
-#endif
+#define GPF_RUN(m0, m1, a, b) dl_run<NN, NEG, m0, m1>(acc, Ap, lda, Bp, ldb, (a), (b), nch, smem, qd, wave)
+  if constexpr (TRI == TRI_NONE) {
+    GPF_RUN(0, 0, 0, nch);
+  } else if constexpr (TRI == TRI_B_KLEC) {  // column ni live iff 16 t <= cb + 16 ni
+    const int t1 = min(nch, qd.cb / 16 + 1), t2 = min(nch, t1 + 1);
+    GPF_RUN(0, 0, 0, t1);
+    GPF_RUN(4, 0, t1, t2);
+    GPF_RUN(4, 4, t2, nch);
+  } else if constexpr (TRI == TRI_B_KGEC) {  // column ni live iff 16 t >= cb + 16 ni
+    const int t1 = min(nch, qd.cb / 16), t2 = min(nch, t1 + 1);
+    GPF_RUN(4, 4, 0, t1);
+    GPF_RUN(0, 4, t1, t2);
+    GPF_RUN(0, 0, t2, nch);
+  } else if constexpr (TRI == TRI_A_KLER) {  // row block mi live iff 16 t <= rb + 16 mi
+    const int t1 = min(nch, qd.rb / 16 + 1);
+    const int t2 = min(nch, t1 + 1), t3 = min(nch, t1 + 2), t4 = min(nch, t1 + 3);
+    GPF_RUN(0, 0, 0, t1);
+    GPF_RUN(1, 1, t1, t2);
+    GPF_RUN(2, 2, t2, t3);
+    GPF_RUN(3, 3, t3, t4);
+    GPF_RUN(4, 4, t4, nch);
+  } else {  // TRI_C_LOWER: block live iff cb + 16 ni <= rb + 16 mi, for every chunk
+    static_assert(TRI == TRI_C_LOWER, "known-zero pattern");
+    // one loop with per-block wave-uniform branches measured faster here than one loop per
+    // pattern (profiles/r1/tri_runs_ab.txt)
 #pragma unroll 1
-  for (int t = 0; t < nch; ++t) {
-    // chunk t landed (own loads; barriers do not drain LDS-DMA) and everyone's are visible
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t + 1 < nch) dl_issue<NN>(Ap, lda, Bp, ldb, (t + 1) * DL_KC, smem + ((t + 1) & 1) * DL_BUF, wave, qd.lane);
-    const double* cur = smem + (t & 1) * DL_BUF;
-    dl_mma<NN, NEG, TRI>(acc, cur, cur + 128 * DL_KC, qd, t * DL_KC);
+    for (int t = 0; t < nch; ++t) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t + 1 < nch) dl_issue<NN>(Ap, lda, Bp, ldb, (t + 1) * DL_KC, smem + ((t + 1) & 1) * DL_BUF, wave, qd.lane);
+      const double* cur = smem + (t & 1) * DL_BUF;
+      dl_mma_blocks<NN, NEG, TRI>(acc, cur, cur + 128 * DL_KC, qd, t * DL_KC);
+    }
   }
-#if GPF_DL_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
+#undef GPF_RUN
   __syncthreads();
 }
 
 // ----------------------------------------------------------------------------
-// Staggered variant (experiment): 8-deep chunks in a ring of 4 LDS buffers (same 64 KiB),
-// prefetch distance 2 chunks, one raw s_barrier per chunk with counted vmcnt, and waves 4-7
-// (the SIMD partners of waves 0-3) computing one chunk behind waves 0-3, so the two waves
-// sharing a SIMD never reach their LDS reads and MFMA bursts together.
-//   buffer of chunk c: read in phase c (waves 0-3) and c+1 (waves 4-7); chunk c+2 is issued at
-//   the start of phase c into buffer (c+2)%4, last read in phase c-1; each wave waits for its
-//   own loads of chunk c before the barrier that opens phase c.
+// Ring variant (experiment): 8-deep chunks in a ring of RING LDS buffers (RING x 16 KiB),
+// prefetch distance DIST chunks (the loads of chunks ph+1 .. ph+DIST-1 stay in flight across
+// phase ph), one raw s_barrier per chunk with counted vmcnt. STAG = 1: waves 4-7 (the SIMD
+// partners of waves 0-3) compute one chunk behind waves 0-3, so the two waves sharing a SIMD
+// never reach their LDS reads and MFMA bursts together.
+//   chunk c lives in buffer c % RING, read in phase c (and c+1 when STAG); chunk ph+DIST is
+//   issued after the barrier that opens phase ph, into the buffer last read in phase
+//   ph+DIST-RING+STAG <= ph-1; each wave waits for its own loads of chunk ph before that barrier.
 // [r][k] layout: a 1 KiB block holds 16 rows x 4 k-pairs; pair kp of row r sits in slot
 // kp ^ ((r >> 2) & 3). [k][c] layout as in gemm_stream_dl.
 // ----------------------------------------------------------------------------
@@ -457,32 +544,52 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <bool NN, bool NEG = false, int TRI = TRI_NONE>
-__device__ void gemm_stream_d8(Acc<128>& acc, const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
-                               int ldb, int K, double* smem, const Quad<128>& qd) {
+// s_waitcnt vmcnt(2 n) for a run-time n in [0, 7) (each chunk is two loads per wave)
+__device__ __forceinline__ void wait_chunks(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+  }
+}
+
+template <bool NN, bool NEG = false, int TRI = TRI_NONE, int RING = 4, int DIST = 2, int STAG = 1>
+__device__ void gemm_stream_ring(Acc<128>& acc, const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
+                                 int ldb, int K, double* smem, const Quad<128>& qd) {
+  static_assert(DIST >= 1 && DIST <= RING - 1 - STAG && DIST <= 7, "ring reuse distance");
   const int nch = K / D8_KC;
   if (nch <= 0) return;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = wave >> 2;
+  const int g = STAG ? (wave >> 2) : 0;
   Ap = launder(Ap);
   Bp = launder(Bp);
-  d8_issue<NN>(Ap, lda, Bp, ldb, 0, smem, wave, qd.lane);
-  if (nch > 1) d8_issue<NN>(Ap, lda, Bp, ldb, D8_KC, smem + D8_BUF, wave, qd.lane);
+#pragma unroll
+  for (int c = 0; c < DIST; ++c)
+    if (c < nch) d8_issue<NN>(Ap, lda, Bp, ldb, c * D8_KC, smem + (c % RING) * D8_BUF, wave, qd.lane);
 #pragma unroll 1
-  for (int ph = 0; ph <= nch; ++ph) {
-    if (ph + 1 < nch)
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // chunk ph landed, chunk ph+1 may be in flight
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int ph = 0; ph < nch + STAG; ++ph) {
+    const int left = nch - 1 - ph;
+    wait_chunks(left <= 0 ? 0 : (left < DIST - 1 ? left : DIST - 1));
     raw_barrier();
-    if (ph + 2 < nch) d8_issue<NN>(Ap, lda, Bp, ldb, (ph + 2) * D8_KC, smem + ((ph + 2) & 3) * D8_BUF, wave, qd.lane);
+    if (ph + DIST < nch)
+      d8_issue<NN>(Ap, lda, Bp, ldb, (ph + DIST) * D8_KC, smem + ((ph + DIST) % RING) * D8_BUF, wave, qd.lane);
     const int c = ph - g;
     if (c >= 0 && c < nch) {
-      const double* cur = smem + (c & 3) * D8_BUF;
+      const double* cur = smem + (c % RING) * D8_BUF;
       d8_mma<NN, NEG, TRI>(acc, cur, cur + 128 * D8_KC, qd, c * D8_KC);
     }
   }
   __syncthreads();
+}
+
+template <bool NN, bool NEG = false, int TRI = TRI_NONE>
+__device__ void gemm_stream_d8(Acc<128>& acc, const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
+                               int ldb, int K, double* smem, const Quad<128>& qd) {
+  gemm_stream_ring<NN, NEG, TRI, 4, 2, 1>(acc, Ap, lda, Bp, ldb, K, smem, qd);
 }
 
 // 64x64x64 GEMM with both operands resident in LDS (8 waves, 32x16 each):

@@ -578,11 +578,16 @@ static_assert(STEP_NTH == DNTH, "the fused diagonal runs on the step workgroup")
 // and hardware placement of every k_step workgroup, per block column J.
 constexpr int WG_TRACE_J = 64, WG_TRACE_N = 4096;
 __device__ unsigned long long g_wg_trace[WG_TRACE_J][WG_TRACE_N][3];
+__device__ unsigned long long g_wg_phase[WG_TRACE_J][WG_TRACE_N][4];  // wave-0 phase ends (see step_item)
 __device__ __forceinline__ unsigned long long realtime() {
   unsigned long long t;
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
   return t;
 }
+#define GPF_PHASE(k) \
+  if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) g_wg_phase[J][blockIdx.x][k] = realtime()
+#else
+#define GPF_PHASE(k)
 #endif
 
 #ifndef GPF_D8
@@ -631,16 +636,19 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
       acc.store(qd, Aij, ld);
     }
     __syncthreads();
+    GPF_PHASE(0);
     // L_IJ = C U_JJ^T
     acc.zero();
     step_gemm<false, false, TRI_B_KLEC>(acc, Aij, Npad, Ujj, Npad, T, smem, qd);
     acc.store(qd, Aij, ld);
     if (tid < T) zj[tid] = yp[J * T + tid];
     __syncthreads();
+    GPF_PHASE(1);
     // look-ahead: A_II -= L_IJ L_IJ^T (the full tile; only its lower half is ever read), y_I -= L_IJ z_J
     acc.load(qd, Aii, ld);
     step_gemm<false, true, TRI_C_LOWER>(acc, Aij, Npad, Aij, Npad, T, smem, qd);
     acc.store(qd, Aii, ld);
+    GPF_PHASE(2);
     {
       const int r = tid & (T - 1), h = tid >> 7;  // 4 quarter-row partial dot products
       const double* row = Aij + (size_t)r * ld + h * 32;
@@ -652,6 +660,7 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
     if (tid < T)
       yp[I * T + tid] =
           yp[I * T + tid] - (((scratch[tid] + scratch[T + tid]) + scratch[2 * T + tid]) + scratch[3 * T + tid]);
+    GPF_PHASE(3);
     if (I == J + 1) {  // fused diagonal factor of block J+1 (every reduction of A_II and y_I is done)
       __syncthreads();
       const DiagSmem sm = carve_diag(smem, small);
@@ -673,10 +682,12 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
     acc.store(qd, Ujk, ld);
     if (tid < T) zj[tid] = yp[J * T + tid];
     __syncthreads();
+    GPF_PHASE(0);
     // U_JK = -U_JJ W (A operand staged negated)
     acc.zero();
     step_gemm<true, true, TRI_A_KLER>(acc, Ujj, Npad, Ujk, Npad, T, smem, qd);
     acc.store(qd, Ujk, ld);
+    GPF_PHASE(1);
     // column partials straight from the accumulators: sum over this wave's rows,
     // then the 4 lane groups, then the two row-halves of the tile (fixed order)
     constexpr int MBR = Geo<T>::MBR, MBC = Geo<T>::MBC;
@@ -781,11 +792,24 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_gemm_benc
   const Quad<T> qd;
   Acc<T> acc;
   acc.zero();
-  if (mode & 8) {  // staggered 8-deep ring (gemm_stream_d8)
-    if (mode & 4)
-      gemm_stream_d8<true, false>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)w * T, Npad, D, smem, qd);
-    else
-      gemm_stream_d8<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, D, smem, qd);
+  if (mode & 8) {  // ring variants (gemm_stream_ring), configuration mode >> 4
+    const double* A0 = Lp + (size_t)I * T * ld;
+    const double* B0 = (mode & 4) ? Lp + (size_t)w * T : Lp + (size_t)J * T * ld;
+    switch (mode >> 4) {
+#define GPF_RING_CASE(id, R, Dd, S)                                                                  \
+  case id:                                                                                         \
+    if (mode & 4)                                                                                  \
+      gemm_stream_ring<true, false, TRI_NONE, R, Dd, S>(acc, A0, Npad, B0, Npad, D, smem, qd);     \
+    else                                                                                           \
+      gemm_stream_ring<false, true, TRI_NONE, R, Dd, S>(acc, A0, Npad, B0, Npad, D, smem, qd);     \
+    break;
+      GPF_RING_CASE(0, 4, 2, 1)  // = gemm_stream_d8
+      GPF_RING_CASE(1, 4, 3, 0)  // 24-deep prefetch
+      GPF_RING_CASE(2, 4, 2, 0)  // 16-deep prefetch (the default path's distance)
+      GPF_RING_CASE(3, 4, 1, 0)  // 8-deep prefetch
+#undef GPF_RING_CASE
+      default: break;
+    }
   } else if (direct && (mode & 4))  // U-tile shape: B given as a [k][c] row panel (NN)
     gemm_stream_dl<true, false>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)w * T, Npad, D, smem, qd);
   else if (direct)

@@ -1002,6 +1002,16 @@ int gpf_debug_wg_trace(unsigned long long* out, int nj, int nwg) {
     std::memcpy(out + (size_t)j * nwg * 3, h.data() + (size_t)j * gpf::WG_TRACE_N * 3, (size_t)nwg * 3 * 8);
   return GPF_OK;
 }
+// diagnostic builds only: wave-0 phase-end stamps of k_step workgroups, [J][wg][4] (see step_item)
+int gpf_debug_wg_phase(unsigned long long* out, int nj, int nwg) {
+  if (!out || nj <= 0 || nwg <= 0 || nj > gpf::WG_TRACE_J || nwg > gpf::WG_TRACE_N) return GPF_BAD_ARG;
+  hipDeviceSynchronize();
+  std::vector<unsigned long long> h((size_t)gpf::WG_TRACE_J * gpf::WG_TRACE_N * 4);
+  if (hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(gpf::g_wg_phase), h.size() * 8) != hipSuccess) return GPF_HIP_ERROR;
+  for (int j = 0; j < nj; ++j)
+    std::memcpy(out + (size_t)j * nwg * 4, h.data() + (size_t)j * gpf::WG_TRACE_N * 4, (size_t)nwg * 4 * 8);
+  return GPF_OK;
+}
 #endif
 
 #ifdef GPF_DIAG_STAMPS
