@@ -296,6 +296,9 @@ __device__ void gemm_stream(Acc<TM>& acc, const double* __restrict__ Ap, int lda
 //                  so the 4 k-rows of an operand read land 128 B apart.
 // NEG negates through the MFMA's own A-negate modifier. LDS: 2 x 2 x 128 x 16 doubles = 64 KiB.
 // ----------------------------------------------------------------------------
+#ifndef GPF_DENSE_RUN
+#define GPF_DENSE_RUN 1  // dense chunk runs without VALU address work (build-time A/B knob)
+#endif
 constexpr int DL_KC = 16;
 constexpr int DL_BUF = 2 * 128 * DL_KC;  // one stage (A + B), doubles
 constexpr int DL_STAGE = 2 * DL_BUF;     // double-buffered
@@ -304,8 +307,22 @@ __device__ __forceinline__ d4 mfma_neg_a(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 1);  // blgp bit 0 = negate A (f64)
 }
 
+// One wave-wide 16 B/lane global -> LDS transfer into the 1 KiB block at l (wave-uniform).
+// Issued from inline asm: the compiler does not track the LDS write of the asm, so it no longer
+// places an s_waitcnt vmcnt(0) in front of the next LDS read (which it must do for the builtin,
+// since it cannot tell which LDS bytes the transfer writes). That wait drained the next chunk's
+// prefetch before the current chunk's MFMAs could start. Every pipeline that uses dl_load waits
+// for its own transfers itself (s_waitcnt vmcnt before the barrier that publishes a chunk).
+#ifndef GPF_DL_ASM
+#define GPF_DL_ASM 1  // build-time A/B knob
+#endif
 __device__ __forceinline__ void dl_load(const double* g, double* l) {
+#if GPF_DL_ASM
+  const uint32_t m = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)l;
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m) : "memory");
+#else
   __builtin_amdgcn_global_load_lds((const void*)g, (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+#endif
 }
 
 template <bool NN>
@@ -404,6 +421,95 @@ __device__ __forceinline__ void dl_mma_blocks(Acc<128>& acc, const double* sA, c
   }
 }
 
+// Dense chunks [t0, t1) (every MFMA block live) with no VALU address work inside the loop:
+// VALU ops do not overlap the FP64 MFMAs of their SIMD, so each one costs issue time. The per-lane
+// LDS byte offsets are formed once per call; the buffer parity is unrolled, so buffer, k-step and
+// row/column-block displacements are ds_read immediates; the global sources are a scalar chunk
+// base plus a fixed 32-bit per-lane byte offset (the saddr form of global_load_lds).
+template <bool NN, bool NEG>
+struct DenseRun {
+  uint32_t la[4], lb[4];  // LDS read offsets (bytes) per k-step: A rows, B^T rows (!NN) / B (NN, [0..1] per ni)
+  uint32_t ga[2], gb[2];  // global byte offsets of the two 1 KiB blocks per operand this wave fills
+  int blk0;               // first block index of this wave
+
+  __device__ __forceinline__ DenseRun(const Quad<128>& qd, int lda, int ldb, int wave) {
+    const int lane = qd.lane, lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int kp = 2 * s + (lk >> 1);
+      la[s] = 8u * (uint32_t)((qd.rb + lr) * DL_KC + 2 * (kp ^ (lr & 7)) + (lk & 1));
+      if (!NN) lb[s] = 8u * (uint32_t)(128 * DL_KC + (qd.cb + lr) * DL_KC + 2 * (kp ^ (lr & 7)) + (lk & 1));
+    }
+    if (NN) {
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const int col = qd.cb + ni * 16 + lr;
+        lb[ni] = 8u * (uint32_t)(128 * DL_KC + lk * 128 + 2 * ((col >> 1) ^ (8 * (lk & 3))) + (col & 1));
+      }
+    }
+    blk0 = 2 * wave;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int blk = blk0 + u, row = 8 * blk + (lane >> 3), kp = (lane & 7) ^ (row & 7);
+      ga[u] = 8u * (uint32_t)(row * lda + 2 * kp);
+      gb[u] = NN ? 8u * (uint32_t)(blk * ldb + 2 * (lane ^ (8 * (blk & 3)))) : 8u * (uint32_t)(row * ldb + 2 * kp);
+    }
+  }
+
+  template <int BUF>
+  __device__ __forceinline__ void issue(const double* Ap, const double* Bp, int ldb, int c, double* smem) const {
+    const char* Ac = (const char*)(Ap + c * DL_KC);
+    const char* Bc = NN ? (const char*)(Bp + (size_t)c * DL_KC * ldb) : (const char*)(Bp + c * DL_KC);
+    double* sbuf = smem + BUF * DL_BUF;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int blk = blk0 + u;
+      dl_load((const double*)(Ac + ga[u]), sbuf + blk * 8 * DL_KC);
+      dl_load((const double*)(Bc + gb[u]), sbuf + 128 * DL_KC + (NN ? blk * 128 : blk * 8 * DL_KC));
+    }
+  }
+
+  template <int BUF>
+  __device__ __forceinline__ void mma(Acc<128>& acc, const double* smem) const {
+    const char* sb = (const char*)smem + BUF * DL_BUF * 8;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      double a[4], b[2];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) a[mi] = *(const double*)(sb + la[s] + mi * 16 * DL_KC * 8);
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+        b[ni] = NN ? *(const double*)(sb + lb[ni] + s * 512 * 8) : *(const double*)(sb + lb[s] + ni * 16 * DL_KC * 8);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          acc.v[mi][ni] = NEG ? mfma_neg_a(a[mi], b[ni], acc.v[mi][ni]) : mfma(a[mi], b[ni], acc.v[mi][ni]);
+    }
+  }
+
+  template <int BUF>
+  __device__ __forceinline__ void chunk(Acc<128>& acc, const double* Ap, const double* Bp, int ldb, int t, int nch,
+                                        double* smem) const {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 < nch) issue<1 - BUF>(Ap, Bp, ldb, t + 1, smem);
+    mma<BUF>(acc, smem);
+  }
+
+  __device__ __forceinline__ void run(Acc<128>& acc, const double* Ap, const double* Bp, int ldb, int t0, int t1,
+                                      int nch, double* smem) const {
+    int t = t0;
+    if (t < t1 && (t & 1)) chunk<1>(acc, Ap, Bp, ldb, t++, nch, smem);
+#pragma unroll 1
+    for (; t + 1 < t1; t += 2) {
+      chunk<0>(acc, Ap, Bp, ldb, t, nch, smem);
+      chunk<1>(acc, Ap, Bp, ldb, t + 1, nch, smem);
+    }
+    if (t < t1) chunk<0>(acc, Ap, Bp, ldb, t, nch, smem);
+  }
+};
+
 // Chunks [t0, t1) of the direct-to-LDS pipeline with one fixed MFMA pattern (M0, M1 as in
 // dl_mma_live; <4, 4> issues none but keeps the loads and barriers of its chunks).
 template <bool NN, bool NEG, int M0, int M1>
@@ -435,10 +541,27 @@ __device__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int
   const int nch = K / DL_KC;
   if (nch <= 0) return;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const double* Ar = Ap;  // scalar bases for the dense runs
+  const double* Br = Bp;
   Ap = launder(Ap);
   Bp = launder(Bp);
   dl_issue<NN>(Ap, lda, Bp, ldb, 0, smem, wave, qd.lane);
+  // Drain every outstanding vector-memory op here (the chunk-0 transfers, which the first chunk
+  // waits for anyway, and e.g. an accumulator seed loaded just before) through the builtin, so
+  // that the compiler's wait bookkeeping sees them done: otherwise it keeps an s_waitcnt for the
+  // seed inside the K loop, where it also drains the asm-issued prefetch of the next chunk.
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+#if GPF_DENSE_RUN
+#define GPF_RUN(m0, m1, a, b)                                                   \
+  do {                                                                          \
+    if constexpr (m0 == 0 && m1 == 0)                                           \
+      DenseRun<NN, NEG>(qd, lda, ldb, wave).run(acc, Ar, Br, ldb, (a), (b), nch, smem); \
+    else                                                                        \
+      dl_run<NN, NEG, m0, m1>(acc, Ap, lda, Bp, ldb, (a), (b), nch, smem, qd, wave); \
+  } while (0)
+#else
 #define GPF_RUN(m0, m1, a, b) dl_run<NN, NEG, m0, m1>(acc, Ap, lda, Bp, ldb, (a), (b), nch, smem, qd, wave)
+#endif
   if constexpr (TRI == TRI_NONE) {
     GPF_RUN(0, 0, 0, nch);
   } else if constexpr (TRI == TRI_B_KLEC) {  // column ni live iff 16 t <= cb + 16 ni
@@ -462,7 +585,7 @@ __device__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int
   } else {  // TRI_C_LOWER: block live iff cb + 16 ni <= rb + 16 mi, for every chunk
     static_assert(TRI == TRI_C_LOWER, "known-zero pattern");
     // one loop with per-block wave-uniform branches measured faster here than one loop per
-    // pattern (profiles/r1/tri_runs_ab.txt)
+    // pattern (profiles/r1/gemm_loop_ab.txt)
 #pragma unroll 1
     for (int t = 0; t < nch; ++t) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
