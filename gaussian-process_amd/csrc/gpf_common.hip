@@ -296,6 +296,12 @@ __device__ void gemm_stream(Acc<TM>& acc, const double* __restrict__ Ap, int lda
 //                  so the 4 k-rows of an operand read land 128 B apart.
 // NEG negates through the MFMA's own A-negate modifier. LDS: 2 x 2 x 128 x 16 doubles = 64 KiB.
 // ----------------------------------------------------------------------------
+#ifndef GPF_SYRK_RUNS
+#define GPF_SYRK_RUNS 0  // the SYRK's known-zero pattern as one loop per wave pattern (A/B knob)
+#endif
+#ifndef GPF_DENSE_DB
+#define GPF_DENSE_DB 1  // dense runs: double-buffered operand registers across k-steps (A/B knob)
+#endif
 #ifndef GPF_DENSE_RUN
 #define GPF_DENSE_RUN 1  // dense chunk runs without VALU address work (build-time A/B knob)
 #endif
@@ -469,23 +475,43 @@ struct DenseRun {
     }
   }
 
+  __device__ __forceinline__ void reads(const char* sb, int s, double (&a)[4], double (&b)[2]) const {
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) a[mi] = *(const double*)(sb + la[s] + mi * 16 * DL_KC * 8);
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+      b[ni] = NN ? *(const double*)(sb + lb[ni] + s * 512 * 8) : *(const double*)(sb + lb[s] + ni * 16 * DL_KC * 8);
+  }
+
   template <int BUF>
   __device__ __forceinline__ void mma(Acc<128>& acc, const double* smem) const {
     const char* sb = (const char*)smem + BUF * DL_BUF * 8;
+#if GPF_DENSE_DB
+    // operands of k-step s+1 are read into the other register set before the MFMAs of step s
+    double a[2][4], b[2][2];
+    reads(sb, 0, a[0], b[0]);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (s < 3) reads(sb, s + 1, a[(s + 1) & 1], b[(s + 1) & 1]);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          acc.v[mi][ni] = NEG ? mfma_neg_a(a[s & 1][mi], b[s & 1][ni], acc.v[mi][ni])
+                              : mfma(a[s & 1][mi], b[s & 1][ni], acc.v[mi][ni]);
+    }
+#else
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       double a[4], b[2];
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) a[mi] = *(const double*)(sb + la[s] + mi * 16 * DL_KC * 8);
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
-        b[ni] = NN ? *(const double*)(sb + lb[ni] + s * 512 * 8) : *(const double*)(sb + lb[s] + ni * 16 * DL_KC * 8);
+      reads(sb, s, a, b);
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni)
           acc.v[mi][ni] = NEG ? mfma_neg_a(a[mi], b[ni], acc.v[mi][ni]) : mfma(a[mi], b[ni], acc.v[mi][ni]);
     }
+#endif
   }
 
   template <int BUF>
@@ -584,8 +610,14 @@ __device__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int
     GPF_RUN(4, 4, t4, nch);
   } else {  // TRI_C_LOWER: block live iff cb + 16 ni <= rb + 16 mi, for every chunk
     static_assert(TRI == TRI_C_LOWER, "known-zero pattern");
-    // one loop with per-block wave-uniform branches measured faster here than one loop per
-    // pattern (profiles/r1/gemm_loop_ab.txt)
+#if GPF_SYRK_RUNS
+    const int dc = qd.cb - qd.rb;  // in {-64, -32, 0, 32, 64, 96}
+    if (dc < 0) GPF_RUN(0, 0, 0, nch);
+    else if (dc == 0) GPF_RUN(0, 1, 0, nch);
+    else if (dc <= 32) GPF_RUN(2, 3, 0, nch);
+    else GPF_RUN(4, 4, 0, nch);
+#else
+    // one loop with per-block wave-uniform branches (profiles/r1/gemm_loop_ab.txt)
 #pragma unroll 1
     for (int t = 0; t < nch; ++t) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -594,6 +626,7 @@ __device__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int
       const double* cur = smem + (t & 1) * DL_BUF;
       dl_mma_blocks<NN, NEG, TRI>(acc, cur, cur + 128 * DL_KC, qd, t * DL_KC);
     }
+#endif
   }
 #undef GPF_RUN
   __syncthreads();
