@@ -19,12 +19,13 @@ constexpr int BT = 64;  // covariance build tile
 // Op order mirrors kernel_func (GP_func.py:56-65): a = x / l, |a|^2 summed over
 // dims in order, (|a_i|^2 + |a_j|^2) - 2 a_i.a_j, clamp >= 0, exp(-0.5 r2).
 // Also seeds the per-particle RHS workspace with y (padded with zeros).
-// grid: (nt*(nt+1)/2, P)
+// grid: (nb*(nb+1)/2, P) for every lower 64x64 tile, or (3*nt, P) with diag_only: the lower
+// tiles of the 128-wide diagonal blocks only (k_step computes the others itself, GPF_KFUSE).
 // ----------------------------------------------------------------------------
 __global__ __launch_bounds__(NTHR) void k_build_cov(int N, int Npad, int d, const double* __restrict__ x,
                                                     const double* __restrict__ y, const double* __restrict__ e,
                                                     const double* __restrict__ ls, double* __restrict__ Lb,
-                                                    double* __restrict__ yb, int* __restrict__ info) {
+                                                    double* __restrict__ yb, int* __restrict__ info, int diag_only) {
   __shared__ double ai[DMAX][BT];
   __shared__ double aj[DMAX][BT];
   __shared__ double ni[BT], nj[BT];
@@ -32,10 +33,17 @@ __global__ __launch_bounds__(NTHR) void k_build_cov(int N, int Npad, int d, cons
   const int p = blockIdx.y;
   // lower-triangular tile index -> (bi, bj), bi >= bj
   const int idx = blockIdx.x;
-  int bi = (int)((sqrt(8.0 * idx + 1.0) - 1.0) * 0.5);
-  while ((bi + 1) * (bi + 2) / 2 <= idx) ++bi;
-  while (bi * (bi + 1) / 2 > idx) --bi;
-  const int bj = idx - bi * (bi + 1) / 2;
+  int bi, bj;
+  if (diag_only) {  // the three lower 64x64 tiles of 128-wide diagonal block idx / 3
+    const int b = idx / 3, m = idx % 3;
+    bi = 2 * b + (m > 0);
+    bj = 2 * b + (m == 2);
+  } else {
+    bi = (int)((sqrt(8.0 * idx + 1.0) - 1.0) * 0.5);
+    while ((bi + 1) * (bi + 2) / 2 <= idx) ++bi;
+    while (bi * (bi + 1) / 2 > idx) --bi;
+    bj = idx - bi * (bi + 1) / 2;
+  }
   const double* lp = ls + (size_t)p * d;
   if (idx == 0 && tid == 0) info[p] = 0;  // the factorisation kernels only ever set it
 

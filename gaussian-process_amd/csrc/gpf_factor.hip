@@ -608,11 +608,65 @@ __device__ __forceinline__ void step_gemm(Acc<T>& acc, const double* Ap, int lda
 #endif
 }
 
+#ifndef GPF_KFUSE
+#define GPF_KFUSE 1  // off-diagonal K tiles computed in k_step instead of read from the K build
+#endif
+// A_IJ (I > J: no diagonal entries, so no noise term) of one particle straight into the
+// accumulator layout, with k_build_cov's op order (bitwise the same values, kernel_func
+// GP_func.py:56-65): the scaled coordinates and squared norms of the tile's 128 rows and 128
+// columns are staged in LDS first. Replaces the write of the K tile in the K build and its read
+// back here; only the diagonal blocks are still built (k_build_cov, diag_only).
+static_assert(2 * DMAX * T + 2 * T <= STEP_SMEM, "coordinate staging fits the step's LDS");
+__device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, const double* __restrict__ x,
+                                             const double* __restrict__ lp, int d, int N, int I, int J,
+                                             double* smem) {
+  const int tid = threadIdx.x;
+  double* sa = smem;              // [d][T] scaled coordinates of rows (block I)
+  double* sb = smem + d * T;      // [d][T] ... of columns (block J)
+  double* na = smem + 2 * d * T;  // [T] squared norms of rows
+  double* nb = na + T;            // [T] ... of columns
+  if (tid < 2 * T) {
+    const int t = tid & (T - 1);
+    const bool rows = tid < T;
+    const int g = (rows ? I : J) * T + t;
+    double* a = rows ? sa : sb;
+    double nrm = 0.0;
+    if (g < N) {
+      for (int k = 0; k < d; ++k) {
+        const double v = x[(size_t)k * N + g] / lp[k];
+        a[k * T + t] = v;
+        nrm = nrm + v * v;
+      }
+    }
+    (rows ? na : nb)[t] = nrm;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int mi = 0; mi < Acc<T>::MBR; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < Acc<T>::MBC; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = qd.row(mi, r), col = qd.col(ni);
+        double v = 0.0;
+        if (I * T + row < N && J * T + col < N) {
+          double dot = sa[row] * sb[col];
+          for (int k = 1; k < d; ++k) dot = fma(sa[k * T + row], sb[k * T + col], dot);
+          double r2 = (na[row] + nb[col]) - 2.0 * dot;
+          r2 = r2 > 0.0 ? r2 : 0.0;  // np.maximum(sq_dist, 0)
+          v = exp(-0.5 * r2);
+        }
+        acc.v[mi][ni][r] = v;
+      }
+  __syncthreads();
+}
+
 // Tile w of block column J of particle p (the unit of work of k_step).
 __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad, double* __restrict__ Lb,
                                           double* __restrict__ Ub, double* __restrict__ yb,
                                           double* __restrict__ s2p, double* __restrict__ szp,
-                                          int* __restrict__ info, int N, double* smem, double* small) {
+                                          int* __restrict__ info, int N, const double* __restrict__ x,
+                                          const double* __restrict__ ls, int d, double* smem, double* small) {
   const int tid = threadIdx.x;
   const int nL = nt - 1 - J;
   const size_t ld = (size_t)Npad;
@@ -630,11 +684,18 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
     double* Aii = Lp + (size_t)I * T * ld + (size_t)I * T;
     Acc<T> acc;
     // C = A_IJ - L_I,<J L_J,<J^T (accumulator seeded with A_IJ, A operand staged negated)
+#if GPF_KFUSE
+    cov_tile_acc(acc, qd, x, ls + (size_t)p * d, d, N, I, J, smem);
+    if (J > 0)
+      step_gemm<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, J * T, smem, qd);
+    acc.store(qd, Aij, ld);  // C (the TRMM below streams it)
+#else
     if (J > 0) {  // (at J = 0, C = A_IJ is already in place)
       acc.load(qd, Aij, ld);
       step_gemm<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, J * T, smem, qd);
       acc.store(qd, Aij, ld);
     }
+#endif
     __syncthreads();
     GPF_PHASE(0);
     // L_IJ = C U_JJ^T
@@ -644,10 +705,23 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
     if (tid < T) zj[tid] = yp[J * T + tid];
     __syncthreads();
     GPF_PHASE(1);
-    // look-ahead: A_II -= L_IJ L_IJ^T (the full tile; only its lower half is ever read), y_I -= L_IJ z_J
-    acc.load(qd, Aii, ld);
-    step_gemm<false, true, TRI_C_LOWER>(acc, Aij, Npad, Aij, Npad, T, smem, qd);
-    acc.store(qd, Aii, ld);
+    // look-ahead: A_II -= L_IJ L_IJ^T (the full tile; only its lower half is ever read), y_I -= L_IJ z_J.
+    // GPF_SYRK_PAIR: the rank-128 updates of A_II are paired — applied at odd J as one rank-256
+    // update with L_I,[J-1,J] — except that the next diagonal block (I = J+1) always takes all of
+    // its pending columns before it is factored; half the A_II read-modify-write passes.
+#ifndef GPF_SYRK_TRI
+#define GPF_SYRK_TRI TRI_C_LOWER  // A/B knob: TRI_NONE computes the whole tile with the dense loop
+#endif
+#ifndef GPF_SYRK_PAIR
+#define GPF_SYRK_PAIR 0  // measured: C +0.3%, B -1.8% (bitwise equal)
+#endif
+    const int j0 = (GPF_SYRK_PAIR && (J & 1)) ? J - 1 : J;
+    if (!GPF_SYRK_PAIR || (J & 1) || I == J + 1) {
+      const double* Lsy = Lp + (size_t)I * T * ld + (size_t)j0 * T;
+      acc.load(qd, Aii, ld);
+      step_gemm<false, true, GPF_SYRK_TRI>(acc, Lsy, Npad, Lsy, Npad, (J - j0 + 1) * T, smem, qd);
+      acc.store(qd, Aii, ld);
+    }
     GPF_PHASE(2);
     {
       const int r = tid & (T - 1), h = tid >> 7;  // 4 quarter-row partial dot products
@@ -729,7 +803,9 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
 __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int J, int nt, int Npad, double* __restrict__ Lb,
                                                   double* __restrict__ Ub, double* __restrict__ yb,
                                                   double* __restrict__ s2p, double* __restrict__ szp,
-                                                  int* __restrict__ info, int P, int grp, int N) {
+                                                  int* __restrict__ info, int P, int grp, int N,
+                                                  const double* __restrict__ x, const double* __restrict__ ls,
+                                                  int d) {
   const int tid = threadIdx.x;
 #ifdef GPF_WG_TRACE
   if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) {
@@ -744,7 +820,7 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
   __shared__ __attribute__((aligned(16))) double small[STEP_SMALL];
   int p, w;
   step_tile(blockIdx.x, P, nt - 1, grp, p, w);
-  step_item(J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, smem, small);
+  step_item(J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, smem, small);
 #ifdef GPF_WG_TRACE
   __syncthreads();
   if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) g_wg_trace[J][blockIdx.x][1] = realtime();

@@ -223,12 +223,14 @@ static int ensure_work(gpf_ctx* c, int want) {
   return GPF_OK;
 }
 
-// Particle groups factorised on concurrent streams (GPF_GROUPS, default 1): meant to
-// fill the tail of each dependent block-column launch with another group's tiles.
-// Measured on MI355X (profiles/r1/groups_ab.txt): 2 groups +3% at N=4096 P=64 but
-// -19% at N=1024 P=32, 4 groups worse everywhere, so one group is the default.
-static int num_groups(int pc) {
-  int g = 1;
+// Particle groups factorised on concurrent streams (GPF_GROUPS overrides): they fill the tail
+// of each dependent block-column launch with another group's tiles. Measured on MI355X
+// (profiles/r1/groups_ab.txt): 2 groups +0.6% at N=4096 P=64, +4.6% at N=4096 P=32 (config D's
+// share of one GPU), -19% at N=1024 P=32, 4 groups worse everywhere. Default: 2 groups for
+// chunks of at most 32 particles with at least 16 block columns, else 1 (at 64 particles the
+// gain is within noise, and one stream keeps per-launch timing exact for the roofline).
+static int num_groups(int pc, int nt) {
+  int g = (pc <= 32 && nt >= 16) ? 2 : 1;
   if (const char* s = getenv("GPF_GROUPS")) g = atoi(s);
   g = std::max(1, std::min(g, MAX_GROUPS));
   while (g > 1 && pc / g < 8) --g;  // keep >= 8 particles (one per XCD) per group
@@ -253,7 +255,7 @@ static int run_factor(gpf_ctx* c, int pc) {
   const int nb = Np / BT;
   const int ntri = nb * (nb + 1) / 2;
   const size_t ld = (size_t)Np;
-  const int ng = num_groups(pc);
+  const int ng = num_groups(pc, nt);
   // algorithmic flops of block-column launch J per particle, potrf + trtri (2/3 N^3) formulation:
   //   L tile: depth-128J GEMM 2 T^3 J + triangular multiply T^3 + look-ahead syrk share T^3
   //   U tile: depth-128(J-K) GEMM with a triangular factor 2 T^3 (J-K) - T^3 + triangular multiply T^3
@@ -288,9 +290,11 @@ static int run_factor(gpf_ctx* c, int pc) {
     double* szg = c->d_szp + (size_t)p0 * nt * ld;
     int* ig = c->d_info + p0;
     const double* lsg = c->d_ls + (size_t)p0 * c->d;
-    int rc = launch_on(c, st, PC_BUILD, 8.0 * ntri * BT * BT * (double)gc, [&] {
-      hipLaunchKernelGGL(gpf::k_build_cov, dim3(ntri, gc), dim3(NTHR), 0, st, N, Np, c->d, c->d_x, c->d_y, c->d_e,
-                         lsg, Lg, yg, ig);
+    // with GPF_KFUSE only the diagonal blocks are built here; k_step computes the other tiles
+    const int nbuild = (GPF_KFUSE && nt > 1) ? 3 * nt : ntri;
+    int rc = launch_on(c, st, PC_BUILD, 8.0 * nbuild * BT * BT * (double)gc, [&] {
+      hipLaunchKernelGGL(gpf::k_build_cov, dim3(nbuild, gc), dim3(NTHR), 0, st, N, Np, c->d, c->d_x, c->d_y, c->d_e,
+                         lsg, Lg, yg, ig, (int)(nbuild != ntri));
     });
     if (rc) return rc;
     // potrf + trtri of the first 128 block: 2/3 T^3 (later blocks are fused into k_step)
@@ -310,7 +314,7 @@ static int run_factor(gpf_ctx* c, int pc) {
         hipLaunchKernelGGL(gpf::k_step, dim3(gc * (nt - 1)), dim3(gpf::STEP_NTH), 0, st, J, nt, Np,
                            c->d_L + (size_t)p0 * ld * ld, c->d_U + (size_t)p0 * ld * ld, c->d_yb + (size_t)p0 * ld,
                            c->d_s2p + (size_t)p0 * nt * ld, c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc,
-                           step_group(gc), N);
+                           step_group(gc), N, c->d_x, c->d_ls + (size_t)p0 * c->d, c->d);
       });
       if (rc) return rc;
       total += fl * gc;
