@@ -312,3 +312,25 @@ def test_headline_size_vs_oracle_identity(ctx, N, d):
     ctx.set_data(x[:, perm], y[perm], e[perm])
     lp = ctx.eval_batch(P)
     assert _rel(lp, loss) < 1e-6
+
+
+def test_large_hetero_vs_oracle_identity(ctx):
+    """Config E's regime (d=4, heteroscedastic noise) at N=8192: 64 block columns, every
+    k_step path (fused K tiles, streamed dense and triangular runs, fused diagonals) at a
+    depth the N<=4096 cases do not reach. Mean/sd against the oracle's identity form."""
+    N, d = 8192, 4
+    rng = np.random.default_rng(7)
+    x = rng.uniform(0, 1, size=(d, N))
+    y = np.sum(np.sin(2 * np.pi * x), axis=0) + 0.1 * rng.standard_normal(N)
+    e = rng.uniform(0.05, 0.2, size=N)
+    lo, hi = ref_cpu.search_bounds(x)
+    s, ex = ref_cpu.sigma_grid()
+    P = rng.uniform(0.1, 0.5, size=(2, d))
+    ctx.set_data(x, y, e)
+    ctx.set_grid(s, ex, lo, hi)
+    loss, mu, sd = ctx.eval_batch(P, want_mu_sd=True)
+    m1, s1 = ref_cpu.GP_train_identity(x, y, e, P[1])
+    assert _rel(mu[1], m1) < RTOL_MU_SD
+    assert _rel(sd[1], s1) < RTOL_MU_SD
+    w = ref_cpu.coverage_loss(m1, s1, y, s, ex) + 0.01 * ref_cpu.proximity_penalty(P[1], lo, hi)
+    assert abs(loss[1] - w) / w < 1e-6  # allows a rare |pull|=1 threshold flip (SURVEY.md §7)
