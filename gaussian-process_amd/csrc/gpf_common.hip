@@ -290,7 +290,7 @@ __device__ void gemm_stream(Acc<TM>& acc, const double* __restrict__ Ap, int lda
 // chunk. Each wave instruction fills one 1 KiB block with 16 B per lane in lane order, so the
 // bank-conflict-free layout is made by choosing which global pair each lane fetches (XOR
 // swizzles):
-//   [r][k] panels: 8 rows x 8 k-pairs per block; pair kp of row r sits in slot kp ^ (r % 8),
+//   [r][k] panels: 8 rows x 8 k-pairs per block; pair kp of row r sits in slot kp ^ dl_sw(r),
 //                  so the 16 rows of an MFMA operand read spread over the banks;
 //   [k][c] panels: one k-row per block; column pair cp of row k sits in slot cp ^ 8 (k % 4),
 //                  so the 4 k-rows of an operand read land 128 B apart.
@@ -331,6 +331,16 @@ __device__ __forceinline__ void dl_load(const double* g, double* l) {
 #endif
 }
 
+// Slot swizzle of the [r][k] panels: k-pair kp of row r sits in slot kp ^ dl_sw(r). An MFMA
+// operand read takes 16 consecutive rows at one k per half-wave; rows r and r+8 share a bank
+// with sw = r & 7, while sw = (r >> 1) & 7 gives the 16 rows 16 distinct bank pairs (even and
+// odd rows sit 16 banks apart). Row offsets of operand blocks are multiples of 16, so the
+// swizzle of a read depends on the lane only and block displacements stay immediates.
+#ifndef GPF_DL_SW
+#define GPF_DL_SW 1
+#endif
+__device__ __forceinline__ int dl_sw(int r) { return GPF_DL_SW ? ((r >> 1) & 7) : (r & 7); }
+
 template <bool NN>
 __device__ __forceinline__ void dl_issue(const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
                                          int ldb, int k0, double* sbuf, int wave, int lane) {
@@ -339,12 +349,12 @@ __device__ __forceinline__ void dl_issue(const double* __restrict__ Ap, int lda,
   for (int u = 0; u < 2; ++u) {
     const int blk = 2 * wave + u;
     {
-      const int row = 8 * blk + (lane >> 3), kp = (lane & 7) ^ (row & 7);
+      const int row = 8 * blk + (lane >> 3), kp = (lane & 7) ^ dl_sw(row);
       dl_load(Ap + (size_t)row * lda + k0 + 2 * kp, sbuf + blk * 8 * DL_KC);
     }
     double* sB = sbuf + 128 * DL_KC;
     if (!NN) {
-      const int row = 8 * blk + (lane >> 3), kp = (lane & 7) ^ (row & 7);
+      const int row = 8 * blk + (lane >> 3), kp = (lane & 7) ^ dl_sw(row);
       dl_load(Bp + (size_t)row * ldb + k0 + 2 * kp, sB + blk * 8 * DL_KC);
     } else {
       const int k = blk, cp = lane ^ (8 * (k & 3));
@@ -375,14 +385,14 @@ __device__ __forceinline__ void dl_mma_live(Acc<128>& acc, const double* sA, con
 #pragma unroll
     for (int mi = MLO; mi < MBR; ++mi) {
       const int row = qd.rb + mi * 16 + lr;
-      a[mi] = sA[row * DL_KC + 2 * (kp ^ (row & 7)) + ko];
+      a[mi] = sA[row * DL_KC + 2 * (kp ^ dl_sw(row)) + ko];
     }
 #pragma unroll
     for (int ni = 0; ni < MBC; ++ni) {
       if ((ni == 0 ? M0 : M1) >= MBR) continue;
       const int col = qd.cb + ni * 16 + lr;
       if (!NN)
-        b[ni] = sB[col * DL_KC + 2 * (kp ^ (col & 7)) + ko];
+        b[ni] = sB[col * DL_KC + 2 * (kp ^ dl_sw(col)) + ko];
       else
         b[ni] = sB[k * 128 + 2 * ((col >> 1) ^ (8 * (k & 3))) + (col & 1)];
     }
@@ -408,13 +418,13 @@ __device__ __forceinline__ void dl_mma_blocks(Acc<128>& acc, const double* sA, c
 #pragma unroll
     for (int mi = 0; mi < MBR; ++mi) {
       const int row = qd.rb + mi * 16 + lr;
-      a[mi] = sA[row * DL_KC + 2 * (kp ^ (row & 7)) + ko];
+      a[mi] = sA[row * DL_KC + 2 * (kp ^ dl_sw(row)) + ko];
     }
 #pragma unroll
     for (int ni = 0; ni < MBC; ++ni) {
       const int col = qd.cb + ni * 16 + lr;
       if (!NN)
-        b[ni] = sB[col * DL_KC + 2 * (kp ^ (col & 7)) + ko];
+        b[ni] = sB[col * DL_KC + 2 * (kp ^ dl_sw(col)) + ko];
       else
         b[ni] = sB[k * 128 + 2 * ((col >> 1) ^ (8 * (k & 3))) + (col & 1)];
     }
@@ -443,8 +453,8 @@ struct DenseRun {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int kp = 2 * s + (lk >> 1);
-      la[s] = 8u * (uint32_t)((qd.rb + lr) * DL_KC + 2 * (kp ^ (lr & 7)) + (lk & 1));
-      if (!NN) lb[s] = 8u * (uint32_t)(128 * DL_KC + (qd.cb + lr) * DL_KC + 2 * (kp ^ (lr & 7)) + (lk & 1));
+      la[s] = 8u * (uint32_t)((qd.rb + lr) * DL_KC + 2 * (kp ^ dl_sw(lr)) + (lk & 1));
+      if (!NN) lb[s] = 8u * (uint32_t)(128 * DL_KC + (qd.cb + lr) * DL_KC + 2 * (kp ^ dl_sw(lr)) + (lk & 1));
     }
     if (NN) {
 #pragma unroll
@@ -456,7 +466,7 @@ struct DenseRun {
     blk0 = 2 * wave;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int blk = blk0 + u, row = 8 * blk + (lane >> 3), kp = (lane & 7) ^ (row & 7);
+      const int blk = blk0 + u, row = 8 * blk + (lane >> 3), kp = (lane & 7) ^ dl_sw(row);
       ga[u] = 8u * (uint32_t)(row * lda + 2 * kp);
       gb[u] = NN ? 8u * (uint32_t)(blk * ldb + 2 * (lane ^ (8 * (blk & 3)))) : 8u * (uint32_t)(row * ldb + 2 * kp);
     }
