@@ -302,6 +302,9 @@ __device__ void gemm_stream(Acc<TM>& acc, const double* __restrict__ Ap, int lda
 #ifndef GPF_DENSE_DB
 #define GPF_DENSE_DB 1  // dense runs: double-buffered operand registers across k-steps (A/B knob)
 #endif
+#ifndef GPF_SHARED_RUNS
+#define GPF_SHARED_RUNS 1  // every liveness run (dense or partial) on the VALU-free loop (A/B knob)
+#endif
 #ifndef GPF_DENSE_RUN
 #define GPF_DENSE_RUN 1  // dense chunk runs without VALU address work (build-time A/B knob)
 #endif
@@ -485,64 +488,76 @@ struct DenseRun {
     }
   }
 
+  // operand reads of k-step s; only rows mi >= MLO and the live columns (patterns as in dl_mma_live)
+  template <int M0 = 0, int M1 = 0>
   __device__ __forceinline__ void reads(const char* sb, int s, double (&a)[4], double (&b)[2]) const {
+    constexpr int MLO = M0 < M1 ? M0 : M1;
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi) a[mi] = *(const double*)(sb + la[s] + mi * 16 * DL_KC * 8);
+    for (int mi = MLO; mi < 4; ++mi) a[mi] = *(const double*)(sb + la[s] + mi * 16 * DL_KC * 8);
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni)
+    for (int ni = 0; ni < 2; ++ni) {
+      if ((ni == 0 ? M0 : M1) >= 4) continue;
       b[ni] = NN ? *(const double*)(sb + lb[ni] + s * 512 * 8) : *(const double*)(sb + lb[s] + ni * 16 * DL_KC * 8);
+    }
   }
 
-  template <int BUF>
+  template <int BUF, int M0 = 0, int M1 = 0>
   __device__ __forceinline__ void mma(Acc<128>& acc, const double* smem) const {
+    if constexpr (M0 >= 4 && M1 >= 4) return;
+    constexpr int MLO = M0 < M1 ? M0 : M1;
     const char* sb = (const char*)smem + BUF * DL_BUF * 8;
 #if GPF_DENSE_DB
     // operands of k-step s+1 are read into the other register set before the MFMAs of step s
     double a[2][4], b[2][2];
-    reads(sb, 0, a[0], b[0]);
+    reads<M0, M1>(sb, 0, a[0], b[0]);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      if (s < 3) reads(sb, s + 1, a[(s + 1) & 1], b[(s + 1) & 1]);
+      if (s < 3) reads<M0, M1>(sb, s + 1, a[(s + 1) & 1], b[(s + 1) & 1]);
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
+      for (int mi = MLO; mi < 4; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni)
-          acc.v[mi][ni] = NEG ? mfma_neg_a(a[s & 1][mi], b[s & 1][ni], acc.v[mi][ni])
-                              : mfma(a[s & 1][mi], b[s & 1][ni], acc.v[mi][ni]);
+          if (mi >= (ni == 0 ? M0 : M1))
+            acc.v[mi][ni] = NEG ? mfma_neg_a(a[s & 1][mi], b[s & 1][ni], acc.v[mi][ni])
+                                : mfma(a[s & 1][mi], b[s & 1][ni], acc.v[mi][ni]);
     }
 #else
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       double a[4], b[2];
-      reads(sb, s, a, b);
+      reads<M0, M1>(sb, s, a, b);
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
+      for (int mi = MLO; mi < 4; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni)
-          acc.v[mi][ni] = NEG ? mfma_neg_a(a[mi], b[ni], acc.v[mi][ni]) : mfma(a[mi], b[ni], acc.v[mi][ni]);
+          if (mi >= (ni == 0 ? M0 : M1))
+            acc.v[mi][ni] = NEG ? mfma_neg_a(a[mi], b[ni], acc.v[mi][ni]) : mfma(a[mi], b[ni], acc.v[mi][ni]);
     }
 #endif
   }
 
-  template <int BUF>
+  template <int BUF, int M0 = 0, int M1 = 0>
   __device__ __forceinline__ void chunk(Acc<128>& acc, const double* Ap, const double* Bp, int ldb, int t, int nch,
                                         double* smem) const {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t + 1 < nch) issue<1 - BUF>(Ap, Bp, ldb, t + 1, smem);
-    mma<BUF>(acc, smem);
+    mma<BUF, M0, M1>(acc, smem);
   }
 
+  // chunks [t0, t1) with one MFMA pattern (M0, M1 as in dl_mma_live; <4, 4> keeps only the
+  // transfers and barriers)
+  template <int M0 = 0, int M1 = 0>
   __device__ __forceinline__ void run(Acc<128>& acc, const double* Ap, const double* Bp, int ldb, int t0, int t1,
                                       int nch, double* smem) const {
     int t = t0;
-    if (t < t1 && (t & 1)) chunk<1>(acc, Ap, Bp, ldb, t++, nch, smem);
+    if (t < t1 && (t & 1)) chunk<1, M0, M1>(acc, Ap, Bp, ldb, t++, nch, smem);
 #pragma unroll 1
     for (; t + 1 < t1; t += 2) {
-      chunk<0>(acc, Ap, Bp, ldb, t, nch, smem);
-      chunk<1>(acc, Ap, Bp, ldb, t + 1, nch, smem);
+      chunk<0, M0, M1>(acc, Ap, Bp, ldb, t, nch, smem);
+      chunk<1, M0, M1>(acc, Ap, Bp, ldb, t + 1, nch, smem);
     }
-    if (t < t1) chunk<0>(acc, Ap, Bp, ldb, t, nch, smem);
+    if (t < t1) chunk<0, M0, M1>(acc, Ap, Bp, ldb, t, nch, smem);
   }
 };
 
@@ -587,7 +602,12 @@ __device__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int
   // that the compiler's wait bookkeeping sees them done: otherwise it keeps an s_waitcnt for the
   // seed inside the K loop, where it also drains the asm-issued prefetch of the next chunk.
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
-#if GPF_DENSE_RUN
+#if GPF_SHARED_RUNS
+  // every run of this GEMM uses one set of per-lane offsets formed here: no VALU address work
+  // in any of the loops, and no per-pattern copies of hoisted offsets competing for VGPRs
+  const DenseRun<NN, NEG> dr(qd, lda, ldb, wave);
+#define GPF_RUN(m0, m1, a, b) dr.template run<m0, m1>(acc, Ar, Br, ldb, (a), (b), nch, smem)
+#elif GPF_DENSE_RUN
 #define GPF_RUN(m0, m1, a, b)                                                   \
   do {                                                                          \
     if constexpr (m0 == 0 && m1 == 0)                                           \
@@ -620,7 +640,15 @@ __device__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int
     GPF_RUN(4, 4, t4, nch);
   } else {  // TRI_C_LOWER: block live iff cb + 16 ni <= rb + 16 mi, for every chunk
     static_assert(TRI == TRI_C_LOWER, "known-zero pattern");
-#if GPF_SYRK_RUNS
+#if GPF_SHARED_RUNS
+    // coarse patterns: the one dead block of the (0,1) and (2,3) sub-tiles is computed as well
+    // (upper-triangle output, never read; the live blocks see the same MFMA sequence), so the
+    // SYRK needs no pattern of its own
+    const int dc = qd.cb - qd.rb;  // in {-64, -32, 0, 32, 64, 96}
+    if (dc <= 0) GPF_RUN(0, 0, 0, nch);
+    else if (dc <= 32) GPF_RUN(2, 2, 0, nch);
+    else GPF_RUN(4, 4, 0, nch);
+#elif GPF_SYRK_RUNS
     const int dc = qd.cb - qd.rb;  // in {-64, -32, 0, 32, 64, 96}
     if (dc < 0) GPF_RUN(0, 0, 0, nch);
     else if (dc == 0) GPF_RUN(0, 1, 0, nch);
