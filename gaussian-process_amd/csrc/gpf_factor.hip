@@ -661,12 +661,62 @@ __device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, con
   __syncthreads();
 }
 
+// ----------------------------------------------------------------------------
+// Split-K for launches with few tiles (a single particle: the prediction path, or small
+// swarms): the streamed GEMM of a tile is cut into S depth ranges, one workgroup each; every
+// workgroup writes its partial product to its slot, and the last one to arrive (agent-scope
+// release -> counter -> acquire, as the guide prescribes for cross-XCD hand-offs) sums the
+// partials in slot order (deterministic) and carries on with the rest of the tile. The
+// counter is reset by that last workgroup for the next launch.
+// ----------------------------------------------------------------------------
+template <bool NN, bool NEG>
+__device__ bool split_part(Acc<T>& acc, const double* Ap, int lda, const double* Bp, int ldb, int nch, int S,
+                           int s, double* __restrict__ pt, unsigned* __restrict__ ct, double* smem,
+                           const Quad<T>& qd, int* flag) {
+  const int c0 = s * nch / S, c1 = (s + 1) * nch / S;
+  if (c1 > c0) {
+    acc.zero();
+    gemm_stream_dl<NN, NEG>(acc, Ap + (size_t)c0 * DL_KC, lda, NN ? Bp + (size_t)c0 * DL_KC * ldb : Bp + (size_t)c0 * DL_KC,
+                            ldb, (c1 - c0) * DL_KC, smem, qd);
+    acc.store(qd, pt + (size_t)s * T * T, T);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (unsigned)(S - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(ct, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+// acc += the non-empty partials, in slot order
+__device__ __forceinline__ void split_sum(Acc<T>& acc, const double* pt, int nch, int S, const Quad<T>& qd) {
+  for (int s = 0; s < S; ++s) {
+    if ((s + 1) * nch / S == s * nch / S) continue;
+    const double* p0 = launder(pt + (size_t)s * T * T + (size_t)(qd.rb + (qd.lane >> 4)) * T + qd.cb + (qd.lane & 15));
+#pragma unroll
+    for (int mi = 0; mi < Acc<T>::MBR; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < Acc<T>::MBC; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc.v[mi][ni][r] = acc.v[mi][ni][r] + p0[(mi * 16 + 4 * r) * T + ni * 16];
+  }
+}
+
 // Tile w of block column J of particle p (the unit of work of k_step).
 __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad, double* __restrict__ Lb,
                                           double* __restrict__ Ub, double* __restrict__ yb,
                                           double* __restrict__ s2p, double* __restrict__ szp,
                                           int* __restrict__ info, int N, const double* __restrict__ x,
-                                          const double* __restrict__ ls, int d, double* smem, double* small) {
+                                          const double* __restrict__ ls, int d, int S, int sidx,
+                                          double* __restrict__ part, unsigned* __restrict__ cnt, int* sflag,
+                                          double* smem, double* small) {
   const int tid = threadIdx.x;
   const int nL = nt - 1 - J;
   const size_t ld = (size_t)Npad;
@@ -685,9 +735,19 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
     Acc<T> acc;
     // C = A_IJ - L_I,<J L_J,<J^T (accumulator seeded with A_IJ, A operand staged negated)
 #if GPF_KFUSE
-    cov_tile_acc(acc, qd, x, ls + (size_t)p * d, d, N, I, J, smem);
-    if (J > 0)
-      step_gemm<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, J * T, smem, qd);
+    if (S > 1 && J > 0) {  // split-K: partial GEMMs, the last workgroup to arrive finishes the tile
+      double* pt = part + (size_t)(p * (nt - 1) + w) * S * T * T;
+      if (!split_part<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, J * T / DL_KC, S,
+                                   sidx, pt, cnt + p * (nt - 1) + w, smem, qd, sflag))
+        return;
+      cov_tile_acc(acc, qd, x, ls + (size_t)p * d, d, N, I, J, smem);
+      split_sum(acc, pt, J * T / DL_KC, S, qd);
+    } else {
+      if (sidx > 0) return;  // nothing to split at J = 0
+      cov_tile_acc(acc, qd, x, ls + (size_t)p * d, d, N, I, J, smem);
+      if (J > 0)
+        step_gemm<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, J * T, smem, qd);
+    }
     acc.store(qd, Aij, ld);  // C (the TRMM below streams it)
 #else
     if (J > 0) {  // (at J = 0, C = A_IJ is already in place)
@@ -749,10 +809,20 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
     const int K = w - nL;
     double* Ujk = Up + (size_t)J * T * ld + (size_t)K * T;
     Acc<T> acc;
-    acc.zero();
     // W = L_J,[K,J) U_[K,J),K, parked in the U_JK slot
-    step_gemm<true, false, TRI_B_KGEC>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
-                                            Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T, smem, qd);
+    if (S > 1) {  // split-K (the triangular first block runs dense: its upper part holds zeros)
+      double* pt = part + (size_t)(p * (nt - 1) + w) * S * T * T;
+      if (!split_part<true, false>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
+                                   Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T / DL_KC, S, sidx, pt,
+                                   cnt + p * (nt - 1) + w, smem, qd, sflag))
+        return;
+      acc.zero();
+      split_sum(acc, pt, (J - K) * T / DL_KC, S, qd);
+    } else {
+      acc.zero();
+      step_gemm<true, false, TRI_B_KGEC>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
+                                              Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T, smem, qd);
+    }
     acc.store(qd, Ujk, ld);
     if (tid < T) zj[tid] = yp[J * T + tid];
     __syncthreads();
@@ -805,7 +875,8 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
                                                   double* __restrict__ s2p, double* __restrict__ szp,
                                                   int* __restrict__ info, int P, int grp, int N,
                                                   const double* __restrict__ x, const double* __restrict__ ls,
-                                                  int d) {
+                                                  int d, int S, double* __restrict__ part,
+                                                  unsigned* __restrict__ cnt) {
   const int tid = threadIdx.x;
 #ifdef GPF_WG_TRACE
   if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) {
@@ -818,9 +889,12 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
 #endif
   __shared__ __attribute__((aligned(16))) double smem[STEP_SMEM];
   __shared__ __attribute__((aligned(16))) double small[STEP_SMALL];
+  __shared__ int sflag;
+  const int tiles = P * (nt - 1);
+  const int sidx = (S > 1) ? (int)(blockIdx.x / tiles) : 0;  // split index, split-major dispatch
   int p, w;
-  step_tile(blockIdx.x, P, nt - 1, grp, p, w);
-  step_item(J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, smem, small);
+  step_tile(blockIdx.x - sidx * tiles, P, nt - 1, grp, p, w);
+  step_item(J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, sidx, part, cnt, &sflag, smem, small);
 #ifdef GPF_WG_TRACE
   __syncthreads();
   if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) g_wg_trace[J][blockIdx.x][1] = realtime();

@@ -72,6 +72,9 @@ struct gpf_ctx {
   double* d_U = nullptr;
   double* d_yb = nullptr;
   double* d_s2p = nullptr;
+  double* d_part = nullptr;    // split-K partial products (run_factor, few tiles per launch)
+  unsigned* d_cnt = nullptr;   // split-K arrival counters, one per (particle, tile), kept zero
+  size_t part_cap = 0, cnt_cap = 0;
   double* d_szp = nullptr;
   double* d_ls = nullptr;
   double* d_mu = nullptr;
@@ -176,6 +179,10 @@ static void free_work(gpf_ctx* c) {
   hipFree(c->d_L); hipFree(c->d_U); hipFree(c->d_yb); hipFree(c->d_s2p); hipFree(c->d_szp);
   hipFree(c->d_ls); hipFree(c->d_mu); hipFree(c->d_sd); hipFree(c->d_loss); hipFree(c->d_info);
   hipFree(c->d_hist);
+  hipFree(c->d_part); hipFree(c->d_cnt);
+  c->d_part = nullptr;
+  c->d_cnt = nullptr;
+  c->part_cap = c->cnt_cap = 0;
   c->d_L = c->d_U = c->d_yb = c->d_s2p = c->d_szp = c->d_ls = c->d_mu = c->d_sd = c->d_loss = nullptr;
   c->d_info = nullptr;
   c->d_hist = nullptr;
@@ -245,6 +252,38 @@ static int step_group(int pc) {
   return std::max(0, std::min(g, pc / 8));
 }
 
+// Split-K factor of the block-column launches: launches with at most 64 tiles (a single
+// particle: the prediction path) cut every tile's GEMM into S depth ranges (gpf::split_part), S
+// filling ~512 workgroup slots. Measured (profiles/r1/split_k_ab.txt): single-particle factor at
+// N=4096 11.3 -> 9.9 ms with S=16; config B (224 tiles, S=2) 21.3k -> 14.3k evals/s, hence the
+// threshold. GPF_SPLIT_K overrides (1 = off). Not for tiny problems (nt < 4).
+static int split_k(int tiles, int nt) {
+  int S = (nt >= 4 && GPF_KFUSE && tiles <= 64) ? std::max(1, std::min(16, 512 / std::max(1, tiles))) : 1;
+  if (const char* s = getenv("GPF_SPLIT_K")) S = std::max(1, std::min(32, atoi(s)));
+  if (nt < 4 || !GPF_KFUSE) S = 1;
+  return S;
+}
+
+static int ensure_split(gpf_ctx* c, int tiles, int S) {
+  const size_t pb = (size_t)tiles * S * T * T * 8, cb = (size_t)tiles * 4;
+  if (pb > c->part_cap) {
+    hipFree(c->d_part);
+    c->d_part = nullptr;
+    c->part_cap = 0;
+    GPF_HIP(c, hipMalloc(&c->d_part, pb));
+    c->part_cap = pb;
+  }
+  if (cb > c->cnt_cap) {
+    hipFree(c->d_cnt);
+    c->d_cnt = nullptr;
+    c->cnt_cap = 0;
+    GPF_HIP(c, hipMalloc(&c->d_cnt, cb));
+    GPF_HIP(c, hipMemset(c->d_cnt, 0, cb));  // the finishing workgroups re-zero what they used
+    c->cnt_cap = cb;
+  }
+  return GPF_OK;
+}
+
 // Factorise `pc` particles whose length scales are already in d_ls, in particle
 // groups on their own streams: per group the K build (lower 64x64 tiles), the first
 // diagonal block (k_diag), then one k_step per 128-wide block column (each also
@@ -304,17 +343,25 @@ static int run_factor(gpf_ctx* c, int pc) {
     if (rc) return rc;
     total += (2.0 / 3.0) * t3 * gc;
   }
+  // split-K for launches with few tiles (one set of partial slots per group, groups run concurrently)
+  const int gmax = (pc + ng - 1) / ng;
+  const int S = split_k(gmax * (nt - 1), nt);
+  if (S > 1) {
+    if (int rc = ensure_split(c, pc * (nt - 1), S)) return rc;
+  }
   // block columns interleaved across groups so every stream has work queued early
   for (int J = 0; nt > 1 && J < nt; ++J) {
     const double fl = step_flops(J);
     for (int g = 0; g < ng; ++g) {
       const int p0 = (int)((long long)pc * g / ng), gc = (int)((long long)pc * (g + 1) / ng) - p0;
       hipStream_t st = (ng > 1) ? c->sub[g] : c->stream;
+      double* partg = S > 1 ? c->d_part + (size_t)p0 * (nt - 1) * S * T * T : nullptr;
+      unsigned* cntg = S > 1 ? c->d_cnt + (size_t)p0 * (nt - 1) : nullptr;
       const int rc = launch_on(c, st, PC_PANEL, fl * gc, [&] {
-        hipLaunchKernelGGL(gpf::k_step, dim3(gc * (nt - 1)), dim3(gpf::STEP_NTH), 0, st, J, nt, Np,
+        hipLaunchKernelGGL(gpf::k_step, dim3(gc * (nt - 1) * S), dim3(gpf::STEP_NTH), 0, st, J, nt, Np,
                            c->d_L + (size_t)p0 * ld * ld, c->d_U + (size_t)p0 * ld * ld, c->d_yb + (size_t)p0 * ld,
                            c->d_s2p + (size_t)p0 * nt * ld, c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc,
-                           step_group(gc), N, c->d_x, c->d_ls + (size_t)p0 * c->d, c->d);
+                           step_group(gc), N, c->d_x, c->d_ls + (size_t)p0 * c->d, c->d, S, partg, cntg);
       });
       if (rc) return rc;
       total += fl * gc;

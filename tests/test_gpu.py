@@ -334,3 +334,29 @@ def test_large_hetero_vs_oracle_identity(ctx):
     assert _rel(sd[1], s1) < RTOL_MU_SD
     w = ref_cpu.coverage_loss(m1, s1, y, s, ex) + 0.01 * ref_cpu.proximity_penalty(P[1], lo, hi)
     assert abs(loss[1] - w) / w < 1e-6  # allows a rare |pull|=1 threshold flip
+
+
+@pytest.mark.parametrize("split", [2, 7])
+def test_split_k_matches_unsplit_and_oracle(ctx, monkeypatch, split):
+    """Split-K launches (gpf::split_part: partial GEMMs summed by the last workgroup to arrive)
+    against the unsplit path and the oracle. GPF_SPLIT_K forces the split factor."""
+    N, d = 1000, 3
+    rng = np.random.default_rng(11)
+    x = rng.uniform(size=(d, N))
+    y = np.sin(4 * x[0]) + x[1] * x[2] + 0.1 * rng.standard_normal(N)
+    e = rng.uniform(0.05, 0.2, size=N)
+    s, ex = ref_cpu.sigma_grid()
+    lo, hi = ref_cpu.search_bounds(x)
+    P = rng.uniform(0.1, 0.5, size=(4, d))
+    ctx.set_data(x, y, e)
+    ctx.set_grid(s, ex, lo, hi)
+    monkeypatch.setenv("GPF_SPLIT_K", "1")
+    l1, m1, s1 = ctx.eval_batch(P, want_mu_sd=True)
+    monkeypatch.setenv("GPF_SPLIT_K", str(split))
+    l2, m2, s2 = ctx.eval_batch(P, want_mu_sd=True)
+    l3, m3, s3 = ctx.eval_batch(P, want_mu_sd=True)
+    np.testing.assert_array_equal(m2, m3)  # deterministic: partials summed in slot order
+    assert _rel(m2, m1) < 1e-10 and _rel(s2, s1) < 1e-10
+    assert _rel(l2, l1) < RTOL_LOSS
+    mo, so = ref_cpu.GP_train_identity(x, y, e, P[2])
+    assert _rel(m2[2], mo) < RTOL_MU_SD and _rel(s2[2], so) < RTOL_MU_SD
