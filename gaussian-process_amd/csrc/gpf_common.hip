@@ -296,18 +296,6 @@ __device__ void gemm_stream(Acc<TM>& acc, const double* __restrict__ Ap, int lda
 //                  so the 4 k-rows of an operand read land 128 B apart.
 // NEG negates through the MFMA's own A-negate modifier. LDS: 2 x 2 x 128 x 16 doubles = 64 KiB.
 // ----------------------------------------------------------------------------
-#ifndef GPF_SYRK_RUNS
-#define GPF_SYRK_RUNS 0  // the SYRK's known-zero pattern as one loop per wave pattern (A/B knob)
-#endif
-#ifndef GPF_DENSE_DB
-#define GPF_DENSE_DB 1  // dense runs: double-buffered operand registers across k-steps (A/B knob)
-#endif
-#ifndef GPF_SHARED_RUNS
-#define GPF_SHARED_RUNS 1  // every liveness run (dense or partial) on the VALU-free loop (A/B knob)
-#endif
-#ifndef GPF_DENSE_RUN
-#define GPF_DENSE_RUN 1  // dense chunk runs without VALU address work (build-time A/B knob)
-#endif
 constexpr int DL_KC = 16;
 constexpr int DL_BUF = 2 * 128 * DL_KC;  // one stage (A + B), doubles
 constexpr int DL_STAGE = 2 * DL_BUF;     // double-buffered
@@ -343,102 +331,6 @@ __device__ __forceinline__ void dl_load(const double* g, double* l) {
 #define GPF_DL_SW 1
 #endif
 __device__ __forceinline__ int dl_sw(int r) { return GPF_DL_SW ? ((r >> 1) & 7) : (r & 7); }
-
-template <bool NN>
-__device__ __forceinline__ void dl_issue(const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
-                                         int ldb, int k0, double* sbuf, int wave, int lane) {
-  // 16 blocks of 1 KiB per operand per chunk; wave w issues blocks 2w and 2w+1 of each
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int blk = 2 * wave + u;
-    {
-      const int row = 8 * blk + (lane >> 3), kp = (lane & 7) ^ dl_sw(row);
-      dl_load(Ap + (size_t)row * lda + k0 + 2 * kp, sbuf + blk * 8 * DL_KC);
-    }
-    double* sB = sbuf + 128 * DL_KC;
-    if (!NN) {
-      const int row = 8 * blk + (lane >> 3), kp = (lane & 7) ^ dl_sw(row);
-      dl_load(Bp + (size_t)row * ldb + k0 + 2 * kp, sB + blk * 8 * DL_KC);
-    } else {
-      const int k = blk, cp = lane ^ (8 * (k & 3));
-      dl_load(Bp + (size_t)(k0 + k) * ldb + 2 * cp, sB + k * 128);
-    }
-  }
-}
-
-// One 16-deep chunk of MFMAs on the LDS stage. Block (mi, ni) of the wave's 64x32 sub-tile is
-// issued iff mi >= M0 (ni = 0) / mi >= M1 (ni = 1); 4 = the whole column is dead. Straight-line
-// code: operand reads of the next k-step can be scheduled across this one's MFMAs.
-template <bool NN, bool NEG, int M0, int M1>
-__device__ __forceinline__ void dl_mma_live(Acc<128>& acc, const double* sA, const double* sB, const Quad<128>& qd) {
-  constexpr int MBR = Geo<128>::MBR, MBC = Geo<128>::MBC;
-  static_assert(MBR == 4 && MBC == 2, "wave sub-tile geometry");
-  constexpr int MLO = M0 < M1 ? M0 : M1;
-  // Partial patterns (the triangular runs): the per-lane swizzled offsets are made opaque per
-  // chunk, so they are recomputed (a few VALU ops) instead of being hoisted out of the K loop
-  // once per variant, which overflows 128 VGPRs. The dense pattern keeps them hoisted: VALU
-  // work does not overlap the FP64 MFMAs of the same SIMD, so every op in the loop costs.
-  int lane = qd.lane;
-  if constexpr (M0 != 0 || M1 != 0) asm volatile("" : "+v"(lane));
-  const int lr = lane & 15, lk = lane >> 4;
-#pragma unroll
-  for (int ks = 0; ks < DL_KC; ks += 4) {
-    const int k = ks + lk, kp = k >> 1, ko = k & 1;
-    double a[MBR], b[MBC];
-#pragma unroll
-    for (int mi = MLO; mi < MBR; ++mi) {
-      const int row = qd.rb + mi * 16 + lr;
-      a[mi] = sA[row * DL_KC + 2 * (kp ^ dl_sw(row)) + ko];
-    }
-#pragma unroll
-    for (int ni = 0; ni < MBC; ++ni) {
-      if ((ni == 0 ? M0 : M1) >= MBR) continue;
-      const int col = qd.cb + ni * 16 + lr;
-      if (!NN)
-        b[ni] = sB[col * DL_KC + 2 * (kp ^ dl_sw(col)) + ko];
-      else
-        b[ni] = sB[k * 128 + 2 * ((col >> 1) ^ (8 * (k & 3))) + (col & 1)];
-    }
-#pragma unroll
-    for (int mi = MLO; mi < MBR; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < MBC; ++ni)
-        if (mi >= (ni == 0 ? M0 : M1))
-          acc.v[mi][ni] = NEG ? mfma_neg_a(a[mi], b[ni], acc.v[mi][ni]) : mfma(a[mi], b[ni], acc.v[mi][ni]);
-  }
-}
-
-// One chunk with a per-MFMA-block wave-uniform skip (tri_live).
-template <bool NN, bool NEG, int TRI>
-__device__ __forceinline__ void dl_mma_blocks(Acc<128>& acc, const double* sA, const double* sB, const Quad<128>& qd,
-                                              int k0) {
-  constexpr int MBR = Geo<128>::MBR, MBC = Geo<128>::MBC;
-  const int lr = qd.lane & 15, lk = qd.lane >> 4;
-#pragma unroll
-  for (int ks = 0; ks < DL_KC; ks += 4) {
-    const int k = ks + lk, kp = k >> 1, ko = k & 1;
-    double a[MBR], b[MBC];
-#pragma unroll
-    for (int mi = 0; mi < MBR; ++mi) {
-      const int row = qd.rb + mi * 16 + lr;
-      a[mi] = sA[row * DL_KC + 2 * (kp ^ dl_sw(row)) + ko];
-    }
-#pragma unroll
-    for (int ni = 0; ni < MBC; ++ni) {
-      const int col = qd.cb + ni * 16 + lr;
-      if (!NN)
-        b[ni] = sB[col * DL_KC + 2 * (kp ^ dl_sw(col)) + ko];
-      else
-        b[ni] = sB[k * 128 + 2 * ((col >> 1) ^ (8 * (k & 3))) + (col & 1)];
-    }
-#pragma unroll
-    for (int mi = 0; mi < MBR; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < MBC; ++ni)
-        if (tri_live<TRI>(qd.rb + mi * 16, qd.cb + ni * 16, k0 + ks))
-          acc.v[mi][ni] = NEG ? mfma_neg_a(a[mi], b[ni], acc.v[mi][ni]) : mfma(a[mi], b[ni], acc.v[mi][ni]);
-  }
-}
 
 // Dense chunks [t0, t1) (every MFMA block live) with no VALU address work inside the loop:
 // VALU ops do not overlap the FP64 MFMAs of their SIMD, so each one costs issue time. The per-lane
@@ -506,7 +398,6 @@ struct DenseRun {
     if constexpr (M0 >= 4 && M1 >= 4) return;
     constexpr int MLO = M0 < M1 ? M0 : M1;
     const char* sb = (const char*)smem + BUF * DL_BUF * 8;
-#if GPF_DENSE_DB
     // operands of k-step s+1 are read into the other register set before the MFMAs of step s
     double a[2][4], b[2][2];
     reads<M0, M1>(sb, 0, a[0], b[0]);
@@ -521,19 +412,6 @@ struct DenseRun {
             acc.v[mi][ni] = NEG ? mfma_neg_a(a[s & 1][mi], b[s & 1][ni], acc.v[mi][ni])
                                 : mfma(a[s & 1][mi], b[s & 1][ni], acc.v[mi][ni]);
     }
-#else
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      double a[4], b[2];
-      reads<M0, M1>(sb, s, a, b);
-#pragma unroll
-      for (int mi = MLO; mi < 4; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-          if (mi >= (ni == 0 ? M0 : M1))
-            acc.v[mi][ni] = NEG ? mfma_neg_a(a[mi], b[ni], acc.v[mi][ni]) : mfma(a[mi], b[ni], acc.v[mi][ni]);
-    }
-#endif
   }
 
   template <int BUF, int M0 = 0, int M1 = 0>
@@ -561,25 +439,6 @@ struct DenseRun {
   }
 };
 
-// Chunks [t0, t1) of the direct-to-LDS pipeline with one fixed MFMA pattern (M0, M1 as in
-// dl_mma_live; <4, 4> issues none but keeps the loads and barriers of its chunks).
-template <bool NN, bool NEG, int M0, int M1>
-__device__ __forceinline__ void dl_run(Acc<128>& acc, const double* __restrict__ Ap, int lda,
-                                       const double* __restrict__ Bp, int ldb, int t0, int t1, int nch, double* smem,
-                                       const Quad<128>& qd, int wave) {
-#pragma unroll 1
-  for (int t = t0; t < t1; ++t) {
-    // chunk t landed (own loads; barriers do not drain LDS-DMA) and everyone's are visible
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t + 1 < nch) dl_issue<NN>(Ap, lda, Bp, ldb, (t + 1) * DL_KC, smem + ((t + 1) & 1) * DL_BUF, wave, qd.lane);
-    if constexpr (M0 < 4 || M1 < 4) {
-      const double* cur = smem + (t & 1) * DL_BUF;
-      dl_mma_live<NN, NEG, M0, M1>(acc, cur, cur + 128 * DL_KC, qd);
-    }
-  }
-}
-
 // Known-zero skipping (Tri) at chunk granularity: every Tri boundary sits on a multiple of 16
 // in k, rows and columns, so whether an MFMA block contributes (tri_live) is the same for the
 // 4 k-steps of a 16-deep chunk, and per wave the chunks fall into a few contiguous runs with one
@@ -592,32 +451,18 @@ __device__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int
   const int nch = K / DL_KC;
   if (nch <= 0) return;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const double* Ar = Ap;  // scalar bases for the dense runs
+  const double* Ar = Ap;  // scalar bases
   const double* Br = Bp;
-  Ap = launder(Ap);
-  Bp = launder(Bp);
-  dl_issue<NN>(Ap, lda, Bp, ldb, 0, smem, wave, qd.lane);
+  const DenseRun<NN, NEG> dr(qd, lda, ldb, wave);
+  dr.template issue<0>(Ar, Br, ldb, 0, smem);
   // Drain every outstanding vector-memory op here (the chunk-0 transfers, which the first chunk
   // waits for anyway, and e.g. an accumulator seed loaded just before) through the builtin, so
   // that the compiler's wait bookkeeping sees them done: otherwise it keeps an s_waitcnt for the
   // seed inside the K loop, where it also drains the asm-issued prefetch of the next chunk.
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
-#if GPF_SHARED_RUNS
-  // every run of this GEMM uses one set of per-lane offsets formed here: no VALU address work
-  // in any of the loops, and no per-pattern copies of hoisted offsets competing for VGPRs
-  const DenseRun<NN, NEG> dr(qd, lda, ldb, wave);
+  // every run of this GEMM uses the one set of per-lane offsets formed above: no VALU address
+  // work in any of the loops, and no per-pattern copies of hoisted offsets competing for VGPRs
 #define GPF_RUN(m0, m1, a, b) dr.template run<m0, m1>(acc, Ar, Br, ldb, (a), (b), nch, smem)
-#elif GPF_DENSE_RUN
-#define GPF_RUN(m0, m1, a, b)                                                   \
-  do {                                                                          \
-    if constexpr (m0 == 0 && m1 == 0)                                           \
-      DenseRun<NN, NEG>(qd, lda, ldb, wave).run(acc, Ar, Br, ldb, (a), (b), nch, smem); \
-    else                                                                        \
-      dl_run<NN, NEG, m0, m1>(acc, Ap, lda, Bp, ldb, (a), (b), nch, smem, qd, wave); \
-  } while (0)
-#else
-#define GPF_RUN(m0, m1, a, b) dl_run<NN, NEG, m0, m1>(acc, Ap, lda, Bp, ldb, (a), (b), nch, smem, qd, wave)
-#endif
   if constexpr (TRI == TRI_NONE) {
     GPF_RUN(0, 0, 0, nch);
   } else if constexpr (TRI == TRI_B_KLEC) {  // column ni live iff 16 t <= cb + 16 ni
@@ -640,150 +485,17 @@ __device__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int
     GPF_RUN(4, 4, t4, nch);
   } else {  // TRI_C_LOWER: block live iff cb + 16 ni <= rb + 16 mi, for every chunk
     static_assert(TRI == TRI_C_LOWER, "known-zero pattern");
-#if GPF_SHARED_RUNS
     // coarse patterns: the one dead block of the (0,1) and (2,3) sub-tiles is computed as well
     // (upper-triangle output, never read; the live blocks see the same MFMA sequence), so the
-    // SYRK needs no pattern of its own
+    // SYRK needs no pattern of its own (per-pattern and per-block variants measured slower,
+    // profiles/r1/gemm_loop_ab.txt)
     const int dc = qd.cb - qd.rb;  // in {-64, -32, 0, 32, 64, 96}
     if (dc <= 0) GPF_RUN(0, 0, 0, nch);
     else if (dc <= 32) GPF_RUN(2, 2, 0, nch);
     else GPF_RUN(4, 4, 0, nch);
-#elif GPF_SYRK_RUNS
-    const int dc = qd.cb - qd.rb;  // in {-64, -32, 0, 32, 64, 96}
-    if (dc < 0) GPF_RUN(0, 0, 0, nch);
-    else if (dc == 0) GPF_RUN(0, 1, 0, nch);
-    else if (dc <= 32) GPF_RUN(2, 3, 0, nch);
-    else GPF_RUN(4, 4, 0, nch);
-#else
-    // one loop with per-block wave-uniform branches (profiles/r1/gemm_loop_ab.txt)
-#pragma unroll 1
-    for (int t = 0; t < nch; ++t) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (t + 1 < nch) dl_issue<NN>(Ap, lda, Bp, ldb, (t + 1) * DL_KC, smem + ((t + 1) & 1) * DL_BUF, wave, qd.lane);
-      const double* cur = smem + (t & 1) * DL_BUF;
-      dl_mma_blocks<NN, NEG, TRI>(acc, cur, cur + 128 * DL_KC, qd, t * DL_KC);
-    }
-#endif
   }
 #undef GPF_RUN
   __syncthreads();
-}
-
-// ----------------------------------------------------------------------------
-// Ring variant (experiment): 8-deep chunks in a ring of RING LDS buffers (RING x 16 KiB),
-// prefetch distance DIST chunks (the loads of chunks ph+1 .. ph+DIST-1 stay in flight across
-// phase ph), one raw s_barrier per chunk with counted vmcnt. STAG = 1: waves 4-7 (the SIMD
-// partners of waves 0-3) compute one chunk behind waves 0-3, so the two waves sharing a SIMD
-// never reach their LDS reads and MFMA bursts together.
-//   chunk c lives in buffer c % RING, read in phase c (and c+1 when STAG); chunk ph+DIST is
-//   issued after the barrier that opens phase ph, into the buffer last read in phase
-//   ph+DIST-RING+STAG <= ph-1; each wave waits for its own loads of chunk ph before that barrier.
-// [r][k] layout: a 1 KiB block holds 16 rows x 4 k-pairs; pair kp of row r sits in slot
-// kp ^ ((r >> 2) & 3). [k][c] layout as in gemm_stream_dl.
-// ----------------------------------------------------------------------------
-constexpr int D8_KC = 8;
-constexpr int D8_BUF = 2 * 128 * D8_KC;  // one chunk (A + B), doubles
-
-template <bool NN>
-__device__ __forceinline__ void d8_issue(const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
-                                         int ldb, int k0, double* sbuf, int wave, int lane) {
-  {
-    const int row = 16 * wave + (lane >> 2), kp = (lane & 3) ^ ((row >> 2) & 3);
-    dl_load(Ap + (size_t)row * lda + k0 + 2 * kp, sbuf + wave * 128);
-  }
-  double* sB = sbuf + 128 * D8_KC;
-  if (!NN) {
-    const int row = 16 * wave + (lane >> 2), kp = (lane & 3) ^ ((row >> 2) & 3);
-    dl_load(Bp + (size_t)row * ldb + k0 + 2 * kp, sB + wave * 128);
-  } else {
-    const int k = wave, cp = lane ^ (8 * (k & 3));
-    dl_load(Bp + (size_t)(k0 + k) * ldb + 2 * cp, sB + k * 128);
-  }
-}
-
-template <bool NN, bool NEG, int TRI>
-__device__ __forceinline__ void d8_mma(Acc<128>& acc, const double* sA, const double* sB, const Quad<128>& qd, int k0) {
-  constexpr int MBR = Geo<128>::MBR, MBC = Geo<128>::MBC;
-  const int lr = qd.lane & 15, lk = qd.lane >> 4;
-#pragma unroll
-  for (int ks = 0; ks < D8_KC; ks += 4) {
-    const int k = ks + lk, kp = k >> 1, ko = k & 1;
-    double a[MBR], b[MBC];
-#pragma unroll
-    for (int mi = 0; mi < MBR; ++mi) {
-      const int row = qd.rb + mi * 16 + lr;
-      a[mi] = sA[row * D8_KC + 2 * (kp ^ ((row >> 2) & 3)) + ko];
-    }
-#pragma unroll
-    for (int ni = 0; ni < MBC; ++ni) {
-      const int col = qd.cb + ni * 16 + lr;
-      if (!NN)
-        b[ni] = sB[col * D8_KC + 2 * (kp ^ ((col >> 2) & 3)) + ko];
-      else
-        b[ni] = sB[k * 128 + 2 * ((col >> 1) ^ (8 * (k & 3))) + (col & 1)];
-    }
-#pragma unroll
-    for (int mi = 0; mi < MBR; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < MBC; ++ni)
-        if (tri_live<TRI>(qd.rb + mi * 16, qd.cb + ni * 16, k0 + ks))
-          acc.v[mi][ni] = NEG ? mfma_neg_a(a[mi], b[ni], acc.v[mi][ni]) : mfma(a[mi], b[ni], acc.v[mi][ni]);
-  }
-}
-
-__device__ __forceinline__ void raw_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-// s_waitcnt vmcnt(2 n) for a run-time n in [0, 7) (each chunk is two loads per wave)
-__device__ __forceinline__ void wait_chunks(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-  }
-}
-
-template <bool NN, bool NEG = false, int TRI = TRI_NONE, int RING = 4, int DIST = 2, int STAG = 1>
-__device__ void gemm_stream_ring(Acc<128>& acc, const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
-                                 int ldb, int K, double* smem, const Quad<128>& qd) {
-  static_assert(DIST >= 1 && DIST <= RING - 1 - STAG && DIST <= 7, "ring reuse distance");
-  const int nch = K / D8_KC;
-  if (nch <= 0) return;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = STAG ? (wave >> 2) : 0;
-  Ap = launder(Ap);
-  Bp = launder(Bp);
-#pragma unroll
-  for (int c = 0; c < DIST; ++c)
-    if (c < nch) d8_issue<NN>(Ap, lda, Bp, ldb, c * D8_KC, smem + (c % RING) * D8_BUF, wave, qd.lane);
-#pragma unroll 1
-  for (int ph = 0; ph < nch + STAG; ++ph) {
-    const int left = nch - 1 - ph;
-    wait_chunks(left <= 0 ? 0 : (left < DIST - 1 ? left : DIST - 1));
-    raw_barrier();
-    if (ph + DIST < nch)
-      d8_issue<NN>(Ap, lda, Bp, ldb, (ph + DIST) * D8_KC, smem + ((ph + DIST) % RING) * D8_BUF, wave, qd.lane);
-    const int c = ph - g;
-    if (c >= 0 && c < nch) {
-      const double* cur = smem + (c % RING) * D8_BUF;
-      d8_mma<NN, NEG, TRI>(acc, cur, cur + 128 * D8_KC, qd, c * D8_KC);
-    }
-  }
-  __syncthreads();
-}
-
-template <bool NN, bool NEG = false, int TRI = TRI_NONE>
-__device__ void gemm_stream_d8(Acc<128>& acc, const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
-                               int ldb, int K, double* smem, const Quad<128>& qd) {
-  gemm_stream_ring<NN, NEG, TRI, 4, 2, 1>(acc, Ap, lda, Bp, ldb, K, smem, qd);
 }
 
 // 64x64x64 GEMM with both operands resident in LDS (8 waves, 32x16 each):

@@ -590,18 +590,13 @@ __device__ __forceinline__ unsigned long long realtime() {
 #define GPF_PHASE(k)
 #endif
 
-#ifndef GPF_D8
-#define GPF_D8 0  // staggered 8-deep ring (gemm_stream_d8) in the block-column GEMMs (build-time A/B knob)
-#endif
 #ifndef GPF_DL
 #define GPF_DL 1  // direct-to-LDS staging in the block-column GEMMs (build-time A/B knob)
 #endif
 template <bool NN, bool NEG = false, int TRI = TRI_NONE>
 __device__ __forceinline__ void step_gemm(Acc<T>& acc, const double* Ap, int lda, const double* Bp, int ldb, int K,
                                           double* smem, const Quad<T>& qd) {
-#if GPF_D8
-  gemm_stream_d8<NN, NEG, TRI>(acc, Ap, lda, Bp, ldb, K, smem, qd);
-#elif GPF_DL
+#if GPF_DL
   gemm_stream_dl<NN, NEG, TRI>(acc, Ap, lda, Bp, ldb, K, smem, qd);
 #else
   gemm_stream<T, NN, NEG, TRI>(acc, Ap, lda, Bp, ldb, K, smem, qd);
@@ -765,23 +760,10 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
     if (tid < T) zj[tid] = yp[J * T + tid];
     __syncthreads();
     GPF_PHASE(1);
-    // look-ahead: A_II -= L_IJ L_IJ^T (the full tile; only its lower half is ever read), y_I -= L_IJ z_J.
-    // GPF_SYRK_PAIR: the rank-128 updates of A_II are paired — applied at odd J as one rank-256
-    // update with L_I,[J-1,J] — except that the next diagonal block (I = J+1) always takes all of
-    // its pending columns before it is factored; half the A_II read-modify-write passes.
-#ifndef GPF_SYRK_TRI
-#define GPF_SYRK_TRI TRI_C_LOWER  // A/B knob: TRI_NONE computes the whole tile with the dense loop
-#endif
-#ifndef GPF_SYRK_PAIR
-#define GPF_SYRK_PAIR 0  // measured: C +0.3%, B -1.8% (bitwise equal)
-#endif
-    const int j0 = (GPF_SYRK_PAIR && (J & 1)) ? J - 1 : J;
-    if (!GPF_SYRK_PAIR || (J & 1) || I == J + 1) {
-      const double* Lsy = Lp + (size_t)I * T * ld + (size_t)j0 * T;
-      acc.load(qd, Aii, ld);
-      step_gemm<false, true, GPF_SYRK_TRI>(acc, Lsy, Npad, Lsy, Npad, (J - j0 + 1) * T, smem, qd);
-      acc.store(qd, Aii, ld);
-    }
+    // look-ahead: A_II -= L_IJ L_IJ^T (the full tile; only its lower half is ever read), y_I -= L_IJ z_J
+    acc.load(qd, Aii, ld);
+    step_gemm<false, true, TRI_C_LOWER>(acc, Aij, Npad, Aij, Npad, T, smem, qd);
+    acc.store(qd, Aii, ld);
     GPF_PHASE(2);
     {
       const int r = tid & (T - 1), h = tid >> 7;  // 4 quarter-row partial dot products
@@ -942,25 +924,7 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_gemm_benc
   const Quad<T> qd;
   Acc<T> acc;
   acc.zero();
-  if (mode & 8) {  // ring variants (gemm_stream_ring), configuration mode >> 4
-    const double* A0 = Lp + (size_t)I * T * ld;
-    const double* B0 = (mode & 4) ? Lp + (size_t)w * T : Lp + (size_t)J * T * ld;
-    switch (mode >> 4) {
-#define GPF_RING_CASE(id, R, Dd, S)                                                                  \
-  case id:                                                                                         \
-    if (mode & 4)                                                                                  \
-      gemm_stream_ring<true, false, TRI_NONE, R, Dd, S>(acc, A0, Npad, B0, Npad, D, smem, qd);     \
-    else                                                                                           \
-      gemm_stream_ring<false, true, TRI_NONE, R, Dd, S>(acc, A0, Npad, B0, Npad, D, smem, qd);     \
-    break;
-      GPF_RING_CASE(0, 4, 2, 1)  // = gemm_stream_d8
-      GPF_RING_CASE(1, 4, 3, 0)  // 24-deep prefetch
-      GPF_RING_CASE(2, 4, 2, 0)  // 16-deep prefetch (the default path's distance)
-      GPF_RING_CASE(3, 4, 1, 0)  // 8-deep prefetch
-#undef GPF_RING_CASE
-      default: break;
-    }
-  } else if (direct && (mode & 4))  // U-tile shape: B given as a [k][c] row panel (NN)
+  if (direct && (mode & 4))  // U-tile shape: B given as a [k][c] row panel (NN)
     gemm_stream_dl<true, false>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)w * T, Npad, D, smem, qd);
   else if (direct)
     gemm_stream_dl<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, D, smem, qd);
