@@ -705,6 +705,7 @@ __device__ __forceinline__ void split_sum(Acc<T>& acc, const double* pt, int nch
 }
 
 // Tile w of block column J of particle p (the unit of work of k_step).
+template <bool SPLIT>
 __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad, double* __restrict__ Lb,
                                           double* __restrict__ Ub, double* __restrict__ yb,
                                           double* __restrict__ s2p, double* __restrict__ szp,
@@ -730,7 +731,7 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
     Acc<T> acc;
     // C = A_IJ - L_I,<J L_J,<J^T (accumulator seeded with A_IJ, A operand staged negated)
 #if GPF_KFUSE
-    if (S > 1 && J > 0) {  // split-K: partial GEMMs, the last workgroup to arrive finishes the tile
+    if (SPLIT && J > 0) {  // split-K: partial GEMMs, the last workgroup to arrive finishes the tile
       double* pt = part + (size_t)(p * (nt - 1) + w) * S * T * T;
       if (!split_part<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, J * T / DL_KC, S,
                                    sidx, pt, cnt + p * (nt - 1) + w, smem, qd, sflag))
@@ -738,7 +739,7 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
       cov_tile_acc(acc, qd, x, ls + (size_t)p * d, d, N, I, J, smem);
       split_sum(acc, pt, J * T / DL_KC, S, qd);
     } else {
-      if (sidx > 0) return;  // nothing to split at J = 0
+      if (SPLIT && sidx > 0) return;  // nothing to split at J = 0
       cov_tile_acc(acc, qd, x, ls + (size_t)p * d, d, N, I, J, smem);
       if (J > 0)
         step_gemm<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, J * T, smem, qd);
@@ -792,7 +793,7 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
     double* Ujk = Up + (size_t)J * T * ld + (size_t)K * T;
     Acc<T> acc;
     // W = L_J,[K,J) U_[K,J),K, parked in the U_JK slot
-    if (S > 1) {  // split-K (the triangular first block runs dense: its upper part holds zeros)
+    if (SPLIT) {  // split-K (the triangular first block runs dense: its upper part holds zeros)
       double* pt = part + (size_t)(p * (nt - 1) + w) * S * T * T;
       if (!split_part<true, false>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
                                    Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T / DL_KC, S, sidx, pt,
@@ -852,6 +853,9 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
   }
 }
 
+// SPLIT: split-K instantiation (launches with few tiles); the other one has no split code at all,
+// so its register allocation is that of the plain schedule.
+template <bool SPLIT>
 __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int J, int nt, int Npad, double* __restrict__ Lb,
                                                   double* __restrict__ Ub, double* __restrict__ yb,
                                                   double* __restrict__ s2p, double* __restrict__ szp,
@@ -873,10 +877,11 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
   __shared__ __attribute__((aligned(16))) double small[STEP_SMALL];
   __shared__ int sflag;
   const int tiles = P * (nt - 1);
-  const int sidx = (S > 1) ? (int)(blockIdx.x / tiles) : 0;  // split index, split-major dispatch
+  const int sidx = SPLIT ? (int)(blockIdx.x / tiles) : 0;  // split index, split-major dispatch
   int p, w;
   step_tile(blockIdx.x - sidx * tiles, P, nt - 1, grp, p, w);
-  step_item(J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, sidx, part, cnt, &sflag, smem, small);
+  step_item<SPLIT>(J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, sidx, part, cnt, &sflag, smem,
+                   small);
 #ifdef GPF_WG_TRACE
   __syncthreads();
   if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) g_wg_trace[J][blockIdx.x][1] = realtime();

@@ -358,7 +358,8 @@ static int run_factor(gpf_ctx* c, int pc) {
       double* partg = S > 1 ? c->d_part + (size_t)p0 * (nt - 1) * S * T * T : nullptr;
       unsigned* cntg = S > 1 ? c->d_cnt + (size_t)p0 * (nt - 1) : nullptr;
       const int rc = launch_on(c, st, PC_PANEL, fl * gc, [&] {
-        hipLaunchKernelGGL(gpf::k_step, dim3(gc * (nt - 1) * S), dim3(gpf::STEP_NTH), 0, st, J, nt, Np,
+        hipLaunchKernelGGL(S > 1 ? gpf::k_step<true> : gpf::k_step<false>, dim3(gc * (nt - 1) * S),
+                           dim3(gpf::STEP_NTH), 0, st, J, nt, Np,
                            c->d_L + (size_t)p0 * ld * ld, c->d_U + (size_t)p0 * ld * ld, c->d_yb + (size_t)p0 * ld,
                            c->d_s2p + (size_t)p0 * nt * ld, c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc,
                            step_group(gc), N, c->d_x, c->d_ls + (size_t)p0 * c->d, c->d, S, partg, cntg);
