@@ -360,3 +360,29 @@ def test_split_k_matches_unsplit_and_oracle(ctx, monkeypatch, split):
     assert _rel(l2, l1) < RTOL_LOSS
     mo, so = ref_cpu.GP_train_identity(x, y, e, P[2])
     assert _rel(m2[2], mo) < RTOL_MU_SD and _rel(s2[2], so) < RTOL_MU_SD
+
+
+@pytest.mark.parametrize("N,d,hetero,seed", [(130, 1, False, 1), (383, 5, True, 2), (512, 2, True, 3),
+                                             (777, 3, False, 4), (1500, 4, True, 5), (2049, 2, False, 6)])
+def test_random_configs_vs_oracle(ctx, N, d, hetero, seed):
+    """Sweep of sizes off the tile grid, dimensionalities 1..5 and both noise models: every
+    particle's mean/sd against the oracle (the reference op sequence up to N=777, the identity
+    form above) and the objective against the oracle's scoring of those."""
+    rng = np.random.default_rng(100 + seed)
+    x = rng.uniform(0, 1, size=(d, N))
+    y = np.sum(np.cos(3 * x), axis=0) + 0.05 * rng.standard_normal(N)
+    e = rng.uniform(0.05, 0.2, size=N) if hetero else np.full(N, 0.1)
+    s, ex = ref_cpu.sigma_grid()
+    lo, hi = ref_cpu.search_bounds(x)
+    P = rng.uniform(0.08, 0.6, size=(3, d))
+    ctx.set_data(x, y, e)
+    ctx.set_grid(s, ex, lo, hi)
+    loss, mu, sd = ctx.eval_batch(P, want_mu_sd=True)
+    for k in range(3):
+        if N <= 777:
+            m0, s0 = ref_cpu.GP(x, y, e, x, P[k], batch_size=N)
+        else:
+            m0, s0 = ref_cpu.GP_train_identity(x, y, e, P[k])
+        assert _rel(mu[k], m0) < RTOL_MU_SD and _rel(sd[k], s0) < RTOL_MU_SD
+        w = ref_cpu.coverage_loss(m0, s0, y, s, ex) + 0.01 * ref_cpu.proximity_penalty(P[k], lo, hi)
+        assert abs(loss[k] - w) / w < 1e-6  # allows a rare |pull|=1 threshold flip (SURVEY.md §7)
