@@ -139,6 +139,21 @@ template <int TM> struct Acc {
 #pragma unroll
         for (int r = 0; r < 4; ++r) p0[(size_t)(mi * 16 + 4 * r) * ld + ni * 16] = v[mi][ni][r];
   }
+  // store() with write-through (sc1) stores: the tile reaches memory without an L2
+  // write-back fence, for a hand-off to another workgroup inside the launch (split-K)
+  __device__ __forceinline__ void store_wt(const Quad<TM>& q, double* base, size_t ld) const {
+    using G = __attribute__((address_space(1))) unsigned long long*;
+    G p0 = (G)launder(base + (size_t)(q.rb + (q.lane >> 4)) * ld + q.cb + (q.lane & 15));
+#pragma unroll
+    for (int mi = 0; mi < MBR; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < MBC; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          __hip_atomic_store(p0 + (size_t)(mi * 16 + 4 * r) * ld + ni * 16,
+                             (unsigned long long)__double_as_longlong(v[mi][ni][r]), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  }
   // Visit each owned element together with its slot in a row-major global tile.
   // The per-lane base is formed once; the per-element offsets are wave-uniform
   // (scalar registers), so no per-element 64-bit address stays live.

@@ -659,8 +659,9 @@ __device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, con
 // ----------------------------------------------------------------------------
 // Split-K for launches with few tiles (a single particle: the prediction path, or small
 // swarms): the streamed GEMM of a tile is cut into S depth ranges, one workgroup each; every
-// workgroup writes its partial product to its slot, and the last one to arrive (agent-scope
-// release -> counter -> acquire, as the guide prescribes for cross-XCD hand-offs) sums the
+// workgroup writes its partial product to its slot with write-through (sc1) stores, drains
+// them, takes a ticket, and the last one to arrive (agent-scope acquire; no release fence: its
+// L2 write-back stalled on every dirty line of the XCD, ~10-100 us per piece here) sums the
 // partials in slot order (deterministic) and carries on with the rest of the tile. The
 // counter is reset by that last workgroup for the next launch.
 // ----------------------------------------------------------------------------
@@ -673,15 +674,16 @@ __device__ bool split_part(Acc<T>& acc, const double* Ap, int lda, const double*
     acc.zero();
     gemm_stream_dl<NN, NEG>(acc, Ap + (size_t)c0 * DL_KC, lda, NN ? Bp + (size_t)c0 * DL_KC * ldb : Bp + (size_t)c0 * DL_KC,
                             ldb, (c1 - c0) * DL_KC, smem, qd);
-    acc.store(qd, pt + (size_t)s * T * T, T);
+    acc.store_wt(qd, pt + (size_t)s * T * T, T);  // write-through: no release (L2 write-back) fence
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its partial before the ticket
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned old = __hip_atomic_fetch_add(ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = old == (unsigned)(S - 1);
     if (last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(ct, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     *flag = last;
@@ -704,8 +706,10 @@ __device__ __forceinline__ void split_sum(Acc<T>& acc, const double* pt, int nch
   }
 }
 
+enum { SPLIT_NONE = 0, SPLIT_ALL = 1, SPLIT_CRIT = 2 };
+
 // Tile w of block column J of particle p (the unit of work of k_step).
-template <bool SPLIT>
+template <int SPLIT>
 __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad, double* __restrict__ Lb,
                                           double* __restrict__ Ub, double* __restrict__ yb,
                                           double* __restrict__ s2p, double* __restrict__ szp,
@@ -731,7 +735,8 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
     Acc<T> acc;
     // C = A_IJ - L_I,<J L_J,<J^T (accumulator seeded with A_IJ, A operand staged negated)
 #if GPF_KFUSE
-    if (SPLIT && J > 0) {  // split-K: partial GEMMs, the last workgroup to arrive finishes the tile
+    if ((SPLIT == SPLIT_ALL || (SPLIT == SPLIT_CRIT && w == 0)) && J > 0) {
+      // split-K: partial GEMMs, the last workgroup to arrive finishes the tile
       double* pt = part + (size_t)(p * (nt - 1) + w) * S * T * T;
       if (!split_part<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, J * T / DL_KC, S,
                                    sidx, pt, cnt + p * (nt - 1) + w, smem, qd, sflag))
@@ -793,7 +798,7 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
     double* Ujk = Up + (size_t)J * T * ld + (size_t)K * T;
     Acc<T> acc;
     // W = L_J,[K,J) U_[K,J),K, parked in the U_JK slot
-    if (SPLIT) {  // split-K (the triangular first block runs dense: its upper part holds zeros)
+    if (SPLIT == SPLIT_ALL) {  // split-K (the triangular first block runs dense: its upper part holds zeros)
       double* pt = part + (size_t)(p * (nt - 1) + w) * S * T * T;
       if (!split_part<true, false>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
                                    Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T / DL_KC, S, sidx, pt,
@@ -853,9 +858,11 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
   }
 }
 
-// SPLIT: split-K instantiation (launches with few tiles); the other one has no split code at all,
-// so its register allocation is that of the plain schedule.
-template <bool SPLIT>
+// SPLIT: SPLIT_ALL cuts every tile (launches with few tiles), SPLIT_CRIT only the critical-path
+// tile I = J+1 of each particle (launches that leave slots idle: its S pieces are dispatched
+// first, ahead of the unsplit tiles); SPLIT_NONE carries no split code at all, so its register
+// allocation is that of the plain schedule.
+template <int SPLIT>
 __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int J, int nt, int Npad, double* __restrict__ Lb,
                                                   double* __restrict__ Ub, double* __restrict__ yb,
                                                   double* __restrict__ s2p, double* __restrict__ szp,
@@ -877,9 +884,17 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
   __shared__ __attribute__((aligned(16))) double small[STEP_SMALL];
   __shared__ int sflag;
   const int tiles = P * (nt - 1);
-  const int sidx = SPLIT ? (int)(blockIdx.x / tiles) : 0;  // split index, split-major dispatch
-  int p, w;
-  step_tile(blockIdx.x - sidx * tiles, P, nt - 1, grp, p, w);
+  int p, w, sidx = 0;
+  if (SPLIT == SPLIT_ALL) {
+    sidx = (int)(blockIdx.x / tiles);  // split index, split-major dispatch
+    step_tile(blockIdx.x - sidx * tiles, P, nt - 1, grp, p, w);
+  } else if (SPLIT == SPLIT_CRIT && (int)blockIdx.x < P * S) {  // the S pieces of the critical tiles
+    p = (int)blockIdx.x % P;
+    w = 0;
+    sidx = (int)blockIdx.x / P;
+  } else {  // particle-fastest order (grp = 0) puts the critical tiles w = 0 at b < P
+    step_tile((int)blockIdx.x - (SPLIT == SPLIT_CRIT ? P * (S - 1) : 0), P, nt - 1, grp, p, w);
+  }
   step_item<SPLIT>(J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, sidx, part, cnt, &sflag, smem,
                    small);
 #ifdef GPF_WG_TRACE

@@ -255,12 +255,34 @@ static int step_group(int pc) {
 // Split-K factor of the block-column launches: launches with at most 64 tiles (a single
 // particle: the prediction path) cut every tile's GEMM into S depth ranges (gpf::split_part), S
 // filling ~512 workgroup slots. Measured (profiles/r1/split_k_ab.txt): single-particle factor at
-// N=4096 11.3 -> 9.9 ms with S=16; config B (224 tiles, S=2) 21.3k -> 14.3k evals/s, hence the
+// N=4096 11.3 -> 9.9 ms with S=16 (7.4 ms since the partials are stored write-through, with no
+// release fence); config B (224 tiles, S=2) 21.3k -> 14.3k evals/s with the fence, hence the
 // threshold. GPF_SPLIT_K overrides (1 = off). Not for tiny problems (nt < 4).
 static int split_k(int tiles, int nt) {
   int S = (nt >= 4 && GPF_KFUSE && tiles <= 64) ? std::max(1, std::min(16, 512 / std::max(1, tiles))) : 1;
   if (const char* s = getenv("GPF_SPLIT_K")) S = std::max(1, std::min(32, atoi(s)));
   if (nt < 4 || !GPF_KFUSE) S = 1;
+  return S;
+}
+
+// Critical-tile split of block-column launch J (gpf::SPLIT_CRIT), for launches that leave
+// workgroup slots idle (small N: the launch time is the latency of the tile I = J+1, which runs
+// the depth-128J GEMM, the look-ahead update and the next diagonal factor in sequence): that
+// tile's GEMM is cut into S depth ranges run by S workgroups dispatched ahead of the rest.
+// Needs the particle-fastest tile order (grp = 0). pc: the particles of all concurrent groups
+// (they share the 512 workgroup slots). Pieces of at least 20 16-deep chunks: shorter ones lose
+// more to the partial round trip than they save (A/B, profiles/r1/split_crit_ab.txt: N=1024
+// P=32 +2.4% at S <= 2, -5..-12% with 8-chunk pieces; N=2048 P=32 +12% at S = 4).
+// GPF_SPLIT_CRIT = maximum S (1 = off), GPF_SPLIT_CRIT_MIN = minimum chunks per piece.
+static int split_crit(int pc, int nt, int J, int grp, int S_all) {
+  if (S_all > 1 || grp > 0 || J == 0 || nt < 4 || !GPF_KFUSE) return 1;
+  const int slots = 512, tiles = pc * (nt - 1);
+  int S = 4, minch = 20;
+  if (const char* s = getenv("GPF_SPLIT_CRIT")) S = std::max(1, std::min(32, atoi(s)));
+  if (const char* s = getenv("GPF_SPLIT_CRIT_MIN")) minch = std::max(2, atoi(s));
+  const int nch = J * T / gpf::DL_KC;
+  S = std::min(S, std::max(1, nch / minch));
+  while (S > 1 && tiles + pc * (S - 1) > slots) --S;
   return S;
 }
 
@@ -346,8 +368,10 @@ static int run_factor(gpf_ctx* c, int pc) {
   // split-K for launches with few tiles (one set of partial slots per group, groups run concurrently)
   const int gmax = (pc + ng - 1) / ng;
   const int S = split_k(gmax * (nt - 1), nt);
-  if (S > 1) {
-    if (int rc = ensure_split(c, pc * (nt - 1), S)) return rc;
+  int Smax = S;
+  for (int J = 1; S == 1 && J < nt; ++J) Smax = std::max(Smax, split_crit(pc, nt, J, step_group(gmax), S));
+  if (Smax > 1) {
+    if (int rc = ensure_split(c, pc * (nt - 1), Smax)) return rc;
   }
   // block columns interleaved across groups so every stream has work queued early
   for (int J = 0; nt > 1 && J < nt; ++J) {
@@ -355,14 +379,20 @@ static int run_factor(gpf_ctx* c, int pc) {
     for (int g = 0; g < ng; ++g) {
       const int p0 = (int)((long long)pc * g / ng), gc = (int)((long long)pc * (g + 1) / ng) - p0;
       hipStream_t st = (ng > 1) ? c->sub[g] : c->stream;
-      double* partg = S > 1 ? c->d_part + (size_t)p0 * (nt - 1) * S * T * T : nullptr;
-      unsigned* cntg = S > 1 ? c->d_cnt + (size_t)p0 * (nt - 1) : nullptr;
+      const int grp = step_group(gc);
+      const int Sc = split_crit(pc, nt, J, grp, S);
+      const int Sl = S > 1 ? S : Sc;  // pieces per split tile in this launch
+      double* partg = Sl > 1 ? c->d_part + (size_t)p0 * (nt - 1) * Smax * T * T : nullptr;
+      unsigned* cntg = Sl > 1 ? c->d_cnt + (size_t)p0 * (nt - 1) : nullptr;
+      const auto kern = S > 1 ? gpf::k_step<gpf::SPLIT_ALL> : Sc > 1 ? gpf::k_step<gpf::SPLIT_CRIT>
+                                                                     : gpf::k_step<gpf::SPLIT_NONE>;
+      const unsigned grid = S > 1 ? gc * (nt - 1) * S : gc * (nt - 1) + gc * (Sc - 1);
       const int rc = launch_on(c, st, PC_PANEL, fl * gc, [&] {
-        hipLaunchKernelGGL(S > 1 ? gpf::k_step<true> : gpf::k_step<false>, dim3(gc * (nt - 1) * S),
+        hipLaunchKernelGGL(kern, dim3(grid),
                            dim3(gpf::STEP_NTH), 0, st, J, nt, Np,
                            c->d_L + (size_t)p0 * ld * ld, c->d_U + (size_t)p0 * ld * ld, c->d_yb + (size_t)p0 * ld,
                            c->d_s2p + (size_t)p0 * nt * ld, c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc,
-                           step_group(gc), N, c->d_x, c->d_ls + (size_t)p0 * c->d, c->d, S, partg, cntg);
+                           grp, N, c->d_x, c->d_ls + (size_t)p0 * c->d, c->d, Sl, partg, cntg);
       });
       if (rc) return rc;
       total += fl * gc;

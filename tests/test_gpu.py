@@ -362,6 +362,37 @@ def test_split_k_matches_unsplit_and_oracle(ctx, monkeypatch, split):
     assert _rel(m2[2], mo) < RTOL_MU_SD and _rel(s2[2], so) < RTOL_MU_SD
 
 
+@pytest.mark.parametrize("split", [3, 8])
+def test_critical_tile_split_matches_unsplit_and_oracle(ctx, monkeypatch, split):
+    """Critical-tile split (gpf::SPLIT_CRIT: only the tile I = J+1 of each particle is cut into
+    depth ranges, its pieces dispatched ahead of the unsplit tiles) against the unsplit path and
+    the oracle. GPF_SPLIT_CRIT forces its factor; GPF_SPLIT_K=1 keeps the all-tile split off."""
+    N, d = 1000, 2
+    rng = np.random.default_rng(12)
+    x = rng.uniform(size=(d, N))
+    y = np.cos(5 * x[0]) * x[1] + 0.1 * rng.standard_normal(N)
+    e = rng.uniform(0.05, 0.2, size=N)
+    s, ex = ref_cpu.sigma_grid()
+    lo, hi = ref_cpu.search_bounds(x)
+    P = rng.uniform(0.1, 0.5, size=(12, d))
+    ctx.set_data(x, y, e)
+    ctx.set_grid(s, ex, lo, hi)
+    monkeypatch.setenv("GPF_SPLIT_K", "1")
+    monkeypatch.setenv("GPF_SPLIT_CRIT", "1")
+    l1, m1, s1 = ctx.eval_batch(P, want_mu_sd=True)
+    monkeypatch.setenv("GPF_SPLIT_CRIT", str(split))
+    monkeypatch.setenv("GPF_SPLIT_CRIT_MIN", "2")  # short pieces too, so the forced factor is used
+    l2, m2, s2 = ctx.eval_batch(P, want_mu_sd=True)
+    l3, m3, s3 = ctx.eval_batch(P, want_mu_sd=True)
+    np.testing.assert_array_equal(m2, m3)  # deterministic: partials summed in slot order
+    np.testing.assert_array_equal(s2, s3)
+    assert _rel(m2, m1) < 1e-10 and _rel(s2, s1) < 1e-10
+    assert _rel(l2, l1) < RTOL_LOSS
+    for i in (0, 7, 11):
+        mo, so = ref_cpu.GP_train_identity(x, y, e, P[i])
+        assert _rel(m2[i], mo) < RTOL_MU_SD and _rel(s2[i], so) < RTOL_MU_SD
+
+
 @pytest.mark.parametrize("N,d,hetero,seed", [(130, 1, False, 1), (383, 5, True, 2), (512, 2, True, 3),
                                              (777, 3, False, 4), (1500, 4, True, 5), (2049, 2, False, 6)])
 def test_random_configs_vs_oracle(ctx, N, d, hetero, seed):
