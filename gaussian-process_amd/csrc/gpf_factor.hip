@@ -794,6 +794,7 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
                 I * T + H >= N);
     }
   } else {
+    if (SPLIT == SPLIT_CRIT && sidx > 0) return;  // only L tiles are split here (host never asks)
     const int K = w - nL;
     double* Ujk = Up + (size_t)J * T * ld + (size_t)K * T;
     Acc<T> acc;

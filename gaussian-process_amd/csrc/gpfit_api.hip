@@ -222,7 +222,8 @@ static int ensure_work(gpf_ctx* c, int want) {
   GPF_HIP(c, hipMalloc(&c->d_loss, (size_t)cap * 8));
   GPF_HIP(c, hipMalloc(&c->d_info, (size_t)cap * 4));
   GPF_HIP(c, hipMalloc(&c->d_hist, (size_t)cap * (c->K + 1) * 4));
-  GPF_HIP(c, hipMemset(c->d_hist, 0, (size_t)cap * (c->K + 1) * 4));  // k_score re-zeroes what it read
+  // on the library stream: the legacy null stream does not order against our non-blocking streams
+  GPF_HIP(c, hipMemsetAsync(c->d_hist, 0, (size_t)cap * (c->K + 1) * 4, c->stream));  // k_score re-zeroes what it read
   GPF_HIP(c, hipHostMalloc((void**)&c->h_ls, (size_t)cap * std::max(c->d, 1) * 8, hipHostMallocDefault));
   GPF_HIP(c, hipHostMalloc((void**)&c->h_loss, (size_t)cap * 8, hipHostMallocDefault));
   GPF_HIP(c, hipHostMalloc((void**)&c->h_info, (size_t)cap * 4, hipHostMallocDefault));
@@ -275,7 +276,8 @@ static int split_k(int tiles, int nt) {
 // P=32 +2.4% at S <= 2, -5..-12% with 8-chunk pieces; N=2048 P=32 +12% at S = 4).
 // GPF_SPLIT_CRIT = maximum S (1 = off), GPF_SPLIT_CRIT_MIN = minimum chunks per piece.
 static int split_crit(int pc, int nt, int J, int grp, int S_all) {
-  if (S_all > 1 || grp > 0 || J == 0 || nt < 4 || !GPF_KFUSE) return 1;
+  // the last launch (J = nt-1) has no L tiles: its w = 0 is a U tile, which never splits
+  if (S_all > 1 || grp > 0 || J == 0 || J >= nt - 1 || nt < 4 || !GPF_KFUSE) return 1;
   const int slots = 512, tiles = pc * (nt - 1);
   int S = 4, minch = 20;
   if (const char* s = getenv("GPF_SPLIT_CRIT")) S = std::max(1, std::min(32, atoi(s)));
@@ -289,6 +291,7 @@ static int split_crit(int pc, int nt, int J, int grp, int S_all) {
 static int ensure_split(gpf_ctx* c, int tiles, int S) {
   const size_t pb = (size_t)tiles * S * T * T * 8, cb = (size_t)tiles * 4;
   if (pb > c->part_cap) {
+    clear_graphs(c);  // captured graphs hold the old pointers
     hipFree(c->d_part);
     c->d_part = nullptr;
     c->part_cap = 0;
@@ -296,14 +299,29 @@ static int ensure_split(gpf_ctx* c, int tiles, int S) {
     c->part_cap = pb;
   }
   if (cb > c->cnt_cap) {
+    clear_graphs(c);
     hipFree(c->d_cnt);
     c->d_cnt = nullptr;
     c->cnt_cap = 0;
     GPF_HIP(c, hipMalloc(&c->d_cnt, cb));
-    GPF_HIP(c, hipMemset(c->d_cnt, 0, cb));  // the finishing workgroups re-zero what they used
+    // on the library stream (the null stream would not order against it); the finishing
+    // workgroups re-zero what they used
+    GPF_HIP(c, hipMemsetAsync(c->d_cnt, 0, cb, c->stream));
     c->cnt_cap = cb;
   }
   return GPF_OK;
+}
+
+// Split-K plan of a factorisation of pc particles: S (all tiles) and the largest factor any
+// launch uses; the partial buffers are sized for it (before a graph capture, so that a captured
+// graph never sees them reallocated).
+static int split_plan(gpf_ctx* c, int pc, int& S, int& Smax) {
+  const int nt = c->nt, ng = num_groups(pc, nt);
+  const int gmax = (pc + ng - 1) / ng;
+  S = split_k(gmax * (nt - 1), nt);
+  Smax = S;
+  for (int J = 1; S == 1 && J < nt; ++J) Smax = std::max(Smax, split_crit(pc, nt, J, step_group(gmax), S));
+  return Smax > 1 ? ensure_split(c, pc * (nt - 1), Smax) : GPF_OK;
 }
 
 // Factorise `pc` particles whose length scales are already in d_ls, in particle
@@ -366,13 +384,8 @@ static int run_factor(gpf_ctx* c, int pc) {
     total += (2.0 / 3.0) * t3 * gc;
   }
   // split-K for launches with few tiles (one set of partial slots per group, groups run concurrently)
-  const int gmax = (pc + ng - 1) / ng;
-  const int S = split_k(gmax * (nt - 1), nt);
-  int Smax = S;
-  for (int J = 1; S == 1 && J < nt; ++J) Smax = std::max(Smax, split_crit(pc, nt, J, step_group(gmax), S));
-  if (Smax > 1) {
-    if (int rc = ensure_split(c, pc * (nt - 1), Smax)) return rc;
-  }
+  int S = 1, Smax = 1;
+  if (int rc = split_plan(c, pc, S, Smax)) return rc;
   // block columns interleaved across groups so every stream has work queued early
   for (int J = 0; nt > 1 && J < nt; ++J) {
     const double fl = step_flops(J);
@@ -607,6 +620,8 @@ int gpf_eval_batch(gpf_ctx* c, const double* ls, int P, double* loss, double* mu
   // Small problems are launch-latency bound: the whole batch (copies + ~5 kernels) is
   // captured once per batch size as a HIP graph and replayed. The batch is padded to all P
   // slots (spare slots repeat an active particle) so one graph serves every PSO iteration.
+  // (Replaying graphs of the live particles up to N = 1920 measured no gain at N = 1024: the
+  // ~10 us between dependent k_step launches is not launch overhead; profiles/r1/split_crit_ab.txt.)
   const bool graph = !c->prof && !mu && !sd && c->nt <= GRAPH_NT_MAX && getenv("GPF_NO_GRAPH") == nullptr;
   if (graph) {
     int rc = ensure_work(c, P);

@@ -393,6 +393,38 @@ def test_critical_tile_split_matches_unsplit_and_oracle(ctx, monkeypatch, split)
         assert _rel(m2[i], mo) < RTOL_MU_SD and _rel(s2[i], so) < RTOL_MU_SD
 
 
+@pytest.mark.parametrize("N,d", [(700, 2), (1920, 3)])
+def test_default_critical_split_live_counts(ctx, monkeypatch, N, d):
+    """The default critical-tile split (on whenever a launch leaves slots idle, up to the last
+    block column, whose w = 0 tile is a U tile and must not be duplicated) across changing
+    live-particle counts (sentinels never run; buffers grow between batches): deterministic,
+    and within 1e-10 of the unsplit path (GPF_SPLIT_CRIT=1)."""
+    rng = np.random.default_rng(N + d)
+    x = rng.uniform(size=(d, N))
+    y = np.sin(3 * x[0]) + 0.1 * rng.standard_normal(N)
+    e = rng.uniform(0.05, 0.2, size=N)
+    s, ex = ref_cpu.sigma_grid()
+    lo, hi = ref_cpu.search_bounds(x)
+    ctx.set_data(x, y, e)
+    ctx.set_grid(s, ex, lo, hi)
+    P = rng.uniform(0.1, 0.5, size=(24, d))
+    masks = [np.arange(24) % 3 == 0, np.zeros(24, bool), np.arange(24) % 5 == 1, np.arange(24) % 3 == 0]
+    got = []
+    for m in masks:
+        Q = P.copy()
+        Q[m, 0] = hi[0] + 1.0  # sentinels: outside the box
+        monkeypatch.delenv("GPF_SPLIT_CRIT", raising=False)
+        g = ctx.eval_batch(Q)
+        np.testing.assert_array_equal(g, ctx.eval_batch(Q))  # deterministic
+        monkeypatch.setenv("GPF_SPLIT_CRIT", "1")
+        w = ctx.eval_batch(Q)
+        monkeypatch.delenv("GPF_SPLIT_CRIT", raising=False)
+        assert np.all(g[m] == 1e13)
+        assert _rel(g, w) < 1e-10
+        got.append(g)
+    np.testing.assert_array_equal(got[0], got[3])
+
+
 @pytest.mark.parametrize("N,d,hetero,seed", [(130, 1, False, 1), (383, 5, True, 2), (512, 2, True, 3),
                                              (777, 3, False, 4), (1500, 4, True, 5), (2049, 2, False, 6)])
 def test_random_configs_vs_oracle(ctx, N, d, hetero, seed):
