@@ -271,15 +271,15 @@ static int split_k(int tiles, int nt) {
 // the depth-128J GEMM, the look-ahead update and the next diagonal factor in sequence): that
 // tile's GEMM is cut into S depth ranges run by S workgroups dispatched ahead of the rest.
 // Needs the particle-fastest tile order (grp = 0). pc: the particles of all concurrent groups
-// (they share the 512 workgroup slots). Pieces of at least 20 16-deep chunks: shorter ones lose
+// (they share the 512 workgroup slots). Pieces of at least 16 16-deep chunks: shorter ones lose
 // more to the partial round trip than they save (A/B, profiles/r1/split_crit_ab.txt: N=1024
-// P=32 +2.4% at S <= 2, -5..-12% with 8-chunk pieces; N=2048 P=32 +12% at S = 4).
+// P=32 +2.4%, -5..-12% with 8-chunk pieces; N=2048 P=32 +9%).
 // GPF_SPLIT_CRIT = maximum S (1 = off), GPF_SPLIT_CRIT_MIN = minimum chunks per piece.
 static int split_crit(int pc, int nt, int J, int grp, int S_all) {
   // the last launch (J = nt-1) has no L tiles: its w = 0 is a U tile, which never splits
   if (S_all > 1 || grp > 0 || J == 0 || J >= nt - 1 || nt < 4 || !GPF_KFUSE) return 1;
   const int slots = 512, tiles = pc * (nt - 1);
-  int S = 4, minch = 20;
+  int S = 4, minch = 16;
   if (const char* s = getenv("GPF_SPLIT_CRIT")) S = std::max(1, std::min(32, atoi(s)));
   if (const char* s = getenv("GPF_SPLIT_CRIT_MIN")) minch = std::max(2, atoi(s));
   const int nch = J * T / gpf::DL_KC;
