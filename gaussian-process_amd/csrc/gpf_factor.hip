@@ -546,7 +546,10 @@ __global__ __launch_bounds__(DNTH) void k_diag(int J, int nt, int N, int Npad, d
 // longest-first over the whole launch; smaller groups keep fewer particles'
 // B panels live in the 4 MB L2 at a time.
 // ----------------------------------------------------------------------------
-__device__ __forceinline__ void step_tile(int b, int P, int ntl, int grp, int& p, int& w) {
+#ifndef GPF_KFUSE
+#define GPF_KFUSE 1  // off-diagonal K tiles computed in k_step instead of read from the K build
+#endif
+__host__ __device__ __forceinline__ void step_tile(int b, int P, int ntl, int grp, int& p, int& w) {
   if ((P & 7) != 0 || grp <= 0) {  // particle fastest
     p = b % P;
     w = b / P;
@@ -555,9 +558,41 @@ __device__ __forceinline__ void step_tile(int b, int P, int ntl, int grp, int& p
   const int xcd = b & 7, s = b >> 3, pq = P >> 3;
   const int per = grp * ntl;
   const int gi = s / per, r = s - gi * per;
-  const int gs = min(grp, pq - gi * grp);  // the last group may be smaller
+  const int gs = grp < pq - gi * grp ? grp : pq - gi * grp;  // the last group may be smaller
   w = r / gs;
   p = (gi * grp + (r - w * gs)) * 8 + xcd;
+}
+
+enum { SPLIT_NONE = 0, SPLIT_ALL = 1, SPLIT_CRIT = 2 };
+enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2 };
+
+// Workgroup b of a k_step<SPLIT> launch (grid: P*(nt-1)*S for SPLIT_ALL, P*(nt-1) + P*(S-1)
+// for SPLIT_CRIT, P*(nt-1) otherwise): its particle p, tile w, split index sidx, and whether
+// it runs the whole tile, one depth range (piece sidx of S) of it, or nothing. The kernel and
+// the host-side plan check (gpf_plan_check) both decode through this function.
+template <int SPLIT>
+__host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt, int grp, int S, int& p, int& w,
+                                                    int& sidx) {
+  const int tiles = P * (nt - 1);
+  sidx = 0;
+  if (SPLIT == SPLIT_ALL) {
+    sidx = b / tiles;  // split-major dispatch
+    step_tile(b - sidx * tiles, P, nt - 1, grp, p, w);
+  } else if (SPLIT == SPLIT_CRIT && b < P * S) {  // the S pieces of the critical tiles
+    p = b % P;
+    w = 0;
+    sidx = b / P;
+  } else {  // particle-fastest order (grp = 0) puts the critical tiles w = 0 at b < P
+    step_tile(b - (SPLIT == SPLIT_CRIT ? P * (S - 1) : 0), P, nt - 1, grp, p, w);
+  }
+  const bool ltile = w < nt - 1 - J;
+  if (ltile) {
+    // L tiles split their depth-128J GEMM (only with the K tiles fused into k_step)
+    if (GPF_KFUSE && (SPLIT == SPLIT_ALL || (SPLIT == SPLIT_CRIT && w == 0)) && J > 0) return ROLE_PIECE;
+    return (SPLIT != SPLIT_NONE && sidx > 0) ? ROLE_IDLE : ROLE_WHOLE;  // nothing to split at J = 0
+  }
+  if (SPLIT == SPLIT_ALL) return ROLE_PIECE;
+  return (SPLIT == SPLIT_CRIT && sidx > 0) ? ROLE_IDLE : ROLE_WHOLE;  // U tiles never split in CRIT
 }
 
 constexpr int STEP_STAGE = (Geo<T>::STAGE > DL_STAGE) ? Geo<T>::STAGE : DL_STAGE;
@@ -603,9 +638,6 @@ __device__ __forceinline__ void step_gemm(Acc<T>& acc, const double* Ap, int lda
 #endif
 }
 
-#ifndef GPF_KFUSE
-#define GPF_KFUSE 1  // off-diagonal K tiles computed in k_step instead of read from the K build
-#endif
 // A_IJ (I > J: no diagonal entries, so no noise term) of one particle straight into the
 // accumulator layout, with k_build_cov's op order (bitwise the same values, kernel_func
 // GP_func.py:56-65): the scaled coordinates and squared norms of the tile's 128 rows and 128
@@ -706,11 +738,9 @@ __device__ __forceinline__ void split_sum(Acc<T>& acc, const double* pt, int nch
   }
 }
 
-enum { SPLIT_NONE = 0, SPLIT_ALL = 1, SPLIT_CRIT = 2 };
-
-// Tile w of block column J of particle p (the unit of work of k_step).
+// Tile w of block column J of particle p (the unit of work of k_step); role from step_decode.
 template <int SPLIT>
-__device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad, double* __restrict__ Lb,
+__device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt, int Npad, double* __restrict__ Lb,
                                           double* __restrict__ Ub, double* __restrict__ yb,
                                           double* __restrict__ s2p, double* __restrict__ szp,
                                           int* __restrict__ info, int N, const double* __restrict__ x,
@@ -720,6 +750,7 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
   const int tid = threadIdx.x;
   const int nL = nt - 1 - J;
   const size_t ld = (size_t)Npad;
+  if (SPLIT != SPLIT_NONE && role == ROLE_IDLE) return;
   double* Lp = Lb + (size_t)p * ld * ld;
   double* Up = Ub + (size_t)p * ld * ld;
   double* yp = yb + (size_t)p * Npad;
@@ -735,7 +766,7 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
     Acc<T> acc;
     // C = A_IJ - L_I,<J L_J,<J^T (accumulator seeded with A_IJ, A operand staged negated)
 #if GPF_KFUSE
-    if ((SPLIT == SPLIT_ALL || (SPLIT == SPLIT_CRIT && w == 0)) && J > 0) {
+    if (SPLIT != SPLIT_NONE && role == ROLE_PIECE) {
       // split-K: partial GEMMs, the last workgroup to arrive finishes the tile
       double* pt = part + (size_t)(p * (nt - 1) + w) * S * T * T;
       if (!split_part<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, J * T / DL_KC, S,
@@ -744,7 +775,6 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
       cov_tile_acc(acc, qd, x, ls + (size_t)p * d, d, N, I, J, smem);
       split_sum(acc, pt, J * T / DL_KC, S, qd);
     } else {
-      if (SPLIT && sidx > 0) return;  // nothing to split at J = 0
       cov_tile_acc(acc, qd, x, ls + (size_t)p * d, d, N, I, J, smem);
       if (J > 0)
         step_gemm<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, J * T, smem, qd);
@@ -794,12 +824,11 @@ __device__ __forceinline__ void step_item(int J, int w, int p, int nt, int Npad,
                 I * T + H >= N);
     }
   } else {
-    if (SPLIT == SPLIT_CRIT && sidx > 0) return;  // only L tiles are split here (host never asks)
     const int K = w - nL;
     double* Ujk = Up + (size_t)J * T * ld + (size_t)K * T;
     Acc<T> acc;
     // W = L_J,[K,J) U_[K,J),K, parked in the U_JK slot
-    if (SPLIT == SPLIT_ALL) {  // split-K (the triangular first block runs dense: its upper part holds zeros)
+    if (SPLIT == SPLIT_ALL && role == ROLE_PIECE) {  // split-K (the triangular first block runs dense: its upper part holds zeros)
       double* pt = part + (size_t)(p * (nt - 1) + w) * S * T * T;
       if (!split_part<true, false>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
                                    Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T / DL_KC, S, sidx, pt,
@@ -884,19 +913,9 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
   __shared__ __attribute__((aligned(16))) double smem[STEP_SMEM];
   __shared__ __attribute__((aligned(16))) double small[STEP_SMALL];
   __shared__ int sflag;
-  const int tiles = P * (nt - 1);
-  int p, w, sidx = 0;
-  if (SPLIT == SPLIT_ALL) {
-    sidx = (int)(blockIdx.x / tiles);  // split index, split-major dispatch
-    step_tile(blockIdx.x - sidx * tiles, P, nt - 1, grp, p, w);
-  } else if (SPLIT == SPLIT_CRIT && (int)blockIdx.x < P * S) {  // the S pieces of the critical tiles
-    p = (int)blockIdx.x % P;
-    w = 0;
-    sidx = (int)blockIdx.x / P;
-  } else {  // particle-fastest order (grp = 0) puts the critical tiles w = 0 at b < P
-    step_tile((int)blockIdx.x - (SPLIT == SPLIT_CRIT ? P * (S - 1) : 0), P, nt - 1, grp, p, w);
-  }
-  step_item<SPLIT>(J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, sidx, part, cnt, &sflag, smem,
+  int p, w, sidx;
+  const int role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, p, w, sidx);
+  step_item<SPLIT>(role, J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, sidx, part, cnt, &sflag, smem,
                    small);
 #ifdef GPF_WG_TRACE
   __syncthreads();

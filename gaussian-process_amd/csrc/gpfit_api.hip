@@ -9,6 +9,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdarg>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -34,6 +36,8 @@ enum ProfClass { PC_PANEL = 0, PC_DIAG = 1, PC_BUILD = 2, PC_LOSS = 3, PC_FACTOR
 
 constexpr int MAX_GROUPS = 4;  // particle groups factorised on concurrent streams
 constexpr int GRAPH_NT_MAX = 2;  // eval batches with N <= 256 run as a replayed HIP graph
+// a captured batch must never reach split_plan's hipMalloc/hipFree (splits start at nt = 4)
+static_assert(GRAPH_NT_MAX < 4, "graph-captured batches must not use split-K buffers");
 
 struct Pending {
   hipEvent_t a, b;
@@ -313,15 +317,55 @@ static int ensure_split(gpf_ctx* c, int tiles, int S) {
 }
 
 // Split-K plan of a factorisation of pc particles: S (all tiles) and the largest factor any
-// launch uses; the partial buffers are sized for it (before a graph capture, so that a captured
-// graph never sees them reallocated).
-static int split_plan(gpf_ctx* c, int pc, int& S, int& Smax) {
-  const int nt = c->nt, ng = num_groups(pc, nt);
+// launch uses; the partial buffers are sized for it. run_factor calls this before it forks
+// the group streams. The graph path (N <= 128 * GRAPH_NT_MAX) captures run_factor, but
+// split_k and split_crit never split below nt = 4, so nothing is allocated during a capture
+// (static_assert below).
+static void split_sizes(int pc, int nt, int& S, int& Smax) {
+  const int ng = num_groups(pc, nt);
   const int gmax = (pc + ng - 1) / ng;
   S = split_k(gmax * (nt - 1), nt);
   Smax = S;
   for (int J = 1; S == 1 && J < nt; ++J) Smax = std::max(Smax, split_crit(pc, nt, J, step_group(gmax), S));
-  return Smax > 1 ? ensure_split(c, pc * (nt - 1), Smax) : GPF_OK;
+}
+
+static int split_plan(gpf_ctx* c, int pc, int& S, int& Smax) {
+  split_sizes(pc, c->nt, S, Smax);
+  return Smax > 1 ? ensure_split(c, pc * (c->nt - 1), Smax) : GPF_OK;
+}
+
+// One k_step launch of a factorisation: block column J of particle group g (particles
+// [p0, p0+gc) of the chunk, on that group's stream), its kernel variant, grid, pieces per split
+// tile, and where its split-K partial slots and arrival counters start (element offsets into
+// d_part / d_cnt). run_factor launches exactly this list; gpf_plan_check verifies it on the host.
+struct StepLaunch {
+  int J, g, p0, gc, split, S, grp;
+  unsigned grid;
+  size_t part_off, cnt_off;
+};
+
+static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& out) {
+  out.clear();
+  const int ng = num_groups(pc, nt);
+  // block columns interleaved across groups so every stream has work queued early
+  for (int J = 0; nt > 1 && J < nt; ++J) {
+    for (int g = 0; g < ng; ++g) {
+      StepLaunch l{};
+      l.J = J;
+      l.g = g;
+      l.p0 = (int)((long long)pc * g / ng);
+      l.gc = (int)((long long)pc * (g + 1) / ng) - l.p0;
+      l.grp = step_group(l.gc);
+      const int Sc = split_crit(pc, nt, J, l.grp, S);
+      l.S = S > 1 ? S : Sc;  // pieces per split tile in this launch
+      l.split = S > 1 ? gpf::SPLIT_ALL : Sc > 1 ? gpf::SPLIT_CRIT : gpf::SPLIT_NONE;
+      l.grid = S > 1 ? l.gc * (nt - 1) * S : l.gc * (nt - 1) + l.gc * (Sc - 1);
+      // one set of partial slots per group: groups run concurrently
+      l.part_off = (size_t)l.p0 * (nt - 1) * Smax * T * T;
+      l.cnt_off = (size_t)l.p0 * (nt - 1);
+      out.push_back(l);
+    }
+  }
 }
 
 // Factorise `pc` particles whose length scales are already in d_ls, in particle
@@ -348,6 +392,12 @@ static int run_factor(gpf_ctx* c, int pc) {
     if (J + 1 < nt) fl += (2.0 / 3.0) * t3;
     return fl;
   };
+  // Split-K plan first: a (re)allocation of the arrival counters queues their zeroing memset on
+  // c->stream, which must precede the fork event the group streams wait on (with ng > 1 the
+  // k_step launches run on the sub-streams, and an unordered memset could land after a piece
+  // took its ticket, leaving a tile unfinished).
+  int S = 1, Smax = 1;
+  if (int rc = split_plan(c, pc, S, Smax)) return rc;
   hipEvent_t wa = nullptr, wb = nullptr;
   if (c->prof) {
     wa = take_event(c);
@@ -383,33 +433,26 @@ static int run_factor(gpf_ctx* c, int pc) {
     if (rc) return rc;
     total += (2.0 / 3.0) * t3 * gc;
   }
-  // split-K for launches with few tiles (one set of partial slots per group, groups run concurrently)
-  int S = 1, Smax = 1;
-  if (int rc = split_plan(c, pc, S, Smax)) return rc;
-  // block columns interleaved across groups so every stream has work queued early
-  for (int J = 0; nt > 1 && J < nt; ++J) {
-    const double fl = step_flops(J);
-    for (int g = 0; g < ng; ++g) {
-      const int p0 = (int)((long long)pc * g / ng), gc = (int)((long long)pc * (g + 1) / ng) - p0;
-      hipStream_t st = (ng > 1) ? c->sub[g] : c->stream;
-      const int grp = step_group(gc);
-      const int Sc = split_crit(pc, nt, J, grp, S);
-      const int Sl = S > 1 ? S : Sc;  // pieces per split tile in this launch
-      double* partg = Sl > 1 ? c->d_part + (size_t)p0 * (nt - 1) * Smax * T * T : nullptr;
-      unsigned* cntg = Sl > 1 ? c->d_cnt + (size_t)p0 * (nt - 1) : nullptr;
-      const auto kern = S > 1 ? gpf::k_step<gpf::SPLIT_ALL> : Sc > 1 ? gpf::k_step<gpf::SPLIT_CRIT>
-                                                                     : gpf::k_step<gpf::SPLIT_NONE>;
-      const unsigned grid = S > 1 ? gc * (nt - 1) * S : gc * (nt - 1) + gc * (Sc - 1);
-      const int rc = launch_on(c, st, PC_PANEL, fl * gc, [&] {
-        hipLaunchKernelGGL(kern, dim3(grid),
-                           dim3(gpf::STEP_NTH), 0, st, J, nt, Np,
-                           c->d_L + (size_t)p0 * ld * ld, c->d_U + (size_t)p0 * ld * ld, c->d_yb + (size_t)p0 * ld,
-                           c->d_s2p + (size_t)p0 * nt * ld, c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc,
-                           grp, N, c->d_x, c->d_ls + (size_t)p0 * c->d, c->d, Sl, partg, cntg);
-      });
-      if (rc) return rc;
-      total += fl * gc;
-    }
+  // block-column launches (split-K for launches with few tiles, planned above)
+  std::vector<StepLaunch> plan;
+  step_plan(pc, nt, S, Smax, plan);
+  for (const StepLaunch& l : plan) {
+    const double fl = step_flops(l.J);
+    const int p0 = l.p0, gc = l.gc;
+    hipStream_t st = (ng > 1) ? c->sub[l.g] : c->stream;
+    double* partg = l.S > 1 ? c->d_part + l.part_off : nullptr;
+    unsigned* cntg = l.S > 1 ? c->d_cnt + l.cnt_off : nullptr;
+    const auto kern = l.split == gpf::SPLIT_ALL    ? gpf::k_step<gpf::SPLIT_ALL>
+                      : l.split == gpf::SPLIT_CRIT ? gpf::k_step<gpf::SPLIT_CRIT>
+                                                   : gpf::k_step<gpf::SPLIT_NONE>;
+    const int rc = launch_on(c, st, PC_PANEL, fl * gc, [&] {
+      hipLaunchKernelGGL(kern, dim3(l.grid), dim3(gpf::STEP_NTH), 0, st, l.J, nt, Np, c->d_L + (size_t)p0 * ld * ld,
+                         c->d_U + (size_t)p0 * ld * ld, c->d_yb + (size_t)p0 * ld, c->d_s2p + (size_t)p0 * nt * ld,
+                         c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc, l.grp, N, c->d_x,
+                         c->d_ls + (size_t)p0 * c->d, c->d, l.S, partg, cntg);
+    });
+    if (rc) return rc;
+    total += fl * gc;
   }
   if (ng > 1) {
     for (int g = 0; g < ng; ++g) {
@@ -478,7 +521,11 @@ static int hull_sort_unique(gpf_ctx* c, DevBuf& rows, int64_t& n, int d, const i
 
 extern "C" {
 
+#ifndef GPF_BUILD_INFO
+#define GPF_BUILD_INFO "unknown"
+#endif
 int gpf_version(void) { return GPF_ABI_VERSION; }
+const char* gpf_build_info(void) { return GPF_BUILD_INFO; }
 int gpf_tile(void) { return T; }
 
 int gpf_open(int device, gpf_ctx** out) {
@@ -844,6 +891,95 @@ int gpf_log_marginal_likelihood(gpf_ctx* c, const double* ls, double* out) {
   for (int64_t i = 0; i < N; ++i) ya += c->h_y[i] * a[i];
   for (int64_t i = 0; i < N; ++i) ld += std::log(dg[i]);
   *out = -0.5 * ya - ld - 0.5 * (double)N * std::log(2.0 * M_PI);
+  return GPF_OK;
+}
+
+static int plan_fail(char* msg, int len, const char* fmt, ...) {
+  if (msg && len > 0) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(msg, (size_t)len, fmt, ap);
+    va_end(ap);
+  }
+  return GPF_BAD_ARG;
+}
+
+// Host-only structural check of the k_step dispatch plan (no device, no context): see gpfit.h.
+int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
+  if (msg && msg_len > 0) msg[0] = 0;
+  if (pc <= 0 || nt <= 0) return plan_fail(msg, msg_len, "bad arguments pc=%d nt=%d", pc, nt);
+  int S = 1, Smax = 1;
+  split_sizes(pc, nt, S, Smax);
+  std::vector<StepLaunch> plan;
+  step_plan(pc, nt, S, Smax, plan);
+  const int ntl = nt - 1, ng = num_groups(pc, nt);
+  const size_t part_cap = Smax > 1 ? (size_t)pc * ntl * Smax * T * T : 0;
+  const size_t cnt_cap = Smax > 1 ? (size_t)pc * ntl : 0;
+  // partial-slot and counter ranges each group touches: groups run concurrently, so they must
+  // be disjoint (within a group the launches are ordered on its stream)
+  std::vector<size_t> plo(MAX_GROUPS, SIZE_MAX), phi(MAX_GROUPS, 0), clo(MAX_GROUPS, SIZE_MAX), chi(MAX_GROUPS, 0);
+  long long wgs = 0, whole_tiles = 0, split_tiles = 0;
+  std::vector<int> whole, piece;
+  if ((int)plan.size() != (nt > 1 ? nt * ng : 0)) return plan_fail(msg, msg_len, "plan has %d launches, want %d",
+                                                              (int)plan.size(), nt * ng);
+  for (const StepLaunch& l : plan) {
+    if (l.gc <= 0 || l.p0 < 0 || l.p0 + l.gc > pc || l.g < 0 || l.g >= ng)
+      return plan_fail(msg, msg_len, "J=%d: bad group range p0=%d gc=%d g=%d", l.J, l.p0, l.gc, l.g);
+    if (l.S < 1 || l.S > Smax || (l.split != gpf::SPLIT_NONE) != (l.S > 1))
+      return plan_fail(msg, msg_len, "J=%d g=%d: split kind %d with S=%d", l.J, l.g, l.split, l.S);
+    const int tiles = l.gc * ntl;
+    whole.assign((size_t)tiles, 0);
+    piece.assign((size_t)tiles * l.S, 0);
+    for (unsigned b = 0; b < l.grid; ++b) {
+      int p = -1, w = -1, sidx = -1;
+      const int role = l.split == gpf::SPLIT_ALL    ? gpf::step_decode<gpf::SPLIT_ALL>(b, l.J, l.gc, nt, l.grp, l.S, p, w, sidx)
+                       : l.split == gpf::SPLIT_CRIT ? gpf::step_decode<gpf::SPLIT_CRIT>(b, l.J, l.gc, nt, l.grp, l.S, p, w, sidx)
+                                                    : gpf::step_decode<gpf::SPLIT_NONE>(b, l.J, l.gc, nt, l.grp, l.S, p, w, sidx);
+      if (p < 0 || p >= l.gc || w < 0 || w >= ntl || sidx < 0 || sidx >= l.S)
+        return plan_fail(msg, msg_len, "J=%d block %u decodes out of range (p=%d w=%d)", l.J, b, p, w);
+      const int t = p * ntl + w;
+      if (role == gpf::ROLE_WHOLE) {
+        ++whole[t];
+      } else if (role == gpf::ROLE_PIECE) {
+        if (l.S < 2) return plan_fail(msg, msg_len, "J=%d block %u is a piece of an unsplit launch (S=%d)", l.J, b, l.S);
+        ++piece[(size_t)t * l.S + sidx];
+        const size_t off = l.part_off + ((size_t)t * l.S + sidx) * T * T, ci = l.cnt_off + t;
+        if (off + (size_t)T * T > part_cap || ci >= cnt_cap)
+          return plan_fail(msg, msg_len, "J=%d tile %d piece %d outside the split buffers (S=%d)", l.J, t, sidx, l.S);
+        plo[l.g] = std::min(plo[l.g], off);
+        phi[l.g] = std::max(phi[l.g], off + (size_t)T * T);
+        clo[l.g] = std::min(clo[l.g], ci);
+        chi[l.g] = std::max(chi[l.g], ci + 1);
+      }
+      ++wgs;
+    }
+    for (int t = 0; t < tiles; ++t) {
+      int np = 0;
+      for (int s = 0; s < l.S; ++s) {
+        if (piece[(size_t)t * l.S + s] > 1) return plan_fail(msg, msg_len, "J=%d tile %d: piece %d run %d times", l.J, t, s, piece[(size_t)t * l.S + s]);
+        np += piece[(size_t)t * l.S + s];
+      }
+      if (whole[t] == 1 && np == 0) ++whole_tiles;
+      else if (whole[t] == 0 && np == l.S) ++split_tiles;  // S arrivals on a zeroed counter: one finisher
+      else return plan_fail(msg, msg_len, "J=%d tile %d: %d whole runs and %d pieces", l.J, t, whole[t], np);
+    }
+  }
+  for (int a = 0; a < ng; ++a)
+    for (int b2 = a + 1; b2 < ng; ++b2) {
+      if (plo[a] < phi[a] && plo[b2] < phi[b2] && plo[a] < phi[b2] && plo[b2] < phi[a])
+        return plan_fail(msg, msg_len, "groups %d and %d share split-K partial slots", a, b2);
+      if (clo[a] < chi[a] && clo[b2] < chi[b2] && clo[a] < chi[b2] && clo[b2] < chi[a])
+        return plan_fail(msg, msg_len, "groups %d and %d share split-K counters", a, b2);
+    }
+  if (stats) {
+    stats[0] = (long long)plan.size();
+    stats[1] = wgs;
+    stats[2] = whole_tiles;
+    stats[3] = split_tiles;
+    stats[4] = S;
+    stats[5] = Smax;
+    stats[6] = ng;
+  }
   return GPF_OK;
 }
 

@@ -48,6 +48,9 @@ SIGNATURES = {
     "gpf_hull_fetch": (ctypes.c_int, [_vp, _dp]),
     "gpf_gemm_bench": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_int, _dp]),
+    "gpf_build_info": (ctypes.c_char_p, []),
+    "gpf_plan_check": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_longlong),
+                                      ctypes.c_char_p, ctypes.c_int]),
 }
 
 _LIB = None
@@ -73,6 +76,24 @@ def load_library():
         raise OSError(f"libgpfit ABI {lib.gpf_version()} != expected {ABI_VERSION}")
     _LIB = lib
     return lib
+
+
+def build_info():
+    """Provenance string baked into the loaded library (gpf_build_info)."""
+    return load_library().gpf_build_info().decode()
+
+
+def plan_check(particles, nt):
+    """Host-side check of the k_step dispatch plan (gpf_plan_check); raises AssertionError
+    naming the first violation, else returns the stats dict. Reads the GPF_* environment."""
+    lib = load_library()
+    stats = (ctypes.c_longlong * 7)()
+    msg = ctypes.create_string_buffer(256)
+    rc = lib.gpf_plan_check(int(particles), int(nt), stats, msg, 256)
+    if rc != GPF_OK:
+        raise AssertionError(f"plan_check(pc={particles}, nt={nt}): {msg.value.decode()}")
+    keys = ("launches", "workgroups", "whole_tiles", "split_tiles", "S", "Smax", "groups")
+    return dict(zip(keys, list(stats)))
 
 
 def _f64(a):

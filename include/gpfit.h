@@ -131,6 +131,24 @@ int gpf_reset_profile(gpf_ctx* ctx);
 /* Tile edge used by the factorisation (padding granule). */
 int gpf_tile(void);
 
+/* Build provenance baked in at compile time by __graft_entry__.build(): "src=<sha256 of the
+ * csrc .hip and include .h sources> hipcc=<compiler version line>" ("unknown" if compiled by
+ * hand). Tests compare it with the hash of the sources in the tree. */
+const char* gpf_build_info(void);
+
+/* Host-only structural check of the k_step dispatch plan (needs no device and no context):
+ * for a chunk of pc particles with nt block columns, under the current GPF_GROUPS /
+ * GPF_SPLIT_K / GPF_SPLIT_CRIT / GPF_SPLIT_CRIT_MIN / GPF_STEP_GROUP environment, builds the
+ * launch list run_factor issues and decodes every workgroup of every launch with the kernel's
+ * own decoder (gpf::step_decode). Checks that every (block column, particle, tile) is computed
+ * exactly once (one whole-tile workgroup, or all S depth pieces exactly once, whose S arrivals
+ * on a zeroed counter elect exactly one finisher), that pieces stay inside the split-K buffers,
+ * and that concurrent particle groups never share partial slots or counters.
+ * stats (nullable, 7 entries): launches, workgroups, whole tiles, split tiles, S (all-tile
+ * split factor), largest split factor, particle groups. Returns GPF_OK, or GPF_BAD_ARG with a
+ * description of the first violation in msg. */
+int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len);
+
 /* Self-test of the f64 MFMA fragment layout: C = A(16x4) B(4x16) on device,
  * compared on the host by the caller. a: 16x4 row-major, b: 4x16 row-major,
  * c: 16x16 row-major. */

@@ -30,6 +30,15 @@ def test_abi_version_and_tile():
     assert lib.gpf_tile() == 128
 
 
+def test_library_was_built_from_these_sources():
+    """gpf_build_info carries the source hash __graft_entry__.build() compiled it from: the
+    library every test loads is the one built from this tree."""
+    import __graft_entry__ as ge
+    import gpfit
+    info = gpfit.build_info()
+    assert info.startswith(f"src={ge.source_hash()};hipcc="), (info, ge.source_hash())
+
+
 def test_library_is_gfx950_code_object():
     import subprocess
     so = ROOT / "gaussian-process_amd" / "libgpfit.so"

@@ -1,0 +1,80 @@
+"""Host-side enumeration of the k_step dispatch plan (no GPU needed).
+
+gpf_plan_check (include/gpfit.h) builds the launch list run_factor issues (num_groups,
+split_k, split_crit, step_group and the grid sizing in csrc/gpfit_api.hip) and decodes every
+workgroup of every launch with the kernel's own decoder (gpf::step_decode). Every
+(block column, particle, tile) must be computed exactly once: one whole-tile workgroup, or
+all S depth pieces exactly once (S arrivals on a zeroed counter elect exactly one finisher);
+pieces must stay inside the split-K buffers and concurrent particle groups must not share
+partial slots or counters. This is the structural guard for races like the v14 duplicate of
+the last block column's w = 0 tile.
+"""
+import os
+
+import pytest
+
+import gpfit
+
+NT = list(range(1, 21)) + [31, 32, 33, 64, 127, 128, 129, 130]
+
+ENVS = [
+    {},                                            # the defaults
+    {"GPF_GROUPS": "2"}, {"GPF_GROUPS": "3"}, {"GPF_GROUPS": "4"},
+    {"GPF_SPLIT_K": "2"}, {"GPF_SPLIT_K": "7"}, {"GPF_SPLIT_K": "16"},
+    {"GPF_SPLIT_K": "7", "GPF_GROUPS": "3"},
+    {"GPF_SPLIT_CRIT": "3"}, {"GPF_SPLIT_CRIT": "8", "GPF_SPLIT_CRIT_MIN": "2"},
+    {"GPF_SPLIT_CRIT": "8", "GPF_SPLIT_CRIT_MIN": "2", "GPF_GROUPS": "2"},
+    {"GPF_STEP_GROUP": "1"}, {"GPF_STEP_GROUP": "2", "GPF_GROUPS": "2"},
+]
+
+
+@pytest.fixture
+def env(monkeypatch):
+    def apply(kv):
+        for k in ("GPF_GROUPS", "GPF_SPLIT_K", "GPF_SPLIT_CRIT", "GPF_SPLIT_CRIT_MIN", "GPF_STEP_GROUP"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in kv.items():
+            monkeypatch.setenv(k, v)
+    return apply
+
+
+@pytest.mark.parametrize("kv", ENVS, ids=lambda kv: ",".join(f"{k}={v}" for k, v in kv.items()) or "default")
+def test_every_tile_has_exactly_one_finisher(env, kv):
+    env(kv)
+    seen_split = seen_groups = 0
+    for nt in NT:
+        # all chunk sizes up to 64 at small nt; a spread at large nt (the check is O(pc nt^2))
+        pcs = range(1, 65) if nt <= 33 else (1, 2, 7, 8, 15, 16, 17, 31, 32, 33, 63, 64)
+        for pc in pcs:
+            st = gpfit.plan_check(pc, nt)
+            assert st["launches"] == (nt * st["groups"] if nt > 1 else 0)
+            assert st["whole_tiles"] + st["split_tiles"] == pc * (nt - 1) * nt  # every (J, p, w)
+            seen_split += st["split_tiles"] > 0
+            seen_groups += st["groups"] > 1
+    if kv.get("GPF_SPLIT_K") or kv.get("GPF_SPLIT_CRIT") or not kv:
+        assert seen_split, "the sweep never reached a split launch"
+    if "GPF_GROUPS" in kv or not kv:
+        assert seen_groups, "the sweep never reached a multi-group plan"
+
+
+def test_default_plans_of_the_baseline_configs(env):
+    """The schedules the bench and the GPU tests rely on."""
+    env({})
+    c = gpfit.plan_check(64, 32)            # config C: one stream, no split
+    assert (c["groups"], c["Smax"]) == (1, 1)
+    d = gpfit.plan_check(32, 32)            # config D's per-GPU share: two concurrent groups
+    assert d["groups"] == 2
+    e = gpfit.plan_check(16, 128)           # config E's per-GPU share at N=16384
+    assert e["groups"] == 2
+    b = gpfit.plan_check(32, 8)             # config B: critical-tile split
+    assert b["groups"] == 1 and b["S"] == 1 and b["Smax"] > 1 and b["split_tiles"] > 0
+    one = gpfit.plan_check(1, 32)           # prediction: single particle, all tiles split
+    assert one["S"] == 16 and one["whole_tiles"] == 31  # J = 0 has nothing to split
+
+
+def test_env_is_read_per_call(env):
+    env({"GPF_GROUPS": "4"})
+    assert gpfit.plan_check(32, 32)["groups"] == 4
+    env({"GPF_GROUPS": "1"})
+    assert gpfit.plan_check(32, 32)["groups"] == 1
+    assert os.environ.get("GPF_GROUPS") == "1"
