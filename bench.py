@@ -10,8 +10,15 @@ region, max over ranks; at N GPUs the swarm is 64 particles per GPU (weak
 scaling). The real PSO update loop, whose box-clipped particles are free
 sentinels, is timed separately and reported under "pso_loop".
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 4096] [--d 3] [--swarm-per-gpu 64]
-                    [--cpu-sample 8] [--cpu-workers 8] [--no-cpu]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 4096] [--d 3] [--swarm-per-gpu P]
+                    [--no-cpu] [--plumbing]
+
+N > 1: one process per GPU. Under a launcher (torchrun: RANK / WORLD_SIZE / LOCAL_RANK set)
+this process is one rank; without one, `--gpus N` starts the N rank processes itself before
+anything touches a GPU and exits with their status. The swarm exchange (one all-reduce per
+batch) and the barrier / max-over-ranks timing go through libgpfit's own RCCL communicator
+(gpf_comm_*). Default swarm: 64 particles on one GPU (config C); 32 per GPU at N > 1, which
+is config D's 256-particle swarm at 8 GPUs (weak scaling, 32 per GPU).
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with a
 "roofline" object for the dominant kernel (k_panel, the MFMA GEMM step) timed
@@ -23,10 +30,13 @@ from __future__ import annotations
 
 import os
 
-# BLAS pins must precede numpy (SURVEY.md §6 gotcha) — the CPU baseline runs
-# one single-threaded evaluation per worker, exactly as the reference's pool.
-os.environ.setdefault("OMP_NUM_THREADS", "1")
-os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
+# BLAS pins must precede numpy (SURVEY.md §6 gotcha) — the CPU baseline runs one
+# single-threaded evaluation per worker, exactly as the reference's pool (its modules assign
+# these at import, GP_func.py:3-7, find_len_scales.py:3-7). Assigned, not defaulted: the GPU
+# box presets OMP_NUM_THREADS=16.
+for _k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS", "VECLIB_MAXIMUM_THREADS",
+           "NUMEXPR_NUM_THREADS"):
+    os.environ[_k] = "1"
 
 import argparse  # noqa: E402
 import json  # noqa: E402
@@ -82,8 +92,31 @@ def _cpu_eval(args):
     return ref_cpu.evaluate_loss(*args)
 
 
+def effective_cpus():
+    """CPUs this process may actually use: affinity mask and cgroup quota (the GPU box shows
+    the whole machine in os.cpu_count() but grants a 16-CPU share)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def blas_threads():
+    """Effective BLAS threading of this process (threadpoolctl), for the baseline record."""
+    try:
+        from threadpoolctl import threadpool_info
+        return sorted({(i.get("internal_api"), i.get("num_threads")) for i in threadpool_info()})
+    except Exception:  # noqa: BLE001 - diagnostic only
+        return None
+
+
 def cpu_baseline(x, y, e, positions, lo, hi, workers):
-    """Reference-policy CPU path: fork pool, one BLAS thread per worker."""
+    """Reference-policy CPU path: a fork pool of single-BLAS-thread workers mapping
+    evaluate_loss over the particles (find_len_scales.py:73-77)."""
     import multiprocessing as mp
     from oracle import ref_cpu
     s, ex = ref_cpu.sigma_grid()
@@ -94,6 +127,35 @@ def cpu_baseline(x, y, e, positions, lo, hi, workers):
         out = pool.map(_cpu_eval, args, chunksize=1)
         dt = time.perf_counter() - t0
     return len(args) / dt, np.array(out), dt
+
+
+def cpu_baselines(x, y, e, lo, hi, N, d, seed):
+    """Primary: the reference's own pool policy, Pool(max(1, os.cpu_count() // 4))
+    (find_len_scales.py:73-75), every worker scoring one particle of the same workload.
+    Secondary: one worker per CPU this process may use (cgroup quota / affinity)."""
+    d_ = x.shape[0]
+    rng = np.random.default_rng(seed + 7)
+    eff = effective_cpus()
+    policy = max(1, (os.cpu_count() or 1) // 4)
+    out = {}
+    for key, workers in (("primary", policy), ("all_cores", eff)):
+        n = workers  # each worker scores (at least) one particle
+        sample = lo + (hi - lo) * rng.uniform(0.2, 0.8, size=(n, d_))
+        v, _, dt = cpu_baseline(x, y, e, sample, lo, hi, workers)
+        out[key] = {"value": v, "unit": "evals/s", "workers": workers, "cores": min(workers, eff), "s": dt,
+                    "evals": n}
+    p = out["primary"]
+    return {"value": p["value"], "unit": "evals/s", "cores": p["cores"], "kind": "port",
+            "sample": f"{p['evals']} evaluate_loss calls (oracle/ref_cpu.py: the reference's NumPy/LAPACK calls, "
+                      f"find_len_scales.py:154-182) at N={N} d={d} on the bench's synthetic data, in the reference's "
+                      f"pool policy Pool(os.cpu_count()//4) = {p['workers']} fork workers on os.cpu_count() = "
+                      f"{os.cpu_count()}, which this box's cgroup limits to {eff} CPUs; one BLAS thread per worker; "
+                      f"{p['s']:.1f} s wall",
+            "policy": "Pool(max(1, os.cpu_count() // 4)) (find_len_scales.py:73-75)",
+            "workers": p["workers"], "host_cpu_count": os.cpu_count(), "effective_cpus": eff,
+            "blas_env": {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS")},
+            "blas_threads": blas_threads(),
+            "all_cores": out["all_cores"]}
 
 
 def predict_line(ctx, x, y, e, N, d, args):
@@ -107,11 +169,10 @@ def predict_line(ctx, x, y, e, N, d, args):
     ctx.predict(ls, xf)  # warm-up (workspace, code objects)
     ctx.reset_profile()
     ctx.set_profiling(True)
-    import torch
-    torch.cuda.synchronize()
+    ctx.synchronize()
     t0 = time.perf_counter()
     ctx.predict(ls, xf)
-    torch.cuda.synchronize()
+    ctx.synchronize()
     dt = time.perf_counter() - t0
     prof = ctx.profile()
     ctx.set_profiling(False)
@@ -130,7 +191,7 @@ def predict_line(ctx, x, y, e, N, d, args):
         ref_cpu.GP(x, y, e, xf[:, :m], ls, batch_size=10000)
         cdt = time.perf_counter() - t1
         out["cpu_baseline"] = {"points_per_s": m / cdt, "sample": f"oracle GP (GP_func.py:12-45 restated) on {m} "
-                               f"query points, host BLAS threads={os.environ.get('OMP_NUM_THREADS')}", "s": cdt}
+                               f"query points, 1 core", "cores": 1, "blas_threads": blas_threads(), "s": cdt}
     return out
 
 
@@ -198,6 +259,47 @@ def psurf_line(ctx, args):
     return out
 
 
+def launch_ranks(n):
+    """`--gpus N` without a launcher: start the N rank processes (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* set, one GPU each) before this process touches any GPU, and exit
+    with their status. Only rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc != 0), 0)
+
+
+def plumbing(args, world, rank):
+    """CPU-only check of the multi-rank plumbing (`--plumbing`): the rank processes, the
+    library's host-transport communicator, the barrier and the max-over-ranks timing, with a
+    trivial stand-in score (no GP, no GPU). Prints n_gpus and the rank count; no measurement."""
+    import gpfit
+    comm = gpfit.Comm.from_env(transport="host") if world > 1 else None
+    P = (args.swarm_per_gpu or (64 if world == 1 else 32)) * world
+    pos = np.random.default_rng(args.seed).uniform(0.05, 0.6, size=(P, args.d))
+    lo_r, hi_r = rank * P // world, (rank + 1) * P // world
+    t0 = time.perf_counter()
+    local = np.sum(pos[lo_r:hi_r] ** 2, axis=1)
+    full = comm.exchange_scores(P, local) if comm else local
+    dt = time.perf_counter() - t0
+    ranks = int(comm.allreduce([1.0])[0]) if comm else 1
+    dt = float(comm.allreduce([dt], op="max")[0]) if comm else dt
+    if rank == 0:
+        print(json.dumps({"metric": "plumbing check (no GPU work)", "value": None, "unit": None, "n_gpus": world,
+                          "ranks_joined": ranks, "swarm": P, "scores_ok": bool(np.array_equal(full, np.sum(pos ** 2, axis=1))),
+                          "ms": dt * 1e3}), flush=True)
+    if comm:
+        comm.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -205,11 +307,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--n", type=int, default=4096)
     ap.add_argument("--d", type=int, default=3)
-    ap.add_argument("--swarm-per-gpu", type=int, default=64)
+    ap.add_argument("--swarm-per-gpu", type=int, default=None,
+                    help="particles per GPU (default 64 on one GPU = config C, 32 per GPU at N > 1 = config D)")
     ap.add_argument("--hetero", action="store_true")
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--cpu-sample", type=int, default=8)
-    ap.add_argument("--cpu-workers", type=int, default=8)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="do not bracket launches with HIP events")
     ap.add_argument("--pso-steps", type=int, default=3, help="secondary: real PSO iterations timed")
@@ -219,28 +320,34 @@ def main():
     ap.add_argument("--no-hull", action="store_true", help="skip the convex-hull grid line (SURVEY.md §8f row 3)")
     ap.add_argument("--psurf-rows", type=int, default=100000,
                     help="secondary (SURVEY.md §8f row 4): probability-surface rows, 0 = skip")
+    ap.add_argument("--plumbing", action="store_true", help="CPU-only multi-rank plumbing check (no measurement)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    import torch.distributed as dist
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)", file=sys.stderr)
+        sys.exit(2)
+    if args.plumbing:
+        plumbing(args, world, rank)
+        return
 
     import gpfit
     from gpfit.swarm import Swarm, centred_lhs, make_scorer, search_bounds, sigma_grid  # noqa: F401
 
     N, d = args.n, args.d
+    spg = args.swarm_per_gpu or (64 if world == 1 else 32)
     x, y, e = synthetic(N, d, args.seed, args.hetero)
     lo, hi = search_bounds(x)
     s, ex = sigma_grid()
-    P = args.swarm_per_gpu * world
+    P = spg * world
 
     ctx = gpfit.Context(local)
-    score = make_scorer(x, y, e, s, ex, lo, hi, ctx=ctx)
+    comm = gpfit.Comm.from_env(ctx) if world > 1 else None  # RCCL on this rank's GPU
+    score = make_scorer(x, y, e, s, ex, lo, hi, ctx=ctx, comm=comm)
     rng = np.random.default_rng(args.seed + 1000)  # identical on every rank
 
     def batch():
@@ -248,31 +355,29 @@ def main():
         # so every evaluation is a full factorise + score (no sentinel short-cuts)
         return rng.uniform(0.05, 0.6, size=(P, d))
 
+    def fence():
+        ctx.synchronize()  # device-wide (hipDeviceSynchronize): the torch.cuda.synchronize() role
+        if comm is not None:
+            comm.barrier()
+
     for _ in range(args.warmup):
         score(batch())
 
     if not args.no_profile:
         ctx.set_profiling(True)
     ctx.reset_profile()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    fence()
     t0 = time.perf_counter()
     best = np.inf
     for _ in range(args.steps):
         sc = score(batch())
         best = min(best, float(sc[np.argmin(sc)]))
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    fence()
     dt = time.perf_counter() - t0
     prof = ctx.profile()
     ctx.set_profiling(False)
-
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    if comm is not None:
+        dt = float(comm.allreduce([dt], op="max")[0])  # max over ranks
     evals = P * args.steps                # swarm x iterations, all of them full evaluations
     value = evals / dt
 
@@ -284,32 +389,43 @@ def main():
         sw = Swarm(centred_lhs(lo, hi, P, args.seed), lo, hi, score, progress=False, verbose=False)
         ctx.reset_profile()
         ctx.set_profiling(True)
-        if world > 1:
-            dist.barrier()
+        fence()
         t1 = time.perf_counter()
         e0 = sw.evals
         for i in range(args.pso_steps):
             sw.step(i)
-        if world > 1:
-            dist.barrier()
+        fence()
         pdt = time.perf_counter() - t1
         live = ctx.profile()["evals"]
         ctx.set_profiling(False)
+        if comm is not None:
+            pdt = float(comm.allreduce([pdt], op="max")[0])
         pso = {"iters": args.pso_steps, "evals_per_s": (sw.evals - e0) / pdt,
                "iters_per_s": args.pso_steps / pdt,
                "live_fraction_rank0": live / max(1, (sw.evals - e0) / world)}
 
-    # roofline of the dominant kernel, from HIP events on the library stream
-    achieved = prof["panel_flops"] / (prof["panel_ms"] * 1e-3) / 1e12 if prof["panel_ms"] > 0 else None
+    # roofline of the dominant kernel, from HIP events on the library's streams
+    groups = gpfit.plan_check(spg, -(-N // 128))["groups"]
+    if groups == 1:
+        # one stream: the launches do not overlap, per-launch event time is exact
+        achieved = prof["panel_flops"] / (prof["panel_ms"] * 1e-3) / 1e12 if prof["panel_ms"] > 0 else None
+        timing = "k_step launch average (HIP events on the library stream)"
+    else:
+        # concurrent particle-group streams: per-launch windows overlap, so rate the whole
+        # factorisation phase (its wall time, all groups) on the k_step + diagonal flops
+        fl = prof["panel_flops"] + prof["diag_flops"]
+        achieved = fl / (prof["factor_wall_ms"] * 1e-3) / 1e12 if prof["factor_wall_ms"] > 0 else None
+        timing = f"factorisation-phase wall over {groups} concurrent group streams (non-overlapping)"
     # practical ceiling: the same GEMM core alone on L-tile-shaped operands (gpf_gemm_bench,
     # direct-to-LDS, N=4096-sized panels, depth 2048, 960 workgroups)
     core = ctx.gemm_bench(mode=2, npad=4096, particles=64, tiles=15, depth=2048, iters=3) \
         if (rank == 0 and N >= 2048) else None
-    traffic = pmc_traffic(N, d, args.swarm_per_gpu)
+    traffic = pmc_traffic(N, d, spg)
     roof = {"kernel": "k_step", "bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
             "traffic": traffic["bytes_per_launch"] if traffic else None,
             "traffic_source": traffic["source"] if traffic else None,
+            "timing": timing, "particle_groups": groups,
             "gemm_core_tflops": core,
             "frac_of_gemm_core": (achieved / core) if (achieved and core) else None,
             "launches": prof["panel_launches"], "avg_launch_ms": prof["panel_ms"] / max(prof["panel_launches"], 1),
@@ -318,7 +434,7 @@ def main():
             "factor_phase_tflops": (prof["factor_flops"] / (prof["factor_wall_ms"] * 1e-3) / 1e12)
             if prof["factor_wall_ms"] > 0 else None}
     build_gbs = (prof["build_bytes"] / (prof["build_ms"] * 1e-3) / 1e9) if prof["build_ms"] > 0 else None
-    breakdown = {k: prof[k] for k in ("panel_ms", "diag_ms", "build_ms", "loss_ms")}
+    breakdown = {k: prof[k] for k in ("panel_ms", "diag_ms", "build_ms", "loss_ms", "factor_wall_ms")}
     breakdown["k_build_cov_GBps"] = build_gbs
     breakdown["evals_on_gpu"] = prof["evals"]
 
@@ -335,28 +451,24 @@ def main():
     hull = None
     if solo and not args.no_hull:
         hull = hull_line(ctx, args)
-
-    if solo and not args.no_cpu and args.cpu_sample > 0:
-        rng = np.random.default_rng(args.seed + 7)
-        sample = lo + (hi - lo) * rng.uniform(0.2, 0.8, size=(args.cpu_sample, d))
-        workers = max(1, min(args.cpu_workers, args.cpu_sample))
-        cv, _, cdt = cpu_baseline(x, y, e, sample, lo, hi, workers)
-        cpu = {"value": cv, "unit": "evals/s", "cores": workers, "kind": "port",
-               "sample": f"{args.cpu_sample} evaluate_loss calls (oracle/ref_cpu.py, same NumPy/LAPACK calls as "
-                         f"find_len_scales.py:154-182) at N={N} d={d} on the same synthetic data, fork pool of "
-                         f"{workers} single-BLAS-thread workers, {cdt:.1f} s wall",
-               "host_cpu_count": os.cpu_count()}
+    if solo and not args.no_cpu:
+        cpu = cpu_baselines(x, y, e, lo, hi, N, d, args.seed)
 
     if rank == 0:
+        letter = config_letter(N, d, spg, args.hetero)
         line = {
             "metric": f"PSO objective evals/sec (swarm x iters) at N={N} d={d}",
             "value": value, "unit": "evals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": f"PSO objective, BASELINE config {config_letter(N, d, args.swarm_per_gpu, args.hetero)}: "
-                                   f"synthetic N={N} d={d}, swarm {args.swarm_per_gpu}/GPU",
-                       "N": N, "d": d, "swarm": P, "global_batch": P, "seq_len": N,
-                       "parallelism": f"swarm-shard x{world}", "hetero_noise": bool(args.hetero),
+            "vs_baseline": (value / cpu["value"]) if cpu else None,
+            "vs_baseline_basis": "GPU value / CPU reference-policy baseline (cpu_baseline.value) on this box"
+            if cpu else None,
+            "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"PSO objective, BASELINE config {letter}: synthetic N={N} d={d}, "
+                                   f"swarm {spg}/GPU x {world} GPU = {P}",
+                       "N": N, "d": d, "swarm": P, "swarm_per_gpu": spg, "global_batch": P, "seq_len": N,
+                       "parallelism": f"swarm-shard x{world} (libgpfit RCCL all-reduce)" if world > 1 else "single GPU",
+                       "hetero_noise": bool(args.hetero),
                        "pso_iters_per_s": args.steps / dt, "particles": "interior l~U[0.05,0.6]^d (full work)"},
             "pso_loop": pso,
             "predict": predict,
@@ -365,12 +477,14 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
+            "gpu_vs_cpu_all_cores": (value / cpu["all_cores"]["value"]) if cpu else None,
             "breakdown_ms": breakdown,
+            "build": gpfit.build_info(),
         }
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

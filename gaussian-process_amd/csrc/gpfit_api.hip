@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <cmath>
 #include <cstdarg>
 #include <cstdint>
@@ -983,6 +984,13 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
   return GPF_OK;
 }
 
+int gpf_sync(gpf_ctx* c) {
+  if (!c) return GPF_BAD_ARG;
+  GPF_HIP(c, hipSetDevice(c->device));
+  GPF_HIP(c, hipDeviceSynchronize());
+  return GPF_OK;
+}
+
 int gpf_set_profiling(gpf_ctx* c, int on) {
   if (!c) return GPF_BAD_ARG;
   c->prof = on != 0;  // (profiled batches take the plain launch path, never a graph)
@@ -1260,3 +1268,6 @@ int gpf_debug_diag_stamps(unsigned long long* out, int n) {
 #endif
 
 }  // extern "C"
+
+// swarm exchange across ranks (after the C-ABI above: it calls gpf_eval_batch)
+#include "gpf_comm.hip"

@@ -16,6 +16,8 @@ PKG_DIR = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("GPFIT_LIB", PKG_DIR / "libgpfit.so"))
 
 GPF_OK, GPF_NOT_PD, GPF_HIP_ERROR, GPF_BAD_ARG = 0, 1, 2, 3
+GPF_COMM_RCCL, GPF_COMM_HOST = 1, 2
+GPF_OP_SUM, GPF_OP_MAX = 0, 1
 ABI_VERSION = 1
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -49,6 +51,16 @@ SIGNATURES = {
     "gpf_gemm_bench": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_int, _dp]),
     "gpf_build_info": (ctypes.c_char_p, []),
+    "gpf_sync": (ctypes.c_int, [_vp]),
+    "gpf_comm_open": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                     ctypes.POINTER(_vp)]),
+    "gpf_comm_close": (None, [_vp]),
+    "gpf_comm_rank": (ctypes.c_int, [_vp]),
+    "gpf_comm_size": (ctypes.c_int, [_vp]),
+    "gpf_comm_last_error": (ctypes.c_char_p, [_vp]),
+    "gpf_comm_allreduce": (ctypes.c_int, [_vp, _dp, ctypes.c_int64, ctypes.c_int]),
+    "gpf_comm_exchange_scores": (ctypes.c_int, [_vp, ctypes.c_int, _dp, ctypes.c_int, ctypes.c_int, _dp, _ip]),
+    "gpf_eval_batch_sharded": (ctypes.c_int, [_vp, _vp, _dp, ctypes.c_int, _dp, _ip]),
     "gpf_plan_check": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_longlong),
                                       ctypes.c_char_p, ctypes.c_int]),
 }
@@ -186,6 +198,23 @@ class Context:
         self._check(rc, "gpf_eval_batch")
         return (loss, mu, sd) if want_mu_sd else loss
 
+    def eval_batch_sharded(self, comm, positions):
+        """This rank's rows of the (P, d) batch on this GPU, then the swarm exchange
+        (gpf_eval_batch_sharded): every rank returns the same (P,) scores, or raises the same
+        error (LinAlgError for a non-PD particle on any rank)."""
+        P = _f64(positions)
+        if P.ndim == 1:
+            P = P.reshape(1, -1)
+        loss = np.empty(P.shape[0])
+        bad = ctypes.c_int(-1)
+        rc = self.lib.gpf_eval_batch_sharded(self._h, comm.handle, _ptr(P), P.shape[0], _ptr(loss), ctypes.byref(bad))
+        self._check(rc, "gpf_eval_batch_sharded")
+        return loss
+
+    def synchronize(self):
+        """Device-wide fence (gpf_sync): all queued work on this context's GPU has finished."""
+        self._check(self.lib.gpf_sync(self._h), "gpf_sync")
+
     def predict(self, lengths, x_fit, batch_size=10000):
         ls = _f64(lengths).reshape(-1)
         xf = _f64(x_fit)
@@ -287,7 +316,101 @@ class Context:
         return c
 
 
+class Comm:
+    """Rank `rank` of `nranks` in a swarm-exchange group (gpf_comm, include/gpfit.h).
+
+    transport "rccl": ncclAllReduce on `ctx`'s GPU (one process per GPU); "host": the same
+    exchange over the TCP rendezvous sockets (no device; CPU tests and tools).
+    """
+
+    def __init__(self, rank, nranks, host="127.0.0.1", port=29600, transport="rccl", ctx=None):
+        self.lib = load_library()
+        kind = {"rccl": GPF_COMM_RCCL, "host": GPF_COMM_HOST}[transport]
+        if kind == GPF_COMM_RCCL and ctx is None:
+            raise ValueError("the rccl transport needs the rank's Context")
+        h = _vp()
+        rc = self.lib.gpf_comm_open(ctx._h if ctx is not None else None, int(rank), int(nranks), host.encode(),
+                                    int(port), kind, ctypes.byref(h))
+        if rc != GPF_OK or not h.value:
+            why = ctx.lib.gpf_last_error(ctx._h).decode(errors="replace") if ctx is not None else ""
+            raise GPFitError(f"gpf_comm_open(rank={rank}, nranks={nranks}, {host}:{port}, {transport}) failed "
+                             f"(rc={rc}) {why}")
+        self.handle = h
+        self.rank, self.size, self.transport = int(rank), int(nranks), transport
+
+    @classmethod
+    def from_env(cls, ctx=None, transport=None):
+        """torchrun-style environment: RANK, WORLD_SIZE, MASTER_ADDR; the rendezvous port is
+        GPF_COMM_PORT, else MASTER_PORT + 1 (MASTER_PORT itself is the launcher's store)."""
+        rank = int(os.environ.get("RANK", "0"))
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+        port = int(os.environ.get("GPF_COMM_PORT", int(os.environ.get("MASTER_PORT", "29599")) + 1))
+        transport = transport or os.environ.get("GPF_COMM_TRANSPORT", "rccl" if ctx is not None else "host")
+        return cls(rank, world, host, port, transport, ctx)
+
+    def close(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            self.lib.gpf_comm_close(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _err(self):
+        return self.lib.gpf_comm_last_error(self.handle).decode(errors="replace")
+
+    def allreduce(self, values, op="sum"):
+        buf = np.array(values, dtype=np.float64, copy=True).reshape(-1)
+        rc = self.lib.gpf_comm_allreduce(self.handle, _ptr(buf), buf.shape[0],
+                                         {"sum": GPF_OP_SUM, "max": GPF_OP_MAX}[op])
+        if rc != GPF_OK:
+            raise GPFitError(f"gpf_comm_allreduce: {self._err()}")
+        return buf
+
+    def barrier(self):
+        self.allreduce(np.zeros(1))
+
+    def rows(self, P):
+        """This rank's contiguous rows [rP/G, (r+1)P/G) of a P-particle swarm."""
+        return self.rank * P // self.size, (self.rank + 1) * P // self.size
+
+    def exchange_scores(self, P, local, local_rc=GPF_OK, local_bad=-1):
+        """gpf_comm_exchange_scores: this rank's scores of its rows -> the full (P,) vector on
+        every rank; a non-PD particle on any rank raises LinAlgError on every rank."""
+        loss = np.empty(P)
+        loc = _f64(local) if local is not None else np.zeros(0)
+        bad = ctypes.c_int(-1)
+        rc = self.lib.gpf_comm_exchange_scores(self.handle, int(P), _ptr(loc), int(local_rc), int(local_bad),
+                                               _ptr(loss), ctypes.byref(bad))
+        if rc == GPF_NOT_PD:
+            err = np.linalg.LinAlgError("Matrix is not positive definite")
+            err.bad_index = bad.value  # the smallest failing row of the whole swarm
+            raise err
+        if rc == GPF_BAD_ARG:
+            raise ValueError(f"gpf_comm_exchange_scores: {self._err()}")
+        if rc != GPF_OK:
+            raise GPFitError(f"gpf_comm_exchange_scores: {self._err()}")
+        return loss
+
+
 _DEFAULT = {}
+_COMM = {}
+
+
+def default_comm(ctx=None):
+    """The process-wide swarm-exchange group when the launcher started several ranks
+    (WORLD_SIZE > 1 in the environment), else None. Created on first use: RCCL on this
+    process's GPU context, or the host transport when no context is given."""
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        return None
+    key = "ctx" if ctx is not None else "host"
+    if key not in _COMM:
+        _COMM[key] = Comm.from_env(ctx)
+    return _COMM[key]
 
 
 def default_context():

@@ -5,14 +5,15 @@ RNG draws from the global ``np.random`` stream in the same order, same strict
 ``<`` comparisons and first-index ``argmin``, same progress strings); what
 changes is the fan-out: instead of pickling one task per particle into a fork
 pool (:73-77,102-104,133-135), every batch of particles is one call into the
-HIP library (``gpf_eval_batch``), sharded across ranks when torch.distributed
-is initialised (one process per GPU, one all-reduce per batch).
+HIP library (``gpf_eval_batch``), sharded across ranks when the launcher starts
+several (one process per GPU; the library's own RCCL all-reduce per batch,
+``gpf_eval_batch_sharded``).
 """
 from __future__ import annotations
 
 import numpy as np
 
-from ._lib import default_context
+from ._lib import default_comm, default_context
 
 NUM_PARTICLES = 40      # find_len_scales.py:50
 MAX_ITER = 500          # :51
@@ -78,76 +79,60 @@ def centred_lhs(lower, upper, n, seed=None):
     return lower + u * (upper - lower)
 
 
-def dist_rank_world(group=None):
-    """(rank, world) of an initialised torch.distributed group, else (0, 1).
-
-    Looks torch up in sys.modules instead of importing it: a process that never
-    imported torch cannot have a process group.
-    """
-    import sys
-    dist = sys.modules.get("torch.distributed")
-    if dist is None or not dist.is_available() or not dist.is_initialized():
-        return 0, 1
-    return dist.get_rank(group), dist.get_world_size(group)
-
-
 class ShardedScorer:
-    """Scores a (P, d) batch of particles, sharded over ranks.
+    """Scores a (P, d) batch of particles, sharded over the ranks of a gpfit.Comm.
 
-    ``backend(positions) -> scores`` evaluates the local rows (by default one
-    gpf_eval_batch call on this process's GPU). Rank r of G takes rows
-    [r*P//G, (r+1)*P//G); a zero-initialised (P,) buffer is summed across ranks
-    with one all-reduce (exact: every entry has exactly one non-zero
-    contributor), so every rank sees the full score vector and takes the same
-    argmin (find_len_scales.py:81,110). World size 1 is a plain call.
+    ``backend(positions) -> scores`` evaluates the local rows. With a GPU context the whole
+    step is one library call, gpf_eval_batch_sharded: rank r scores rows [r*P//G, (r+1)*P//G)
+    on its GPU and one all-reduce of a zero-initialised [P + G] vector (RCCL) gives every rank
+    the full score vector (exact: one non-zero contributor per entry), so every rank takes the
+    same argmin (find_len_scales.py:81,110). With an injected evaluator (tests) the local rows
+    are scored in Python and the same C exchange runs (gpf_comm_exchange_scores). A failing
+    particle on any rank raises the same error on every rank (the G status entries), instead
+    of leaving the other ranks blocked in the collective. World size 1 is a plain call.
     """
 
-    def __init__(self, backend, group=None):
+    def __init__(self, backend, comm=None, ctx=None):
         self.backend = backend
-        self.group = group
-        self.rank, self.world = dist_rank_world(group)
+        self.comm = comm if (comm is not None and comm.size > 1) else None
+        self.ctx = ctx
+        self.rank, self.world = (comm.rank, comm.size) if self.comm is not None else (0, 1)
         self.evals = 0
 
     def __call__(self, positions):
         P = positions.shape[0]
-        if self.world == 1:
+        if self.comm is None:
             self.evals += P
             return np.asarray(self.backend(positions), dtype=np.float64)
-        lo = self.rank * P // self.world
-        hi = (self.rank + 1) * P // self.world
-        part = np.zeros(P)
-        if hi > lo:
-            part[lo:hi] = self.backend(positions[lo:hi])
+        lo, hi = self.comm.rows(P)
         self.evals += hi - lo
-        return allreduce_sum(part, self.group)
+        if self.ctx is not None:
+            return self.ctx.eval_batch_sharded(self.comm, positions)
+        from ._lib import GPF_HIP_ERROR, GPF_NOT_PD, GPF_OK
+        rc, local, failure = GPF_OK, None, None
+        try:
+            local = np.asarray(self.backend(positions[lo:hi]), dtype=np.float64) if hi > lo else np.zeros(0)
+        except np.linalg.LinAlgError:
+            rc = GPF_NOT_PD  # (the injected evaluator does not say which row; the first is reported)
+        except Exception as exc:  # noqa: BLE001 - re-raised below, after the other ranks are told
+            rc, failure = GPF_HIP_ERROR, exc
+        try:
+            return self.comm.exchange_scores(P, local, rc, 0)
+        except Exception:
+            if failure is not None:
+                raise failure
+            raise
 
 
-def allreduce_sum(buf, group=None):
-    """Sum a float64 vector over ranks (RCCL when the group is nccl, else gloo)."""
-    import torch
-    import torch.distributed as dist
-    backend = dist.get_backend(group)
-    t = torch.from_numpy(np.ascontiguousarray(buf))
-    if backend == "nccl":
-        dev = torch.device("cuda", torch.cuda.current_device())
-        t = t.to(dev)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-        return t.cpu().numpy()
-    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-    return t.numpy()
-
-
-def broadcast_seed(seed, group=None):
-    """All ranks must draw identical r1/r2; rank 0 picks the seed if none given."""
-    import torch
-    import torch.distributed as dist
+def share_seed(seed, comm):
+    """All ranks must draw identical r1/r2 (find_len_scales.py:91-92): rank 0's seed (picked
+    from np.random when none is given) reaches every rank through one all-reduce."""
+    if comm is None or comm.size == 1:
+        return seed
     if seed is None:
-        seed = int(np.random.randint(0, 2**31 - 1)) if dist.get_rank(group) == 0 else 0
-    t = torch.tensor([int(seed)], dtype=torch.int64)
-    if dist.get_backend(group) == "nccl":
-        t = t.cuda()
-    dist.broadcast(t, src=0, group=group)
-    return int(t.item())
+        seed = int(np.random.randint(0, 2**31 - 1)) if comm.rank == 0 else 0
+    mine = float(seed) if comm.rank == 0 else 0.0
+    return int(comm.allreduce([mine])[0])
 
 
 class Swarm:
@@ -234,43 +219,46 @@ def prepare(x_known, y_known, e_known, *, max_points=MAX_POINTS, verbose=True):
 
 
 def make_scorer(x_known, y_known, e_known, sigma_vals, expected, lower, upper, *, evaluator=None, ctx=None,
-                group=None):
-    """Sharded batch objective: gpf_eval_batch on this GPU, or an injected per-particle evaluator."""
+                comm=None):
+    """Sharded batch objective: gpf_eval_batch(_sharded) on this GPU, or an injected per-particle
+    evaluator. comm: a gpfit.Comm, or None for the launcher's group (WORLD_SIZE > 1) if any."""
     if evaluator is None:
         dev = ctx if ctx is not None else default_context()
         dev.set_data(x_known, y_known, e_known)
         dev.set_grid(sigma_vals, expected, lower, upper)
-        backend = dev.eval_batch
-    else:
-        def backend(pos):
-            args = [(p, x_known, y_known, e_known, sigma_vals, expected, lower, upper) for p in pos]
-            return np.array(list(evaluator(args)))
-    return ShardedScorer(backend, group)
+        comm = comm if comm is not None else default_comm(dev)
+        return ShardedScorer(dev.eval_batch, comm, dev)
+
+    def backend(pos):
+        args = [(p, x_known, y_known, e_known, sigma_vals, expected, lower, upper) for p in pos]
+        return np.array(list(evaluator(args)))
+    comm = comm if comm is not None else default_comm()
+    return ShardedScorer(backend, comm)
 
 
 def particle_swarm(x_known, y_known, e_known, PSO_progress, *, num_particles=NUM_PARTICLES,
                    max_iter=MAX_ITER, max_points=MAX_POINTS, init_positions=None, seed=None,
-                   evaluator=None, trace=None, ctx=None, group=None, verbose=True):
+                   evaluator=None, trace=None, ctx=None, comm=None, verbose=True):
     """len_scale_opt body (find_len_scales.py:22-150) with a batched evaluator.
 
     ``evaluator(args_list) -> scores`` (reference-style per-particle args, used
     by tests to inject a checker) replaces the default backend, gpf_eval_batch
-    on this process's GPU. Either way batches are sharded over ranks.
+    on this process's GPU. Either way batches are sharded over the ranks of ``comm`` (default:
+    the launcher's group when WORLD_SIZE > 1, gpfit.default_comm).
     Returns (global_best_position, info) where info holds the final score,
     restart count and evaluation count.
     """
     x_known, y_known, e_known, lower, upper, sigma_vals, expected = prepare(
         x_known, y_known, e_known, max_points=max_points, verbose=verbose)
 
-    if dist_rank_world(group)[1] > 1:
-        seed = broadcast_seed(seed, group)
+    score = make_scorer(x_known, y_known, e_known, sigma_vals, expected, lower, upper,
+                        evaluator=evaluator, ctx=ctx, comm=comm)
+    seed = share_seed(seed, score.comm)
     if seed is not None:
         np.random.seed(seed)
     if init_positions is None:
         init_positions = centred_lhs(lower, upper, num_particles, seed)
 
-    score = make_scorer(x_known, y_known, e_known, sigma_vals, expected, lower, upper,
-                        evaluator=evaluator, ctx=ctx, group=group)
     sw = Swarm(init_positions, lower, upper, score, progress=PSO_progress, verbose=verbose)
     for i in range(max_iter):
         sw.step(i)

@@ -109,6 +109,59 @@ int gpf_hull_fill(gpf_ctx* ctx, const double* shell, int64_t n, int d, const dou
                   int64_t* m);
 int gpf_hull_fetch(gpf_ctx* ctx, double* out);
 
+/* ---- swarm exchange across ranks (one process per GPU) ----
+ *
+ * Replaces the cross-process half of the particle fan-out: the reference's single process
+ * scatters the swarm over a fork pool and gathers the scores (find_len_scales.py:73-77,
+ * 102-104,133-135); here every rank scores its contiguous rows [rP/G, (r+1)P/G) and one
+ * all-reduce (sum) of a zero-initialised [P + G] float64 vector hands every rank the full
+ * score vector (exact: one non-zero contributor per entry), so all ranks take the same
+ * first-index argmin (:81,110). The G trailing entries carry each rank's status, so a non-PD
+ * particle or a device error on one rank is reported on every rank (same bad_idx, same code)
+ * instead of leaving the others blocked in the collective.
+ *
+ * Transports: GPF_COMM_RCCL = ncclAllReduce on the context's device (RCCL over xGMI; rank 0
+ * hands out the ncclUniqueId over TCP); GPF_COMM_HOST = the same exchange over the TCP
+ * rendezvous sockets (rank 0 combines in rank order; needs no device). Rendezvous: rank 0
+ * listens on host:port, the others connect (retrying until GPF_COMM_TIMEOUT_S, default 600 s).
+ * A communicator is not thread-safe. */
+#define GPF_COMM_RCCL 1
+#define GPF_COMM_HOST 2
+#define GPF_OP_SUM 0
+#define GPF_OP_MAX 1
+
+typedef struct gpf_comm gpf_comm;
+
+/* Join rank `rank` of `nranks`. ctx: the rank's context (required for GPF_COMM_RCCL: the
+ * communicator lives on its device; may be NULL for GPF_COMM_HOST). */
+int gpf_comm_open(gpf_ctx* ctx, int rank, int nranks, const char* host, int port, int transport, gpf_comm** out);
+void gpf_comm_close(gpf_comm* comm);
+int gpf_comm_rank(const gpf_comm* comm);
+int gpf_comm_size(const gpf_comm* comm);
+const char* gpf_comm_last_error(const gpf_comm* comm);
+
+/* In-place all-reduce of n host doubles (GPF_OP_SUM or GPF_OP_MAX) across the ranks: the
+ * seed broadcast of the PSO driver, the bench's barrier and max-over-ranks timing. */
+int gpf_comm_allreduce(gpf_comm* comm, double* buf, int64_t n, int op);
+
+/* The exchange step alone, given this rank's results for its rows [rP/G, (r+1)P/G):
+ * local (hi - lo scores; ignored unless local_rc == GPF_OK), local_rc (GPF_OK / GPF_NOT_PD /
+ * other), local_bad (the row, relative to lo, of the first non-PD particle). Fills loss_P on
+ * every rank, or returns on every rank GPF_NOT_PD with *bad_idx = the smallest failing row of
+ * the whole swarm (the particle the reference's in-order map would raise on first), or the
+ * error code of the first failed rank. */
+int gpf_comm_exchange_scores(gpf_comm* comm, int P, const double* local, int local_rc, int local_bad,
+                             double* loss_P, int* bad_idx);
+
+/* Sharded gpf_eval_batch: this rank scores its rows of ls_Pd (P, d) on its context, then
+ * gpf_comm_exchange_scores. Every rank passes the same ls_Pd and receives the same loss_P. */
+int gpf_eval_batch_sharded(gpf_ctx* ctx, gpf_comm* comm, const double* ls_Pd, int P, double* loss_P,
+                           int* bad_idx);
+
+/* Wait until all work queued by this library on the context's device has finished
+ * (hipDeviceSynchronize on that device): the bench's timing fence. */
+int gpf_sync(gpf_ctx* ctx);
+
 /* ---- measurement hooks (bench.py) ---- */
 
 /* Enable per-kernel-class HIP event timing on the context's stream. */

@@ -45,3 +45,31 @@ def f3():
 @pytest.fixture(scope="session")
 def f4():
     return load_golden("f4_pso_trace.npz")
+
+
+def synth_data(N, d, hetero, seed):
+    """SURVEY.md §8d synthetic set (the construction of bench.synthetic and of
+    tests/golden/make_golden.py's synth_data): x~U[0,1)^d, y=sum sin(2 pi x)+0.1 N(0,1),
+    e = 0.1 or U[0.05, 0.2] (heteroscedastic)."""
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(0.0, 1.0, size=(d, N))
+    y = np.sum(np.sin(2 * np.pi * x), axis=0) + 0.1 * rng.standard_normal(N)
+    e = rng.uniform(0.05, 0.2, size=N) if hetero else np.full(N, 0.1)
+    return x, y, e
+
+
+def data_sha256(*arrays):
+    """Hash the reference-side fixture scripts store instead of the regenerated inputs."""
+    import hashlib
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a, dtype=np.float64).tobytes())
+    return h.hexdigest()
+
+
+def fixture_data(meta, sha):
+    """Regenerate a fixture's synthetic inputs from its (N, d, hetero, seed) and check them."""
+    N, d, het, seed = (int(v) for v in meta)
+    x, y, e = synth_data(N, d, bool(het), seed)
+    assert data_sha256(x, y, e) == str(sha), "regenerated inputs differ from the fixture's"
+    return x, y, e

@@ -1,8 +1,11 @@
-"""The N>1 path: swarm rows sharded over ranks with one all-reduce per batch.
+"""The N>1 path: swarm rows sharded over ranks, one exchange per batch, inside libgpfit.
 
-world_size 2 over gloo on CPU; the objective is the injected checker so no GPU
-is needed. The sharded trajectory must equal the single-rank reference
-trajectory bit for bit on every rank.
+Ranks are processes (spawn) joined by the library's own communicator (gpf_comm_open,
+include/gpfit.h). On CPU the host transport carries the exchange (the same C protocol the
+RCCL transport runs on GPUs: gpf_comm_exchange_scores) and the objective is the injected
+checker, so no GPU is needed. The sharded trajectory must equal the single-rank reference
+trajectory (F4, produced by the reference's own len_scale_opt) bit for bit on every rank
+(SURVEY.md §8e), with every particle scored exactly once across the ranks.
 """
 import os
 import socket
@@ -10,6 +13,8 @@ import sys
 
 import numpy as np
 import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
@@ -20,17 +25,18 @@ def _free_port():
     return p
 
 
+def _env(rank, world, port, **extra):
+    os.environ.update(MASTER_ADDR="127.0.0.1", GPF_COMM_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", GPF_COMM_TIMEOUT_S="120", **extra)
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "gaussian-process_amd")]
+
+
 def _worker(rank, world, port, path, k, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path[:0] = [root, os.path.join(root, "gaussian-process_amd")]
-    import io
+    _env(rank, world, port, GPF_COMM_TRANSPORT="host")
     import contextlib
-    import torch.distributed as dist
+    import io
     from gpfit.swarm import particle_swarm
     from oracle import ref_cpu
-    dist.init_process_group("gloo", rank=rank, world_size=world)
     f4 = np.load(path, allow_pickle=False)
     x = np.asfortranarray(f4[f"c{k}_x"])
     buf = io.StringIO()
@@ -39,27 +45,33 @@ def _worker(rank, world, port, path, k, q):
                                     seed=int(f4[f"c{k}_seed"]),
                                     evaluator=lambda args: [ref_cpu.evaluate_loss_helper(a) for a in args])
     q.put((rank, best.tolist(), buf.getvalue(), info["local_evals"], info["evals"]))
-    dist.barrier()
-    dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,k", [(2, 0), (3, 1)])
-def test_sharded_swarm_matches_single_rank(world, k):
-    import torch.multiprocessing as mp
-    from conftest import GOLDEN
-    f4 = np.load(GOLDEN / "f4_pso_trace.npz", allow_pickle=False)
+def _spawn(target, world, *args, timeout=300):
+    import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, str(GOLDEN / "f4_pso_trace.npz"), k, q))
-             for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, *args, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=300) for _ in range(world)]
+    try:
+        res = [q.get(timeout=timeout) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
     for p in procs:
-        p.join(timeout=60)
         assert p.exitcode == 0
-    res.sort()
+    return sorted(res)
+
+
+@pytest.mark.parametrize("world,k", [(2, 0), (3, 1), (8, 0)])
+def test_sharded_swarm_matches_single_rank(world, k):
+    from conftest import GOLDEN
+    f4 = np.load(GOLDEN / "f4_pso_trace.npz", allow_pickle=False)
+    res = _spawn(_worker, world, str(GOLDEN / "f4_pso_trace.npz"), k)
     total_local = 0
     for rank, best, log, local, evals in res:
         assert np.array_equal(np.array(best), f4[f"c{k}_best"]), rank
@@ -68,19 +80,60 @@ def test_sharded_swarm_matches_single_rank(world, k):
     assert total_local == res[0][4]  # every particle scored exactly once across ranks
 
 
+def _exchange_worker(rank, world, port, q):
+    """Protocol checks of gpf_comm_exchange_scores / gpf_comm_allreduce at `world` ranks."""
+    _env(rank, world, port)
+    import gpfit
+    from gpfit._lib import GPF_HIP_ERROR, GPF_NOT_PD
+    comm = gpfit.Comm.from_env()
+    out = {}
+    P = 11
+    lo, hi = comm.rows(P)
+    full = np.arange(P) * 1.5 + 0.25
+    out["scores"] = comm.exchange_scores(P, full[lo:hi]).tolist()
+    # a non-PD particle on the last rank (its 2nd row) and on rank 1 (1st row): every rank
+    # raises LinAlgError; the smallest failing row is the one reported
+    rc = GPF_NOT_PD if rank in (1, world - 1) else 0
+    bad = 1 if rank == world - 1 else 0
+    try:
+        comm.exchange_scores(P, full[lo:hi], rc, bad)
+        out["notpd"] = None
+    except np.linalg.LinAlgError as e:
+        out["notpd"] = e.bad_index
+    # a device error on rank 0: every rank raises GPFitError
+    try:
+        comm.exchange_scores(P, full[lo:hi], GPF_HIP_ERROR if rank == 0 else 0, -1)
+        out["hip"] = "no error"
+    except gpfit.GPFitError as e:
+        out["hip"] = "rank 0 failed" in str(e)
+    out["max"] = comm.allreduce([rank, -rank], op="max").tolist()
+    out["sum"] = comm.allreduce([1.0, rank]).tolist()
+    comm.barrier()
+    comm.close()
+    q.put((rank, out))
+
+
+@pytest.mark.parametrize("world", [1, 2, 5])
+def test_exchange_protocol(world):
+    res = _spawn(_exchange_worker, world, timeout=120)
+    P = 11
+    for rank, out in res:
+        assert out["scores"] == (np.arange(P) * 1.5 + 0.25).tolist()
+        rows = [(r * P // world, (r + 1) * P // world) for r in range(world)]
+        failing = [rows[r][0] + (1 if r == world - 1 else 0) for r in range(world) if r in (1, world - 1)]
+        assert out["notpd"] == min(failing)  # the smallest failing row of the swarm, on every rank
+        assert out["hip"] is True
+        assert out["max"] == [world - 1, 0]
+        assert out["sum"] == [world, world * (world - 1) / 2]
+
+
 def _gpu_worker(rank, world, port, path, k, q):
-    """One rank of a gloo group; every rank scores its shard with gpf_eval_batch on GPU 0."""
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      GPFIT_DEVICE="0", OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path[:0] = [root, os.path.join(root, "gaussian-process_amd")]
-    import io
+    """One rank; every rank scores its shard with gpf_eval_batch_sharded on GPU 0 (the host
+    transport: RCCL needs one GPU per rank, the driver's 8-GPU run covers it)."""
+    _env(rank, world, port, GPFIT_DEVICE="0", GPF_COMM_TRANSPORT="host")
     import contextlib
-    import torch  # noqa: F401  (HIP runtime through torch first)
-    import torch.distributed as dist
+    import io
     from gpfit.swarm import particle_swarm
-    if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
     f4 = np.load(path, allow_pickle=False)
     x = np.asfortranarray(f4[f"c{k}_x"])
     buf = io.StringIO()
@@ -88,39 +141,44 @@ def _gpu_worker(rank, world, port, path, k, q):
         best, info = particle_swarm(x, f4[f"c{k}_y"], f4[f"c{k}_e"], True, init_positions=f4[f"c{k}_init"],
                                     seed=int(f4[f"c{k}_seed"]), max_iter=150)
     q.put((rank, best.tolist(), buf.getvalue(), info["local_evals"], info["evals"]))
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
-
-
-def _run_ranks(world, k):
-    import torch.multiprocessing as mp
-    from conftest import GOLDEN
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, str(GOLDEN / "f4_pso_trace.npz"), k, q))
-             for r in range(world)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=600) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
-    return sorted(res)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 4])
 def test_sharded_gpu_swarm_matches_single_rank(world):
     """The multi-rank GPU path (ranks mapped onto the available device): each rank
-    scores its rows of the swarm with gpf_eval_batch, one all-reduce per batch; the trajectory
-    on every rank equals the single-rank GPU trajectory bit for bit, every particle scored once."""
-    one = _run_ranks(1, 0)[0]
-    res = _run_ranks(world, 0)
+    scores its rows with gpf_eval_batch_sharded, one exchange per batch; the trajectory on every
+    rank equals the single-rank GPU trajectory bit for bit, every particle scored once."""
+    from conftest import GOLDEN
+    path = str(GOLDEN / "f4_pso_trace.npz")
+    one = _spawn(_gpu_worker, 1, path, 0, timeout=600)[0]
+    res = _spawn(_gpu_worker, world, path, 0, timeout=600)
     total_local = 0
     for rank, best, log, local, evals in res:
         assert best == one[1], rank
         assert log == one[2], rank
         total_local += local
     assert total_local == res[0][4] == one[4]
+
+
+@pytest.mark.gpu
+def test_rccl_exchange_single_rank():
+    """The RCCL transport (ncclCommInitRank + ncclAllReduce on the context's device) at one
+    rank, the most the one-GPU box allows: the sharded batch equals the plain batch bit for
+    bit, and the all-reduce ops work on device."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "gaussian-process_amd")]
+    import gpfit
+    from conftest import load_golden
+    f2 = load_golden("f2_loss_testfiles.npz")
+    ctx = gpfit.Context(0)
+    comm = gpfit.Comm(0, 1, transport="rccl", ctx=ctx)
+    try:
+        ctx.set_data(f2["c0_x"], f2["c0_y"], f2["c0_e"])
+        ctx.set_grid(f2["sigma_vals"], f2["expected"], f2["c0_lo"], f2["c0_hi"])
+        P = f2["c0_P"]
+        np.testing.assert_array_equal(ctx.eval_batch_sharded(comm, P), ctx.eval_batch(P))
+        assert comm.allreduce([2.5, -1.0], op="max").tolist() == [2.5, -1.0]
+        assert comm.allreduce([2.5, -1.0]).tolist() == [2.5, -1.0]
+    finally:
+        comm.close()
+        ctx.close()

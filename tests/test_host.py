@@ -63,6 +63,22 @@ def test_kmeans_representatives_match_oracle():
         assert np.array_equal(u, v)
 
 
+def test_kmeans_subsample_matches_reference_fixture():
+    """F10 (tests/golden/make_golden_big.py): the points the reference's len_scale_opt keeps
+    (find_len_scales.py:25-47, sklearn KMeans n_init='auto', random_state=0) at N = 300..4096,
+    d = 2..4, and the search box it derives from them (:56-61). The drop-in's prepare() must
+    keep exactly the same points in the same order."""
+    from conftest import fixture_data, load_golden
+    from gpfit.swarm import prepare
+    f = load_golden("f10_kmeans.npz")
+    for i in range(int(f["ncases"])):
+        x, y, e = fixture_data(f[f"c{i}_meta"], f[f"c{i}_data_sha256"])
+        xs, ys, es, lo, hi, _, _ = prepare(_fx(x), y, e, max_points=100, verbose=False)
+        idx = f[f"c{i}_idx"]
+        assert np.array_equal(xs, x[:, idx]) and np.array_equal(ys, y[idx]) and np.array_equal(es, e[idx])
+        assert np.array_equal(lo, f[f"c{i}_lo"]) and np.array_equal(hi, f[f"c{i}_hi"])
+
+
 def test_kmeans_path_taken_above_max_points(capsys):
     from gpfit.swarm import particle_swarm
     rng = np.random.default_rng(1)
