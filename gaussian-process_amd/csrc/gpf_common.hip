@@ -577,6 +577,34 @@ __device__ __forceinline__ void zero_tile64(double* __restrict__ g, size_t gld) 
   }
 }
 
+// Row sums of the 128-tile accumulator times a column vector z (LDS, 128 entries) over this
+// wave's 32 columns: the two column blocks are combined in each lane, then the 16 lanes of a
+// lane group (same rows, different columns) by a butterfly reduce-scatter (15 shuffles instead
+// of 4 x 16). Returns, in lane (g = lane >> 4, c = lane & 15), the sum of row
+// rb + 16 (c >> 2) + g + 4 (c & 3) (accumulator index mi = c >> 2, r = c & 3). Fixed order.
+__device__ __forceinline__ double acc_row_dot(const Acc<128>& acc, const Quad<128>& qd, const double* z) {
+  static_assert(Acc<128>::MBR == 4 && Acc<128>::MBC == 2, "layout of the 128-tile accumulator");
+  const double z0 = z[qd.col(0)], z1 = z[qd.col(1)];
+  double v[16];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[mi * 4 + r] = fma(acc.v[mi][1][r], z1, acc.v[mi][0][r] * z0);
+  const int c = qd.lane & 15;
+#pragma unroll
+  for (int step = 0; step < 4; ++step) {
+    const int m = 8 >> step, h = 8 >> step;  // partner lane distance, half of the live list
+    const bool up = (c & m) != 0;
+#pragma unroll
+    for (int j = 0; j < h; ++j) {
+      const double send = up ? v[j] : v[j + h];
+      const double keep = up ? v[j + h] : v[j];
+      v[j] = keep + __shfl_xor(send, m);
+    }
+  }
+  return v[0];
+}
+
 // Sum over the 4 lane groups {l, l^16, l^32, l^48} of a wave; the result is
 // bitwise identical in all four lanes ((g0+g1)+(g2+g3), addition commutes).
 __device__ __forceinline__ double sum_lane_groups(double v) {

@@ -796,20 +796,18 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
     if (tid < T) zj[tid] = yp[J * T + tid];
     __syncthreads();
     GPF_PHASE(1);
-    // look-ahead: A_II -= L_IJ L_IJ^T (the full tile; only its lower half is ever read), y_I -= L_IJ z_J
+    // y_I -= L_IJ z_J, row sums straight from the accumulators: one partial per row and column
+    // slab of 32 (scratch[slab][row]), combined in slab order after the SYRK's barriers
+    {
+      const int c = qd.lane & 15;
+      scratch[(qd.cb / 32) * T + qd.rb + 16 * (c >> 2) + (qd.lane >> 4) + 4 * (c & 3)] = acc_row_dot(acc, qd, zj);
+    }
+    // look-ahead: A_II -= L_IJ L_IJ^T (the full tile; only its lower half is ever read)
     acc.load(qd, Aii, ld);
     step_gemm<false, true, TRI_C_LOWER>(acc, Aij, Npad, Aij, Npad, T, smem, qd);
     acc.store(qd, Aii, ld);
     GPF_PHASE(2);
-    {
-      const int r = tid & (T - 1), h = tid >> 7;  // 4 quarter-row partial dot products
-      const double* row = Aij + (size_t)r * ld + h * 32;
-      double s = 0.0;
-      for (int c = 0; c < 32; ++c) s = fma(row[c], zj[h * 32 + c], s);
-      scratch[h * T + r] = s;
-    }
-    __syncthreads();
-    if (tid < T)
+    if (tid < T)  // (the SYRK's barriers ordered the scratch writes)
       yp[I * T + tid] =
           yp[I * T + tid] - (((scratch[tid] + scratch[T + tid]) + scratch[2 * T + tid]) + scratch[3 * T + tid]);
     GPF_PHASE(3);
