@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 namespace gpf {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -577,6 +579,15 @@ __device__ __forceinline__ void zero_tile64(double* __restrict__ g, size_t gld) 
   }
 }
 
+// One butterfly step of acc_row_dot over the live list v[0 .. 2H): lanes with bit H of their
+// column index keep the upper half. Every index is a compile-time constant (pack expansion, no
+// loop): a loop over j left the selects to the optimiser, which turned them into a
+// lane-dependent index into v and lowered that as chains of 16 v_cndmask per element.
+template <int H, int... J>
+__device__ __forceinline__ void row_dot_step(double (&v)[16], bool up, std::integer_sequence<int, J...>) {
+  ((v[J] = (up ? v[J + H] : v[J]) + __shfl_xor(up ? v[J] : v[J + H], H)), ...);
+}
+
 // Row sums of the 128-tile accumulator times a column vector z (LDS, 128 entries) over this
 // wave's 32 columns: the two column blocks are combined in each lane, then the 16 lanes of a
 // lane group (same rows, different columns) by a butterfly reduce-scatter (15 shuffles instead
@@ -591,17 +602,10 @@ __device__ __forceinline__ double acc_row_dot(const Acc<128>& acc, const Quad<12
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[mi * 4 + r] = fma(acc.v[mi][1][r], z1, acc.v[mi][0][r] * z0);
   const int c = qd.lane & 15;
-#pragma unroll
-  for (int step = 0; step < 4; ++step) {
-    const int m = 8 >> step, h = 8 >> step;  // partner lane distance, half of the live list
-    const bool up = (c & m) != 0;
-#pragma unroll
-    for (int j = 0; j < h; ++j) {
-      const double send = up ? v[j] : v[j + h];
-      const double keep = up ? v[j + h] : v[j];
-      v[j] = keep + __shfl_xor(send, m);
-    }
-  }
+  row_dot_step<8>(v, (c & 8) != 0, std::make_integer_sequence<int, 8>{});
+  row_dot_step<4>(v, (c & 4) != 0, std::make_integer_sequence<int, 4>{});
+  row_dot_step<2>(v, (c & 2) != 0, std::make_integer_sequence<int, 2>{});
+  row_dot_step<1>(v, (c & 1) != 0, std::make_integer_sequence<int, 1>{});
   return v[0];
 }
 
