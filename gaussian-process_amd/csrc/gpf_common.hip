@@ -517,13 +517,23 @@ __device__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int
 
 // 64x64x64 GEMM with both operands resident in LDS (8 waves, 32x16 each):
 //   A (r,k) at sA[r*la + k];  B (k,c) at sB[c*lb + k] (!NN) or sB[k*lb + c] (NN).
-template <bool NN>
+// TRI: known-zero structure (as in the streamed GEMMs): each wave runs only the k-steps whose
+// 16x16x4 blocks can be non-zero (wave-uniform bounds; 16-aligned blocks, so every skipped
+// MFMA would add exact zeros: results are bitwise those of the dense loop).
+template <bool NN, int TRI = TRI_NONE>
 __device__ __forceinline__ void gemm_lds64(Acc<64>& acc, const double* sA, int la, const double* sB, int lb,
                                            const Quad<64>& qd) {
   constexpr int MBR = Geo<64>::MBR, MBC = Geo<64>::MBC;
+  static_assert(MBR == 2 && MBC == 1, "wave sub-tile of the 64-tile GEMM");
   const int lr = qd.lane & 15, lk = qd.lane >> 4;
+  int k0 = 0, k1 = H;
+  if (TRI == TRI_B_KLEC) k1 = qd.cb + 16;           // B(k,c) = 0 for k > c
+  if (TRI == TRI_B_KGEC) k0 = qd.cb;                // B(k,c) = 0 for k < c
+  if (TRI == TRI_A_KLER) k1 = qd.rb + 32;           // A(r,k) = 0 for k > r (row block 0 stops at rb + 16)
+  const bool live0 = TRI != TRI_C_LOWER || qd.cb < qd.rb + 16;  // lower-only output: row block 0
+  const bool live1 = TRI != TRI_C_LOWER || qd.cb < qd.rb + 32;  // ... row block 1
 #pragma unroll 4
-  for (int ks = 0; ks < H; ks += 4) {
+  for (int ks = k0; ks < k1; ks += 4) {
     double a[MBR], b[MBC];
 #pragma unroll
     for (int mi = 0; mi < MBR; ++mi) a[mi] = sA[(qd.rb + mi * 16 + lr) * la + ks + lk];
@@ -534,10 +544,9 @@ __device__ __forceinline__ void gemm_lds64(Acc<64>& acc, const double* sA, int l
       else
         b[ni] = sB[(ks + lk) * lb + qd.cb + ni * 16 + lr];
     }
-#pragma unroll
-    for (int mi = 0; mi < MBR; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < MBC; ++ni) acc.v[mi][ni] = mfma(a[mi], b[ni], acc.v[mi][ni]);
+    const bool m0 = TRI == TRI_A_KLER ? ks < qd.rb + 16 : live0;
+    if (m0) acc.v[0][0] = mfma(a[0], b[0], acc.v[0][0]);
+    if (live1) acc.v[1][0] = mfma(a[1], b[0], acc.v[1][0]);
   }
 }
 
@@ -554,7 +563,20 @@ __device__ __forceinline__ void tile64_to_lds(double* s, int ld, const double* _
   }
 }
 
+// Global store of one double; WT: write-through (agent-scope relaxed atomic store: the line is
+// written to memory without an L2 write-back fence), for data another workgroup of the same
+// launch reads after a flag hand-off (the early diagonal factor, k_step).
+template <bool WT = false>
+__device__ __forceinline__ void gst(double* p, double v) {
+  if (WT)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+
 // LDS 64x64 -> global, optionally zeroing the strict upper triangle.
+template <bool WT = false>
 __device__ __forceinline__ void lds_to_tile64(double* __restrict__ g, size_t gld, const double* s, int ld,
                                               bool lower_only) {
   const int tid = threadIdx.x;
@@ -565,17 +587,30 @@ __device__ __forceinline__ void lds_to_tile64(double* __restrict__ g, size_t gld
     d2 v;
     v.x = (lower_only && 2 * c2 > row) ? 0.0 : s[row * ld + 2 * c2];
     v.y = (lower_only && 2 * c2 + 1 > row) ? 0.0 : s[row * ld + 2 * c2 + 1];
-    *reinterpret_cast<d2*>(g + (size_t)row * gld + 2 * c2) = v;
+    double* gp = g + (size_t)row * gld + 2 * c2;
+    if (WT) {
+      gst<true>(gp, v.x);
+      gst<true>(gp + 1, v.y);
+    } else {
+      *reinterpret_cast<d2*>(gp) = v;
+    }
   }
 }
 
+template <bool WT = false>
 __device__ __forceinline__ void zero_tile64(double* __restrict__ g, size_t gld) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int u = 0; u < 2048 / DNTH; ++u) {
     const int q = tid + DNTH * u;
     const int row = q >> 5, c2 = q & 31;
-    *reinterpret_cast<d2*>(g + (size_t)row * gld + 2 * c2) = d2{0.0, 0.0};
+    double* gp = g + (size_t)row * gld + 2 * c2;
+    if (WT) {
+      gst<true>(gp, 0.0);
+      gst<true>(gp + 1, 0.0);
+    } else {
+      *reinterpret_cast<d2*>(gp) = d2{0.0, 0.0};
+    }
   }
 }
 

@@ -381,6 +381,7 @@ struct DiagSmem {
 // Lt/Ut: top-left of the block in the particle's L / U buffers (row stride ld);
 // yseg: the block's 128 RHS entries (replaced by z); s2o/szo: 128 partial outputs.
 // ----------------------------------------------------------------------------
+template <bool WT = false>
 __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __restrict__ Ut, size_t ld,
                                           double* __restrict__ yseg, double* __restrict__ s2o,
                                           double* __restrict__ szo, int* __restrict__ info, const DiagSmem& sm,
@@ -404,8 +405,8 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
   DIAG_STAMP(1);
   lds_to_tile64(Lt, ld, t0, LDH, true);
   zero_tile64(Lt + H, ld);
-  lds_to_tile64(Ut, ld, t1, LDH, false);
-  zero_tile64(Ut + H, ld);
+  lds_to_tile64<WT>(Ut, ld, t1, LDH, false);
+  zero_tile64<WT>(Ut + H, ld);
   rows_dot64(sm.z, t1, LDH, sm.y, sm.scratch, false);          // z1 = U11 y1
   cols_partial64(sm.ps2, sm.psz, t1, LDH, sm.z, sm.scratch);   // U11 columns
 
@@ -414,16 +415,16 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
     // no earlier column touches them): L21 = U21 = 0, L22 = U22 = I, z2 = 0 — exactly what the
     // general path computes, without the second 64x64 factor
     zero_tile64(Lt + (size_t)H * ld, ld);
-    zero_tile64(Ut + (size_t)H * ld, ld);
+    zero_tile64<WT>(Ut + (size_t)H * ld, ld);
     for (int i = tid; i < H * H; i += DNTH) {
       const int r = i >> 6, c = i & 63;
       Lt[(size_t)(H + r) * ld + H + c] = (r == c) ? 1.0 : 0.0;
-      Ut[(size_t)(H + r) * ld + H + c] = (r == c) ? 1.0 : 0.0;
+      gst<WT>(&Ut[(size_t)(H + r) * ld + H + c], (r == c) ? 1.0 : 0.0);
     }
     if (tid < T) {
       s2o[tid] = (tid < H) ? sm.ps2[tid] : 1.0;
       szo[tid] = (tid < H) ? sm.psz[tid] : 0.0;
-      yseg[tid] = (tid < H) ? sm.z[tid] : 0.0;
+      gst<WT>(&yseg[tid], (tid < H) ? sm.z[tid] : 0.0);
     }
     if (bad && tid == 0 && *info == 0) *info = 1;
     return;
@@ -435,7 +436,7 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
   __syncthreads();
   Acc<64> acc;
   acc.zero();
-  gemm_lds64<false>(acc, t0, LDH, t1, LDH, qd);
+  gemm_lds64<false, TRI_B_KLEC>(acc, t0, LDH, t1, LDH, qd);  // U11^T is upper triangular
   __syncthreads();
   acc.foreach(qd, [&](int r, int c, double v) {
       t0[r * LDH + c] = v;
@@ -446,15 +447,15 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
   DIAG_STAMP(3);
   // (c) A22 -= L21 L21^T ; y2 -= L21 z1 ; T = L21 U11 (to the U21 slot as scratch)
   acc.zero();
-  gemm_lds64<false>(acc, t0, LDH, t0, LDH, qd);
+  gemm_lds64<false, TRI_C_LOWER>(acc, t0, LDH, t0, LDH, qd);  // factor64 reads the lower triangle only
   rows_dot64(sm.y + H, t0, LDH, sm.z, sm.scratch, true);
   Acc<64> tt;
   tt.zero();
-  gemm_lds64<true>(tt, t0, LDH, t1, LDH, qd);
+  gemm_lds64<true, TRI_B_KGEC>(tt, t0, LDH, t1, LDH, qd);  // U11 is lower triangular
   __syncthreads();
   double* U21 = Ut + (size_t)H * ld;
   const double* A22 = Lt + (size_t)H * ld + H;
-  tt.foreach(qd, [&](int r, int c, double v) { U21[(size_t)r * ld + c] = v; });
+  tt.foreach(qd, [&](int r, int c, double v) { gst<WT>(&U21[(size_t)r * ld + c], v); });
   acc.foreach(qd, [&](int r, int c, double v) { t0[r * LDH + c] = A22[(size_t)r * ld + c] - v; });
   __syncthreads();
 
@@ -464,7 +465,7 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
   __syncthreads();
   DIAG_STAMP(5);
   lds_to_tile64(Lt + (size_t)H * ld + H, ld, t0, LDH, true);
-  lds_to_tile64(Ut + (size_t)H * ld + H, ld, t1, LDH, false);
+  lds_to_tile64<WT>(Ut + (size_t)H * ld + H, ld, t1, LDH, false);
   __syncthreads();
 
   DIAG_STAMP(6);
@@ -472,11 +473,11 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
   tile64_to_lds(t0, LDH, U21, ld);
   __syncthreads();
   acc.zero();
-  gemm_lds64<true>(acc, t1, LDH, t0, LDH, qd);
+  gemm_lds64<true, TRI_A_KLER>(acc, t1, LDH, t0, LDH, qd);  // U22 is lower triangular
   __syncthreads();
   acc.foreach(qd, [&](int r, int c, double v) {
       t0[r * LDH + c] = -v;
-      U21[(size_t)r * ld + c] = -v;
+      gst<WT>(&U21[(size_t)r * ld + c], -v);
     });
   __syncthreads();
 
@@ -490,7 +491,7 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
   if (tid < T) {
     s2o[tid] = sm.ps2[tid];
     szo[tid] = sm.psz[tid];
-    yseg[tid] = sm.z[tid];
+    gst<WT>(&yseg[tid], sm.z[tid]);
   }
   if (bad && tid == 0 && *info == 0) *info = 1;
   DIAG_STAMP(9);
@@ -520,7 +521,8 @@ __device__ __forceinline__ DiagSmem carve_diag(double* base, double* small) {
 __global__ __launch_bounds__(DNTH) void k_diag(int J, int nt, int N, int Npad, double* __restrict__ Lb,
                                                   double* __restrict__ Ub, double* __restrict__ yb,
                                                   double* __restrict__ s2p, double* __restrict__ szp,
-                                                  int* __restrict__ info) {
+                                                  int* __restrict__ info, int* __restrict__ dflag) {
+  if (threadIdx.x == 0) dflag[blockIdx.x] = J;  // a new factorisation: block J published (launches follow in order)
   __shared__ __attribute__((aligned(16))) double tiles[DIAG_BASE];
   __shared__ __attribute__((aligned(16))) double small[DIAG_SMALL];
   const int p = blockIdx.x;
@@ -564,17 +566,35 @@ __host__ __device__ __forceinline__ void step_tile(int b, int P, int ntl, int gr
 }
 
 enum { SPLIT_NONE = 0, SPLIT_ALL = 1, SPLIT_CRIT = 2 };
-enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2 };
+enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2, ROLE_DIAG = 3 };
 
-// Workgroup b of a k_step<SPLIT> launch (grid: P*(nt-1)*S for SPLIT_ALL, P*(nt-1) + P*(S-1)
-// for SPLIT_CRIT, P*(nt-1) otherwise): its particle p, tile w, split index sidx, and whether
-// it runs the whole tile, one depth range (piece sidx of S) of it, or nothing. The kernel and
-// the host-side plan check (gpf_plan_check) both decode through this function.
+// Early diagonal factor (k_step<SPLIT, ED = 1>; the host chooses it for launches that leave
+// workgroup slots idle): launch J >= 1 starts with P extra workgroups that factor diagonal
+// block J (factor128: L_JJ, U_JJ, z_J, the column partials) and publish it through a
+// per-particle flag, while every tile of the launch runs the GEMM part of its work; a tile waits
+// for the flag only before its first use of U_JJ / z_J. The diagonal factor (~55 us on one
+// workgroup) then overlaps the launch's GEMMs instead of closing the previous launch's critical
+// tile (I = J+1) in series. With ED = 0 that tile factors block J+1 itself (fused, as before).
+// k_diag factors block 0 either way.
+
+// Workgroup b of a k_step<SPLIT> launch (grid: [P diagonal workgroups if ed] + P*(nt-1)*S for
+// SPLIT_ALL, P*(nt-1) + P*(S-1) for SPLIT_CRIT, P*(nt-1) otherwise): its particle p, tile w,
+// split index sidx, and whether it factors the diagonal block (ROLE_DIAG, w = -1), runs the whole
+// tile, one depth range (piece sidx of S) of it, or nothing. The kernel and the host-side plan
+// check (gpf_plan_check) both decode through this function.
 template <int SPLIT>
-__host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt, int grp, int S, int& p, int& w,
-                                                    int& sidx) {
+__host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt, int grp, int S, int ed, int& p,
+                                                    int& w, int& sidx) {
   const int tiles = P * (nt - 1);
   sidx = 0;
+  if (ed) {
+    if (b < P) {
+      p = b;
+      w = -1;
+      return ROLE_DIAG;
+    }
+    b -= P;
+  }
   if (SPLIT == SPLIT_ALL) {
     sidx = b / tiles;  // split-major dispatch
     step_tile(b - sidx * tiles, P, nt - 1, grp, p, w);
@@ -738,15 +758,35 @@ __device__ __forceinline__ void split_sum(Acc<T>& acc, const double* pt, int nch
   }
 }
 
+// Consumer side of the early diagonal factor: wait until the launch's diagonal workgroup of this
+// particle has published block J (flag >= J), then an agent-scope acquire (its stores are
+// write-through, factor128<true>, so no L2 write-back fence was needed on its side). The spin is
+// bounded: on timeout (~1 s) info gets bit 2 and the host reports an error instead of the GPU
+// hanging.
+__device__ __forceinline__ void wait_diag(const int* flag, int J, int* info) {
+  if (threadIdx.x == 0) {
+    int spins = 0;
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < J) {
+      __builtin_amdgcn_s_sleep(16);
+      if (++spins > (1 << 21)) {
+        __hip_atomic_fetch_or(info, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
 // Tile w of block column J of particle p (the unit of work of k_step); role from step_decode.
-template <int SPLIT>
+template <int SPLIT, int ED>
 __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt, int Npad, double* __restrict__ Lb,
                                           double* __restrict__ Ub, double* __restrict__ yb,
                                           double* __restrict__ s2p, double* __restrict__ szp,
                                           int* __restrict__ info, int N, const double* __restrict__ x,
                                           const double* __restrict__ ls, int d, int S, int sidx,
                                           double* __restrict__ part, unsigned* __restrict__ cnt, int* sflag,
-                                          double* smem, double* small) {
+                                          const int* __restrict__ dflag, double* smem, double* small) {
   const int tid = threadIdx.x;
   const int nL = nt - 1 - J;
   const size_t ld = (size_t)Npad;
@@ -789,6 +829,7 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
 #endif
     __syncthreads();
     GPF_PHASE(0);
+    if (ED && J > 0) wait_diag(dflag + p, J, info + p);  // U_JJ, z_J
     // L_IJ = C U_JJ^T
     acc.zero();
     step_gemm<false, false, TRI_B_KLEC>(acc, Aij, Npad, Ujj, Npad, T, smem, qd);
@@ -811,7 +852,7 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
       yp[I * T + tid] =
           yp[I * T + tid] - (((scratch[tid] + scratch[T + tid]) + scratch[2 * T + tid]) + scratch[3 * T + tid]);
     GPF_PHASE(3);
-    if (I == J + 1) {  // fused diagonal factor of block J+1 (every reduction of A_II and y_I is done)
+    if (!ED && I == J + 1) {  // fused diagonal factor of block J+1 (A_II, y_I fully reduced)
       __syncthreads();
       const DiagSmem sm = carve_diag(smem, small);
       const size_t poff = ((size_t)p * nt + I) * Npad + (size_t)I * T;
@@ -840,6 +881,7 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
                                               Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T, smem, qd);
     }
     acc.store(qd, Ujk, ld);
+    if (ED) wait_diag(dflag + p, J, info + p);  // U_JJ, z_J (U tiles exist for J > 0 only)
     if (tid < T) zj[tid] = yp[J * T + tid];
     __syncthreads();
     GPF_PHASE(0);
@@ -890,14 +932,14 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
 // tile I = J+1 of each particle (launches that leave slots idle: its S pieces are dispatched
 // first, ahead of the unsplit tiles); SPLIT_NONE carries no split code at all, so its register
 // allocation is that of the plain schedule.
-template <int SPLIT>
+template <int SPLIT, int ED>
 __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int J, int nt, int Npad, double* __restrict__ Lb,
                                                   double* __restrict__ Ub, double* __restrict__ yb,
                                                   double* __restrict__ s2p, double* __restrict__ szp,
                                                   int* __restrict__ info, int P, int grp, int N,
                                                   const double* __restrict__ x, const double* __restrict__ ls,
                                                   int d, int S, double* __restrict__ part,
-                                                  unsigned* __restrict__ cnt) {
+                                                  unsigned* __restrict__ cnt, int* __restrict__ dflag, int ed) {
   const int tid = threadIdx.x;
 #ifdef GPF_WG_TRACE
   if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) {
@@ -912,9 +954,25 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
   __shared__ __attribute__((aligned(16))) double small[STEP_SMALL];
   __shared__ int sflag;
   int p, w, sidx;
-  const int role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, p, w, sidx);
-  step_item<SPLIT>(role, J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, sidx, part, cnt, &sflag, smem,
-                   small);
+  const int role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, p, w, sidx);
+  if (ED && role == ROLE_DIAG) {
+    // diagonal block J of particle p (fully reduced by the previous launches' look-ahead): factor,
+    // then publish to this launch's tiles (write-through stores drained, then the flag)
+    const size_t ld = (size_t)Npad;
+    const size_t off = (size_t)p * ld * ld + (size_t)J * T * ld + (size_t)J * T;
+    const size_t poff = ((size_t)p * nt + J) * Npad + (size_t)J * T;
+#if GPF_DIAG_PRIO
+    __builtin_amdgcn_s_setprio(3);  // the launch's tiles wait for this block
+#endif
+    factor128<true>(Lb + off, Ub + off, ld, yb + (size_t)p * Npad + J * T, s2p + poff, szp + poff, info + p,
+                    carve_diag(smem, small), J * T + H >= N);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(dflag + p, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    step_item<SPLIT, ED>(role, J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, sidx, part, cnt, &sflag,
+                     dflag, smem, small);
+  }
 #ifdef GPF_WG_TRACE
   __syncthreads();
   if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) g_wg_trace[J][blockIdx.x][1] = realtime();

@@ -86,6 +86,7 @@ struct gpf_ctx {
   double* d_sd = nullptr;
   double* d_loss = nullptr;
   int* d_info = nullptr;
+  int* d_flag = nullptr;  // per particle: last diagonal block published in the running launch (early_diag)
   int* d_hist = nullptr;
   // pinned host staging for the per-batch transfers (async DMA, capturable in graphs)
   double* h_ls = nullptr;
@@ -184,6 +185,8 @@ static void free_work(gpf_ctx* c) {
   hipFree(c->d_L); hipFree(c->d_U); hipFree(c->d_yb); hipFree(c->d_s2p); hipFree(c->d_szp);
   hipFree(c->d_ls); hipFree(c->d_mu); hipFree(c->d_sd); hipFree(c->d_loss); hipFree(c->d_info);
   hipFree(c->d_hist);
+  hipFree(c->d_flag);
+  c->d_flag = nullptr;
   hipFree(c->d_part); hipFree(c->d_cnt);
   c->d_part = nullptr;
   c->d_cnt = nullptr;
@@ -226,6 +229,7 @@ static int ensure_work(gpf_ctx* c, int want) {
   GPF_HIP(c, hipMalloc(&c->d_sd, (size_t)cap * np * 8));
   GPF_HIP(c, hipMalloc(&c->d_loss, (size_t)cap * 8));
   GPF_HIP(c, hipMalloc(&c->d_info, (size_t)cap * 4));
+  GPF_HIP(c, hipMalloc(&c->d_flag, (size_t)cap * 4));  // set by k_diag at every factorisation
   GPF_HIP(c, hipMalloc(&c->d_hist, (size_t)cap * (c->K + 1) * 4));
   // on the library stream: the legacy null stream does not order against our non-blocking streams
   GPF_HIP(c, hipMemsetAsync(c->d_hist, 0, (size_t)cap * (c->K + 1) * 4, c->stream));  // k_score re-zeroes what it read
@@ -271,6 +275,19 @@ static int split_k(int tiles, int nt) {
   return S;
 }
 
+// Early diagonal factor (gpf::k_step<SPLIT, 1>, gpf_factor.hip) for factorisations whose launches
+// leave workgroup slots idle: there the launch time is the critical tile's chain, and moving the
+// diagonal factor of block J to the start of launch J, beside the GEMMs, takes it off that chain
+// (config B, N=1024 P=32: 22.3k -> 27.8k evals/s; the single-particle prediction factor 7.1 ->
+// 6.0 ms). Launches with many more tiles than slots are bound by the slot load instead, and
+// their tiles would wait for the flag in the first block columns (config C: -0.5%), so they keep
+// the fused factor. pc: the particles of all concurrent groups. GPF_EARLY_DIAG = 0/1 overrides.
+static bool early_diag(int pc, int nt) {
+  bool on = (long long)pc * (nt - 1) <= 1024;
+  if (const char* s = getenv("GPF_EARLY_DIAG")) on = atoi(s) != 0;
+  return on && nt > 1;
+}
+
 // Critical-tile split of block-column launch J (gpf::SPLIT_CRIT), for launches that leave
 // workgroup slots idle (small N: the launch time is the latency of the tile I = J+1, which runs
 // the depth-128J GEMM, the look-ahead update and the next diagonal factor in sequence): that
@@ -283,7 +300,7 @@ static int split_k(int tiles, int nt) {
 static int split_crit(int pc, int nt, int J, int grp, int S_all) {
   // the last launch (J = nt-1) has no L tiles: its w = 0 is a U tile, which never splits
   if (S_all > 1 || grp > 0 || J == 0 || J >= nt - 1 || nt < 4 || !GPF_KFUSE) return 1;
-  const int slots = 512, tiles = pc * (nt - 1);
+  const int slots = 512, tiles = pc * (nt - 1) + (early_diag(pc, nt) ? pc : 0);  // + the diagonal workgroups
   int S = 4, minch = 16;
   if (const char* s = getenv("GPF_SPLIT_CRIT")) S = std::max(1, std::min(32, atoi(s)));
   if (const char* s = getenv("GPF_SPLIT_CRIT_MIN")) minch = std::max(2, atoi(s));
@@ -340,7 +357,7 @@ static int split_plan(gpf_ctx* c, int pc, int& S, int& Smax) {
 // tile, and where its split-K partial slots and arrival counters start (element offsets into
 // d_part / d_cnt). run_factor launches exactly this list; gpf_plan_check verifies it on the host.
 struct StepLaunch {
-  int J, g, p0, gc, split, S, grp;
+  int J, g, p0, gc, split, S, grp, ed;  // ed: the launch starts with gc diagonal workgroups
   unsigned grid;
   size_t part_off, cnt_off;
 };
@@ -348,6 +365,7 @@ struct StepLaunch {
 static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& out) {
   out.clear();
   const int ng = num_groups(pc, nt);
+  const bool ed = early_diag(pc, nt);
   // block columns interleaved across groups so every stream has work queued early
   for (int J = 0; nt > 1 && J < nt; ++J) {
     for (int g = 0; g < ng; ++g) {
@@ -360,7 +378,8 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
       const int Sc = split_crit(pc, nt, J, l.grp, S);
       l.S = S > 1 ? S : Sc;  // pieces per split tile in this launch
       l.split = S > 1 ? gpf::SPLIT_ALL : Sc > 1 ? gpf::SPLIT_CRIT : gpf::SPLIT_NONE;
-      l.grid = S > 1 ? l.gc * (nt - 1) * S : l.gc * (nt - 1) + l.gc * (Sc - 1);
+      l.ed = (ed && J >= 1) ? 1 : 0;
+      l.grid = (S > 1 ? l.gc * (nt - 1) * S : l.gc * (nt - 1) + l.gc * (Sc - 1)) + (l.ed ? l.gc : 0);
       // one set of partial slots per group: groups run concurrently
       l.part_off = (size_t)l.p0 * (nt - 1) * Smax * T * T;
       l.cnt_off = (size_t)l.p0 * (nt - 1);
@@ -429,7 +448,8 @@ static int run_factor(gpf_ctx* c, int pc) {
     if (rc) return rc;
     // potrf + trtri of the first 128 block: 2/3 T^3 (later blocks are fused into k_step)
     rc = launch_on(c, st, PC_DIAG, (2.0 / 3.0) * t3 * gc, [&] {
-      hipLaunchKernelGGL(gpf::k_diag, dim3(gc), dim3(gpf::DNTH), 0, st, 0, nt, N, Np, Lg, Ug, yg, s2g, szg, ig);
+      hipLaunchKernelGGL(gpf::k_diag, dim3(gc), dim3(gpf::DNTH), 0, st, 0, nt, N, Np, Lg, Ug, yg, s2g, szg, ig,
+                         c->d_flag + p0);
     });
     if (rc) return rc;
     total += (2.0 / 3.0) * t3 * gc;
@@ -437,20 +457,24 @@ static int run_factor(gpf_ctx* c, int pc) {
   // block-column launches (split-K for launches with few tiles, planned above)
   std::vector<StepLaunch> plan;
   step_plan(pc, nt, S, Smax, plan);
+  // one variant for the whole factorisation: with the early diagonal factor, launch 0 (no
+  // diagonal workgroups) must not factor block 1 at the end of its critical tile either
+  const bool ed = early_diag(pc, nt);
   for (const StepLaunch& l : plan) {
     const double fl = step_flops(l.J);
     const int p0 = l.p0, gc = l.gc;
     hipStream_t st = (ng > 1) ? c->sub[l.g] : c->stream;
     double* partg = l.S > 1 ? c->d_part + l.part_off : nullptr;
     unsigned* cntg = l.S > 1 ? c->d_cnt + l.cnt_off : nullptr;
-    const auto kern = l.split == gpf::SPLIT_ALL    ? gpf::k_step<gpf::SPLIT_ALL>
-                      : l.split == gpf::SPLIT_CRIT ? gpf::k_step<gpf::SPLIT_CRIT>
-                                                   : gpf::k_step<gpf::SPLIT_NONE>;
+    // ED = 0 for launch 0 (k_diag factors block 0) and when the fused factor is chosen
+    const auto kern = l.split == gpf::SPLIT_ALL    ? (ed ? gpf::k_step<gpf::SPLIT_ALL, 1> : gpf::k_step<gpf::SPLIT_ALL, 0>)
+                      : l.split == gpf::SPLIT_CRIT ? (ed ? gpf::k_step<gpf::SPLIT_CRIT, 1> : gpf::k_step<gpf::SPLIT_CRIT, 0>)
+                                                   : (ed ? gpf::k_step<gpf::SPLIT_NONE, 1> : gpf::k_step<gpf::SPLIT_NONE, 0>);
     const int rc = launch_on(c, st, PC_PANEL, fl * gc, [&] {
       hipLaunchKernelGGL(kern, dim3(l.grid), dim3(gpf::STEP_NTH), 0, st, l.J, nt, Np, c->d_L + (size_t)p0 * ld * ld,
                          c->d_U + (size_t)p0 * ld * ld, c->d_yb + (size_t)p0 * ld, c->d_s2p + (size_t)p0 * nt * ld,
                          c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc, l.grp, N, c->d_x,
-                         c->d_ls + (size_t)p0 * c->d, c->d, l.S, partg, cntg);
+                         c->d_ls + (size_t)p0 * c->d, c->d, l.S, partg, cntg, c->d_flag + p0, l.ed);
     });
     if (rc) return rc;
     total += fl * gc;
@@ -705,6 +729,10 @@ int gpf_eval_batch(gpf_ctx* c, const double* ls, int P, double* loss, double* mu
       GPF_HIP(c, hipStreamSynchronize(c->stream));
       c->evals += (double)act.size();
       for (size_t q = 0; q < act.size(); ++q) {
+        if (c->h_info[q] & 2) {
+          c->err = "k_step: diagonal-block hand-off timed out";
+          return GPF_HIP_ERROR;
+        }
         if (c->h_info[q] != 0) {
           if (bad_idx) *bad_idx = act[q];
           c->err = "Matrix is not positive definite";
@@ -734,6 +762,10 @@ int gpf_eval_batch(gpf_ctx* c, const double* ls, int P, double* loss, double* mu
     c->evals += pc;
     for (int q = 0; q < pc; ++q) {
       const int p = act[s + q];
+      if (c->h_info[q] & 2) {
+        c->err = "k_step: diagonal-block hand-off timed out";
+        return GPF_HIP_ERROR;
+      }
       if (c->h_info[q] != 0) {
         if (bad_idx) *bad_idx = p;
         c->err = "Matrix is not positive definite";
@@ -764,6 +796,10 @@ static int factor_single(gpf_ctx* c, const double* ls, double** alpha_out) {
   int info = 0;
   GPF_HIP(c, hipMemcpyAsync(&info, c->d_info, 4, hipMemcpyDeviceToHost, c->stream));
   GPF_HIP(c, hipStreamSynchronize(c->stream));
+  if (info & 2) {
+    c->err = "k_step: diagonal-block hand-off timed out";
+    return GPF_HIP_ERROR;
+  }
   if (info != 0) {
     c->err = "Matrix is not positive definite";
     return GPF_NOT_PD;
@@ -920,7 +956,8 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
   // be disjoint (within a group the launches are ordered on its stream)
   std::vector<size_t> plo(MAX_GROUPS, SIZE_MAX), phi(MAX_GROUPS, 0), clo(MAX_GROUPS, SIZE_MAX), chi(MAX_GROUPS, 0);
   long long wgs = 0, whole_tiles = 0, split_tiles = 0;
-  std::vector<int> whole, piece;
+  std::vector<int> whole, piece, diag;
+  long long diag_wgs = 0;
   if ((int)plan.size() != (nt > 1 ? nt * ng : 0)) return plan_fail(msg, msg_len, "plan has %d launches, want %d",
                                                               (int)plan.size(), nt * ng);
   for (const StepLaunch& l : plan) {
@@ -931,11 +968,19 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     const int tiles = l.gc * ntl;
     whole.assign((size_t)tiles, 0);
     piece.assign((size_t)tiles * l.S, 0);
+    diag.assign((size_t)l.gc, 0);
     for (unsigned b = 0; b < l.grid; ++b) {
       int p = -1, w = -1, sidx = -1;
-      const int role = l.split == gpf::SPLIT_ALL    ? gpf::step_decode<gpf::SPLIT_ALL>(b, l.J, l.gc, nt, l.grp, l.S, p, w, sidx)
-                       : l.split == gpf::SPLIT_CRIT ? gpf::step_decode<gpf::SPLIT_CRIT>(b, l.J, l.gc, nt, l.grp, l.S, p, w, sidx)
-                                                    : gpf::step_decode<gpf::SPLIT_NONE>(b, l.J, l.gc, nt, l.grp, l.S, p, w, sidx);
+      const int role =
+          l.split == gpf::SPLIT_ALL    ? gpf::step_decode<gpf::SPLIT_ALL>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, p, w, sidx)
+          : l.split == gpf::SPLIT_CRIT ? gpf::step_decode<gpf::SPLIT_CRIT>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, p, w, sidx)
+                                       : gpf::step_decode<gpf::SPLIT_NONE>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, p, w, sidx);
+      if (role == gpf::ROLE_DIAG) {  // one diagonal workgroup per particle, ahead of every tile of the launch
+        if (!l.ed || p < 0 || p >= l.gc || (unsigned)p != b || diag[p]++)
+          return plan_fail(msg, msg_len, "J=%d block %u: misplaced or duplicate diagonal workgroup (p=%d)", l.J, b, p);
+        ++wgs;
+        continue;
+      }
       if (p < 0 || p >= l.gc || w < 0 || w >= ntl || sidx < 0 || sidx >= l.S)
         return plan_fail(msg, msg_len, "J=%d block %u decodes out of range (p=%d w=%d)", l.J, b, p, w);
       const int t = p * ntl + w;
@@ -953,6 +998,10 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
         chi[l.g] = std::max(chi[l.g], ci + 1);
       }
       ++wgs;
+    }
+    for (int q = 0; q < l.gc; ++q) {
+      if (diag[q] != l.ed) return plan_fail(msg, msg_len, "J=%d particle %d: %d diagonal workgroups", l.J, q, diag[q]);
+      diag_wgs += diag[q];
     }
     for (int t = 0; t < tiles; ++t) {
       int np = 0;
@@ -980,6 +1029,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     stats[4] = S;
     stats[5] = Smax;
     stats[6] = ng;
+    stats[7] = diag_wgs;
   }
   return GPF_OK;
 }

@@ -197,9 +197,11 @@ const char* gpf_build_info(void);
  * exactly once (one whole-tile workgroup, or all S depth pieces exactly once, whose S arrivals
  * on a zeroed counter elect exactly one finisher), that pieces stay inside the split-K buffers,
  * and that concurrent particle groups never share partial slots or counters.
- * stats (nullable, 7 entries): launches, workgroups, whole tiles, split tiles, S (all-tile
- * split factor), largest split factor, particle groups. Returns GPF_OK, or GPF_BAD_ARG with a
- * description of the first violation in msg. */
+ * With the early diagonal factor it also checks that every launch J >= 1 starts with exactly one
+ * diagonal workgroup per particle, ahead of all tiles (and launch 0 with none).
+ * stats (nullable, 8 entries): launches, workgroups, whole tiles, split tiles, S (all-tile
+ * split factor), largest split factor, particle groups, diagonal workgroups. Returns GPF_OK, or
+ * GPF_BAD_ARG with a description of the first violation in msg. */
 int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len);
 
 /* Self-test of the f64 MFMA fragment layout: C = A(16x4) B(4x16) on device,

@@ -1,0 +1,82 @@
+"""Critical-tile timeline per block column (diagnostic build libgpfit_trace.so, -DGPF_WG_TRACE).
+
+For each k_step launch J of the last factorisation: the launch span (first workgroup start to
+last end), and for particle 0's tile w = 0 (I = J+1: the GEMM, TRMM, SYRK, dot and the fused
+diagonal factor of the next block) its workgroups' start and GEMM end, then the finisher's
+phase ends (TRMM, SYRK, dot) and its end (after factor128), all relative to the launch start,
+in microseconds. MODE=predict: GP prediction at N (single particle, all tiles split);
+MODE=eval: a batch of P particles (config B: N=1024 P=32)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["GPFIT_LIB"] = os.path.join(ROOT, "gaussian-process_amd", "libgpfit_trace.so")
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gaussian-process_amd")]
+import gpfit  # noqa: E402
+from gpfit import _lib  # noqa: E402
+
+probe = ctypes.CDLL(os.environ["GPFIT_LIB"])
+mode = os.environ.get("MODE", "predict")
+N = int(os.environ.get("N", 4096 if mode == "predict" else 1024))
+d = int(os.environ.get("D", 3 if mode == "predict" else 2))
+P = int(os.environ.get("P", 1 if mode == "predict" else 32))
+T = 128
+nt = -(-N // T)
+rng = np.random.default_rng(1)
+x = rng.uniform(size=(d, N))
+y = np.sin(2 * np.pi * x).sum(0) + 0.1 * rng.standard_normal(N)
+e = np.full(N, 0.1)
+ctx = gpfit.Context(0)
+ctx.set_data(x, y, e)
+if mode == "predict":
+    xf = rng.uniform(size=(d, 2000))
+    for _ in range(2):
+        ctx.predict(np.full(d, 0.3), xf)
+else:
+    s = np.linspace(0.001, 3, 1000)
+    lo, hi = np.full(d, 1e-6), np.full(d, 2.0)
+    ctx.set_grid(s, np.clip(s / 3, 0, 1), lo, hi)
+    for _ in range(2):
+        ctx.eval_batch(rng.uniform(0.05, 0.6, size=(P, d)))
+ctx.synchronize()
+W = 4096
+tr = np.zeros((nt, W, 3), dtype=np.uint64)
+ph = np.zeros((nt, W, 4), dtype=np.uint64)
+u64p = ctypes.POINTER(ctypes.c_ulonglong)
+assert probe.gpf_debug_wg_trace(tr.ctypes.data_as(u64p), nt, W) == 0
+assert probe.gpf_debug_wg_phase(ph.ctypes.data_as(u64p), nt, W) == 0
+tot = 0.0
+print("J   span   | w0: pieces start..gemm-end (max)  finisher: trmm   syrk    dot    end   (us from launch start)")
+for J in range(nt - 1):
+    st, en = tr[J, :, 0].astype(np.int64), tr[J, :, 1].astype(np.int64)
+    live = (st > 0) & (en >= st)
+    # this launch's workgroups: those that started after the previous launch's first start
+    if not live.any():
+        continue
+    t0 = st[live].min()
+    # discard stale entries of an older, longer launch with the same J
+    live &= st >= t0
+    span = (en[live].max() - t0) * 1e-2
+    tot += span
+    # tile w = 0 of particle 0: block ids with (p, w) = (0, 0) in particle-fastest order, plus pieces
+    if mode == "predict":  # split-all: piece s of tile w at b = s * (nt - 1) + w
+        ids = [b for b in range(W) if live[b] and b % (nt - 1) == 0]
+    else:  # critical-tile split (csrc/gpfit_api.hip split_crit): pieces of particle 0 at b = s * P
+        S = 1 if (J == 0 or J >= nt - 1 or nt < 4) else min(4, max(1, J * T // 16 // 16))
+        while S > 1 and P * (nt - 1) + P * (S - 1) > 512:
+            S -= 1
+        ids = [s * P for s in range(S) if live[s * P]]
+    if not ids:
+        print(f"{J:2d} {span:7.1f}")
+        continue
+    p0 = ph[J].astype(np.int64)
+    fin = max(ids, key=lambda b: en[b])
+    g_end = max(p0[b, 0] for b in ids if p0[b, 0] >= t0) if any(p0[b, 0] >= t0 for b in ids) else 0
+    rel = lambda v: (v - t0) * 1e-2 if v >= t0 else float("nan")  # noqa: E731
+    print(f"{J:2d} {span:7.1f}   | {len(ids):2d} pieces {rel(min(st[b] for b in ids)):6.1f}..{rel(g_end):6.1f}"
+          f"   {rel(p0[fin, 1]):6.1f} {rel(p0[fin, 2]):6.1f} {rel(p0[fin, 3]):6.1f} {rel(en[fin]):6.1f}")
+print(f"sum of launch spans {tot:.1f} us")
+ctx.close()

@@ -543,3 +543,36 @@ def test_configE_share_two_groups_vs_reference(ctx, monkeypatch):
     slots = [3, 12]
     P[slots] = fx["P"]
     _reference_share(ctx, monkeypatch, fx, P, slots)
+
+
+@pytest.mark.parametrize("N,d,P", [(1000, 2, 12), (2049, 3, 5), (4096, 3, 1)])
+def test_early_diagonal_factor_matches_fused(ctx, monkeypatch, N, d, P):
+    """The early diagonal factor (k_step<SPLIT, 1>: block J factored by extra workgroups at the
+    start of launch J and handed to the tiles through a flag) against the fused factor at the end
+    of the previous launch's critical tile: the same arithmetic, so bitwise equal scores, mean
+    and sd, on the critical-split (N=1000), unsplit and all-tile-split (one particle) paths; and
+    the factor itself bitwise equal for the prediction path."""
+    rng = np.random.default_rng(N + P)
+    x = rng.uniform(size=(d, N))
+    y = np.sin(5 * x[0]) + 0.1 * rng.standard_normal(N)
+    e = rng.uniform(0.05, 0.2, size=N)
+    s, ex = ref_cpu.sigma_grid()
+    lo, hi = ref_cpu.search_bounds(x)
+    ctx.set_data(x, y, e)
+    ctx.set_grid(s, ex, lo, hi)
+    Q = rng.uniform(0.1, 0.5, size=(P, d))
+    out = {}
+    for ed in ("0", "1"):
+        monkeypatch.setenv("GPF_EARLY_DIAG", ed)
+        out[ed] = ctx.eval_batch(Q, want_mu_sd=True)
+        if P == 1:
+            out[ed + "f"] = ctx.debug_factor(Q[0])
+    monkeypatch.delenv("GPF_EARLY_DIAG")
+    for a, b in zip(out["0"], out["1"]):
+        np.testing.assert_array_equal(a, b)
+    if P == 1:
+        for a, b in zip(out["0f"], out["1f"]):
+            np.testing.assert_array_equal(np.tril(a) if a.ndim == 2 else a, np.tril(b) if b.ndim == 2 else b)
+    mo, so = ref_cpu.GP_train_identity(x, y, e, Q[0]) if N <= 2049 else (None, None)
+    if mo is not None:
+        assert _rel(out["1"][1][0], mo) < RTOL_MU_SD and _rel(out["1"][2][0], so) < RTOL_MU_SD
