@@ -25,7 +25,8 @@ constexpr int BT = 64;  // covariance build tile
 __global__ __launch_bounds__(NTHR) void k_build_cov(int N, int Npad, int d, const double* __restrict__ x,
                                                     const double* __restrict__ y, const double* __restrict__ e,
                                                     const double* __restrict__ ls, double* __restrict__ Lb,
-                                                    double* __restrict__ yb, int* __restrict__ info, int diag_only) {
+                                                    double* __restrict__ yb, int* __restrict__ info, int diag_only,
+                                                    int* __restrict__ dflag) {
   __shared__ double ai[DMAX][BT];
   __shared__ double aj[DMAX][BT];
   __shared__ double ni[BT], nj[BT];
@@ -45,7 +46,10 @@ __global__ __launch_bounds__(NTHR) void k_build_cov(int N, int Npad, int d, cons
     bj = idx - bi * (bi + 1) / 2;
   }
   const double* lp = ls + (size_t)p * d;
-  if (idx == 0 && tid == 0) info[p] = 0;  // the factorisation kernels only ever set it
+  if (idx == 0 && tid == 0) {
+    info[p] = 0;  // the factorisation kernels only ever set it
+    dflag[p] = -1;  // no diagonal block published yet (early diagonal factor, k_step)
+  }
 
   if (tid < 128) {
     const int t = tid & 63;

@@ -569,13 +569,13 @@ enum { SPLIT_NONE = 0, SPLIT_ALL = 1, SPLIT_CRIT = 2 };
 enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2, ROLE_DIAG = 3 };
 
 // Early diagonal factor (k_step<SPLIT, ED = 1>; the host chooses it for launches that leave
-// workgroup slots idle): launch J >= 1 starts with P extra workgroups that factor diagonal
+// workgroup slots idle): launch J starts with P extra workgroups that factor diagonal
 // block J (factor128: L_JJ, U_JJ, z_J, the column partials) and publish it through a
 // per-particle flag, while every tile of the launch runs the GEMM part of its work; a tile waits
 // for the flag only before its first use of U_JJ / z_J. The diagonal factor (~55 us on one
 // workgroup) then overlaps the launch's GEMMs instead of closing the previous launch's critical
-// tile (I = J+1) in series. With ED = 0 that tile factors block J+1 itself (fused, as before).
-// k_diag factors block 0 either way.
+// tile (I = J+1) in series. Launch 0 factors block 0 the same way (k_build_cov resets the flags
+// to -1). With ED = 0 the critical tile factors block J+1 itself (fused) and k_diag block 0.
 
 // Workgroup b of a k_step<SPLIT> launch (grid: [P diagonal workgroups if ed] + P*(nt-1)*S for
 // SPLIT_ALL, P*(nt-1) + P*(S-1) for SPLIT_CRIT, P*(nt-1) otherwise): its particle p, tile w,
@@ -710,45 +710,60 @@ __device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, con
 
 // ----------------------------------------------------------------------------
 // Split-K for launches with few tiles (a single particle: the prediction path, or small
-// swarms): the streamed GEMM of a tile is cut into S depth ranges, one workgroup each; every
-// workgroup writes its partial product to its slot with write-through (sc1) stores, drains
-// them, takes a ticket, and the last one to arrive (agent-scope acquire; no release fence: its
-// L2 write-back stalled on every dirty line of the XCD, ~10-100 us per piece here) sums the
-// partials in slot order (deterministic) and carries on with the rest of the tile. The
-// counter is reset by that last workgroup for the next launch.
+// swarms): the streamed GEMM of a tile is cut into S depth ranges, one workgroup ("piece")
+// each, and the S partial products are summed by a binary tree of hand-offs: at level l the
+// pieces pair up by node (c = s >> l, sibling c ^ 1); each stores its node sum to the node's
+// slot, takes a ticket on the pair's counter, and the second to arrive adds the sibling's slot
+// and carries the pair up; the last one standing holds the whole sum in its accumulators and
+// finishes the tile. Per chain that is log2(S) partial reads instead of S (the prediction's
+// 16-way split: 4 instead of 16, each a latency-bound 128 KiB read). IEEE addition commutes, so
+// a node's sum does not depend on which sibling arrived last: results are deterministic.
+// Hand-off (the memory-model argument): node sums are stored write-through (agent-scope relaxed
+// atomic stores, `sc1`: the line goes to memory, no L2 write-back fence, which on gfx950 would
+// write back every dirty line of the XCD's L2 — ~10-100 us here), every wave drains them
+// (s_waitcnt vmcnt(0)) before the barrier that precedes the ticket, and the second arriver does
+// an agent-scope acquire (L1/L2 invalidate) before reading the sibling's slot, which may have
+// been written from another XCD. The counter is reset by the second arriver for the next launch.
+// seed(acc) (SEEDED: piece 0 only) starts piece 0's accumulator instead of zero: the L tiles seed
+// it with their covariance tile A_IJ, so the finisher does not compute it after the pieces, on
+// the critical path.
 // ----------------------------------------------------------------------------
-template <bool NN, bool NEG>
+constexpr int SPLIT_CNT = 80;  // arrival counters per split tile: node (level l < 5, pair k < 16) at l * 16 + k
+
+template <bool NN, bool NEG, bool SEEDED = false, typename Seed>
 __device__ bool split_part(Acc<T>& acc, const double* Ap, int lda, const double* Bp, int ldb, int nch, int S,
                            int s, double* __restrict__ pt, unsigned* __restrict__ ct, double* smem,
-                           const Quad<T>& qd, int* flag) {
+                           const Quad<T>& qd, int* flag, Seed seed) {
   const int c0 = s * nch / S, c1 = (s + 1) * nch / S;
-  if (c1 > c0) {
+  if (SEEDED && s == 0)
+    seed(acc);
+  else
     acc.zero();
-    gemm_stream_dl<NN, NEG>(acc, Ap + (size_t)c0 * DL_KC, lda, NN ? Bp + (size_t)c0 * DL_KC * ldb : Bp + (size_t)c0 * DL_KC,
-                            ldb, (c1 - c0) * DL_KC, smem, qd);
-    acc.store_wt(qd, pt + (size_t)s * T * T, T);  // write-through: no release (L2 write-back) fence
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its partial before the ticket
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned old = __hip_atomic_fetch_add(ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == (unsigned)(S - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(ct, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (c1 > c0)
+    gemm_stream_dl<NN, NEG>(acc, Ap + (size_t)c0 * DL_KC, lda,
+                            NN ? Bp + (size_t)c0 * DL_KC * ldb : Bp + (size_t)c0 * DL_KC, ldb, (c1 - c0) * DL_KC,
+                            smem, qd);
+  for (int l = 0; (1 << l) < S; ++l) {
+    const int c = s >> l, sib = c ^ 1;
+    if ((sib << l) >= S) continue;  // no sibling range at this level: go up alone
+    acc.store_wt(qd, pt + (size_t)(c << l) * T * T, T);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its part of the node sum
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned* cn = ct + l * 16 + (c >> 1);
+      const unsigned old = __hip_atomic_fetch_add(cn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int second = old == 1u;
+      if (second) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(cn, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      *flag = second;
     }
-    *flag = last;
-  }
-  __syncthreads();
-  return *flag != 0;
-}
-
-// acc += the non-empty partials, in slot order
-__device__ __forceinline__ void split_sum(Acc<T>& acc, const double* pt, int nch, int S, const Quad<T>& qd) {
-  for (int s = 0; s < S; ++s) {
-    if ((s + 1) * nch / S == s * nch / S) continue;
-    const double* p0 = launder(pt + (size_t)s * T * T + (size_t)(qd.rb + (qd.lane >> 4)) * T + qd.cb + (qd.lane & 15));
+    __syncthreads();
+    if (!*flag) return false;  // the sibling carries the pair on
+    const double* p0 =
+        launder(pt + (size_t)(sib << l) * T * T + (size_t)(qd.rb + (qd.lane >> 4)) * T + qd.cb + (qd.lane & 15));
 #pragma unroll
     for (int mi = 0; mi < Acc<T>::MBR; ++mi)
 #pragma unroll
@@ -756,6 +771,7 @@ __device__ __forceinline__ void split_sum(Acc<T>& acc, const double* pt, int nch
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc.v[mi][ni][r] = acc.v[mi][ni][r] + p0[(mi * 16 + 4 * r) * T + ni * 16];
   }
+  return true;
 }
 
 // Consumer side of the early diagonal factor: wait until the launch's diagonal workgroup of this
@@ -809,11 +825,12 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
     if (SPLIT != SPLIT_NONE && role == ROLE_PIECE) {
       // split-K: partial GEMMs, the last workgroup to arrive finishes the tile
       double* pt = part + (size_t)(p * (nt - 1) + w) * S * T * T;
-      if (!split_part<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, J * T / DL_KC, S,
-                                   sidx, pt, cnt + p * (nt - 1) + w, smem, qd, sflag))
-        return;
-      cov_tile_acc(acc, qd, x, ls + (size_t)p * d, d, N, I, J, smem);
-      split_sum(acc, pt, J * T / DL_KC, S, qd);
+      // piece 0 seeds its partial with the covariance tile A_IJ (the unsplit path's accumulator seed)
+      if (!split_part<false, true, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad,
+                                         J * T / DL_KC, S, sidx, pt, cnt + (size_t)(p * (nt - 1) + w) * SPLIT_CNT, smem,
+                                         qd, sflag,
+                                         [&](Acc<T>& a) { cov_tile_acc(a, qd, x, ls + (size_t)p * d, d, N, I, J, smem); }))
+        return;  // (the finisher's accumulators hold A_IJ - L_I,<J L_J,<J^T)
     } else {
       cov_tile_acc(acc, qd, x, ls + (size_t)p * d, d, N, I, J, smem);
       if (J > 0)
@@ -829,7 +846,7 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
 #endif
     __syncthreads();
     GPF_PHASE(0);
-    if (ED && J > 0) wait_diag(dflag + p, J, info + p);  // U_JJ, z_J
+    if (ED) wait_diag(dflag + p, J, info + p);  // U_JJ, z_J (block 0 too: launch 0 has diagonal workgroups)
     // L_IJ = C U_JJ^T
     acc.zero();
     step_gemm<false, false, TRI_B_KLEC>(acc, Aij, Npad, Ujj, Npad, T, smem, qd);
@@ -869,12 +886,10 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
     // W = L_J,[K,J) U_[K,J),K, parked in the U_JK slot
     if (SPLIT == SPLIT_ALL && role == ROLE_PIECE) {  // split-K (the triangular first block runs dense: its upper part holds zeros)
       double* pt = part + (size_t)(p * (nt - 1) + w) * S * T * T;
-      if (!split_part<true, false>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
+      if (!split_part<true, false, false>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
                                    Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T / DL_KC, S, sidx, pt,
-                                   cnt + p * (nt - 1) + w, smem, qd, sflag))
+                                   cnt + (size_t)(p * (nt - 1) + w) * SPLIT_CNT, smem, qd, sflag, [](Acc<T>&) {}))
         return;
-      acc.zero();
-      split_sum(acc, pt, (J - K) * T / DL_KC, S, qd);
     } else {
       acc.zero();
       step_gemm<true, false, TRI_B_KGEC>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,

@@ -229,7 +229,7 @@ static int ensure_work(gpf_ctx* c, int want) {
   GPF_HIP(c, hipMalloc(&c->d_sd, (size_t)cap * np * 8));
   GPF_HIP(c, hipMalloc(&c->d_loss, (size_t)cap * 8));
   GPF_HIP(c, hipMalloc(&c->d_info, (size_t)cap * 4));
-  GPF_HIP(c, hipMalloc(&c->d_flag, (size_t)cap * 4));  // set by k_diag at every factorisation
+  GPF_HIP(c, hipMalloc(&c->d_flag, (size_t)cap * 4));  // reset by k_build_cov at every factorisation
   GPF_HIP(c, hipMalloc(&c->d_hist, (size_t)cap * (c->K + 1) * 4));
   // on the library stream: the legacy null stream does not order against our non-blocking streams
   GPF_HIP(c, hipMemsetAsync(c->d_hist, 0, (size_t)cap * (c->K + 1) * 4, c->stream));  // k_score re-zeroes what it read
@@ -278,12 +278,13 @@ static int split_k(int tiles, int nt) {
 // Early diagonal factor (gpf::k_step<SPLIT, 1>, gpf_factor.hip) for factorisations whose launches
 // leave workgroup slots idle: there the launch time is the critical tile's chain, and moving the
 // diagonal factor of block J to the start of launch J, beside the GEMMs, takes it off that chain
-// (config B, N=1024 P=32: 22.3k -> 27.8k evals/s; the single-particle prediction factor 7.1 ->
-// 6.0 ms). Launches with many more tiles than slots are bound by the slot load instead, and
-// their tiles would wait for the flag in the first block columns (config C: -0.5%), so they keep
-// the fused factor. pc: the particles of all concurrent groups. GPF_EARLY_DIAG = 0/1 overrides.
+// (same-box A/B, gpurun_out r2i: config B, N=1024 P=32, 23.1k -> 29.2k evals/s; N=2048 P=32
+// +5%; the single-particle prediction factor 7.1 -> 6.0 ms). Launches with more tiles than
+// slots are bound by the slot load instead, and their tiles would wait for the flag in the first
+// block columns (config C -0.7%, config D's 32-particle share -0.3%, E neutral), so they keep the
+// fused factor. pc: the particles of all concurrent groups. GPF_EARLY_DIAG = 0/1 overrides.
 static bool early_diag(int pc, int nt) {
-  bool on = (long long)pc * (nt - 1) <= 1024;
+  bool on = (long long)pc * (nt - 1) <= 512;
   if (const char* s = getenv("GPF_EARLY_DIAG")) on = atoi(s) != 0;
   return on && nt > 1;
 }
@@ -311,7 +312,7 @@ static int split_crit(int pc, int nt, int J, int grp, int S_all) {
 }
 
 static int ensure_split(gpf_ctx* c, int tiles, int S) {
-  const size_t pb = (size_t)tiles * S * T * T * 8, cb = (size_t)tiles * 4;
+  const size_t pb = (size_t)tiles * S * T * T * 8, cb = (size_t)tiles * gpf::SPLIT_CNT * 4;
   if (pb > c->part_cap) {
     clear_graphs(c);  // captured graphs hold the old pointers
     hipFree(c->d_part);
@@ -378,20 +379,22 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
       const int Sc = split_crit(pc, nt, J, l.grp, S);
       l.S = S > 1 ? S : Sc;  // pieces per split tile in this launch
       l.split = S > 1 ? gpf::SPLIT_ALL : Sc > 1 ? gpf::SPLIT_CRIT : gpf::SPLIT_NONE;
-      l.ed = (ed && J >= 1) ? 1 : 0;
+      l.ed = ed ? 1 : 0;
       l.grid = (S > 1 ? l.gc * (nt - 1) * S : l.gc * (nt - 1) + l.gc * (Sc - 1)) + (l.ed ? l.gc : 0);
       // one set of partial slots per group: groups run concurrently
       l.part_off = (size_t)l.p0 * (nt - 1) * Smax * T * T;
-      l.cnt_off = (size_t)l.p0 * (nt - 1);
+      l.cnt_off = (size_t)l.p0 * (nt - 1) * gpf::SPLIT_CNT;
       out.push_back(l);
     }
   }
 }
 
 // Factorise `pc` particles whose length scales are already in d_ls, in particle
-// groups on their own streams: per group the K build (lower 64x64 tiles), the first
-// diagonal block (k_diag), then one k_step per 128-wide block column (each also
-// factors the next diagonal block). Joins back into c->stream.
+// groups on their own streams: per group the K build (the 128-wide diagonal blocks), then one
+// k_step per 128-wide block column. With the fused diagonal factor (early_diag false) k_diag
+// factors block 0 first and each launch J factors block J+1 at the end of its critical tile;
+// with the early diagonal factor launch J itself starts with the factor of block J. Joins back
+// into c->stream.
 static int run_factor(gpf_ctx* c, int pc) {
   const int nt = c->nt, Np = (int)c->Npad, N = (int)c->N;
   const double Tf = (double)T, t3 = Tf * Tf * Tf;
@@ -402,14 +405,15 @@ static int run_factor(gpf_ctx* c, int pc) {
   // algorithmic flops of block-column launch J per particle, potrf + trtri (2/3 N^3) formulation:
   //   L tile: depth-128J GEMM 2 T^3 J + triangular multiply T^3 + look-ahead syrk share T^3
   //   U tile: depth-128(J-K) GEMM with a triangular factor 2 T^3 (J-K) - T^3 + triangular multiply T^3
-  //   fused diagonal block J+1: 2/3 T^3
+  //   diagonal block: 2/3 T^3 (block J+1 fused at the end of launch J, or block J early in it)
+  const bool ed = early_diag(pc, nt);
   auto step_flops = [&](int J) {
     double fl = 0.0;
     for (int w = 0; w < nt - 1; ++w) {
       if (w < nt - 1 - J) fl += 2.0 * t3 * J + 2.0 * t3;
       else fl += 2.0 * t3 * (J - (w - (nt - 1 - J)));
     }
-    if (J + 1 < nt) fl += (2.0 / 3.0) * t3;
+    if (ed || J + 1 < nt) fl += (2.0 / 3.0) * t3;
     return fl;
   };
   // Split-K plan first: a (re)allocation of the arrival counters queues their zeroing memset on
@@ -443,9 +447,10 @@ static int run_factor(gpf_ctx* c, int pc) {
     const int nbuild = (GPF_KFUSE && nt > 1) ? 3 * nt : ntri;
     int rc = launch_on(c, st, PC_BUILD, 8.0 * nbuild * BT * BT * (double)gc, [&] {
       hipLaunchKernelGGL(gpf::k_build_cov, dim3(nbuild, gc), dim3(NTHR), 0, st, N, Np, c->d, c->d_x, c->d_y, c->d_e,
-                         lsg, Lg, yg, ig, (int)(nbuild != ntri));
+                         lsg, Lg, yg, ig, (int)(nbuild != ntri), c->d_flag + p0);
     });
     if (rc) return rc;
+    if (ed) continue;  // block 0 is factored by launch 0's diagonal workgroups
     // potrf + trtri of the first 128 block: 2/3 T^3 (later blocks are fused into k_step)
     rc = launch_on(c, st, PC_DIAG, (2.0 / 3.0) * t3 * gc, [&] {
       hipLaunchKernelGGL(gpf::k_diag, dim3(gc), dim3(gpf::DNTH), 0, st, 0, nt, N, Np, Lg, Ug, yg, s2g, szg, ig,
@@ -457,16 +462,12 @@ static int run_factor(gpf_ctx* c, int pc) {
   // block-column launches (split-K for launches with few tiles, planned above)
   std::vector<StepLaunch> plan;
   step_plan(pc, nt, S, Smax, plan);
-  // one variant for the whole factorisation: with the early diagonal factor, launch 0 (no
-  // diagonal workgroups) must not factor block 1 at the end of its critical tile either
-  const bool ed = early_diag(pc, nt);
   for (const StepLaunch& l : plan) {
     const double fl = step_flops(l.J);
     const int p0 = l.p0, gc = l.gc;
     hipStream_t st = (ng > 1) ? c->sub[l.g] : c->stream;
     double* partg = l.S > 1 ? c->d_part + l.part_off : nullptr;
     unsigned* cntg = l.S > 1 ? c->d_cnt + l.cnt_off : nullptr;
-    // ED = 0 for launch 0 (k_diag factors block 0) and when the fused factor is chosen
     const auto kern = l.split == gpf::SPLIT_ALL    ? (ed ? gpf::k_step<gpf::SPLIT_ALL, 1> : gpf::k_step<gpf::SPLIT_ALL, 0>)
                       : l.split == gpf::SPLIT_CRIT ? (ed ? gpf::k_step<gpf::SPLIT_CRIT, 1> : gpf::k_step<gpf::SPLIT_CRIT, 0>)
                                                    : (ed ? gpf::k_step<gpf::SPLIT_NONE, 1> : gpf::k_step<gpf::SPLIT_NONE, 0>);
@@ -951,7 +952,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
   step_plan(pc, nt, S, Smax, plan);
   const int ntl = nt - 1, ng = num_groups(pc, nt);
   const size_t part_cap = Smax > 1 ? (size_t)pc * ntl * Smax * T * T : 0;
-  const size_t cnt_cap = Smax > 1 ? (size_t)pc * ntl : 0;
+  const size_t cnt_cap = Smax > 1 ? (size_t)pc * ntl * gpf::SPLIT_CNT : 0;
   // partial-slot and counter ranges each group touches: groups run concurrently, so they must
   // be disjoint (within a group the launches are ordered on its stream)
   std::vector<size_t> plo(MAX_GROUPS, SIZE_MAX), phi(MAX_GROUPS, 0), clo(MAX_GROUPS, SIZE_MAX), chi(MAX_GROUPS, 0);
@@ -989,16 +990,22 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
       } else if (role == gpf::ROLE_PIECE) {
         if (l.S < 2) return plan_fail(msg, msg_len, "J=%d block %u is a piece of an unsplit launch (S=%d)", l.J, b, l.S);
         ++piece[(size_t)t * l.S + sidx];
-        const size_t off = l.part_off + ((size_t)t * l.S + sidx) * T * T, ci = l.cnt_off + t;
-        if (off + (size_t)T * T > part_cap || ci >= cnt_cap)
+        const size_t off = l.part_off + ((size_t)t * l.S + sidx) * T * T, ci = l.cnt_off + (size_t)t * gpf::SPLIT_CNT;
+        if (off + (size_t)T * T > part_cap || ci + gpf::SPLIT_CNT > cnt_cap || l.S > 32)
           return plan_fail(msg, msg_len, "J=%d tile %d piece %d outside the split buffers (S=%d)", l.J, t, sidx, l.S);
         plo[l.g] = std::min(plo[l.g], off);
         phi[l.g] = std::max(phi[l.g], off + (size_t)T * T);
         clo[l.g] = std::min(clo[l.g], ci);
-        chi[l.g] = std::max(chi[l.g], ci + 1);
+        chi[l.g] = std::max(chi[l.g], ci + gpf::SPLIT_CNT);
       }
       ++wgs;
     }
+    // the split-K reduction tree (gpf::split_part): every pair of node ranges has its own counter
+    for (int lv = 0; l.S > 1 && (1 << lv) < l.S; ++lv)
+      for (int cn = 0; (cn << lv) < l.S; cn += 2)
+        if (((cn + 1) << lv) < l.S && lv * 16 + (cn >> 1) >= gpf::SPLIT_CNT)
+          return plan_fail(msg, msg_len, "J=%d: split factor %d needs more than %d tree counters", l.J, l.S,
+                           gpf::SPLIT_CNT);
     for (int q = 0; q < l.gc; ++q) {
       if (diag[q] != l.ed) return plan_fail(msg, msg_len, "J=%d particle %d: %d diagonal workgroups", l.J, q, diag[q]);
       diag_wgs += diag[q];

@@ -197,8 +197,8 @@ const char* gpf_build_info(void);
  * exactly once (one whole-tile workgroup, or all S depth pieces exactly once, whose S arrivals
  * on a zeroed counter elect exactly one finisher), that pieces stay inside the split-K buffers,
  * and that concurrent particle groups never share partial slots or counters.
- * With the early diagonal factor it also checks that every launch J >= 1 starts with exactly one
- * diagonal workgroup per particle, ahead of all tiles (and launch 0 with none).
+ * With the early diagonal factor it also checks that every launch starts with exactly one
+ * diagonal workgroup per particle, ahead of all tiles.
  * stats (nullable, 8 entries): launches, workgroups, whole tiles, split tiles, S (all-tile
  * split factor), largest split factor, particle groups, diagonal workgroups. Returns GPF_OK, or
  * GPF_BAD_ARG with a description of the first violation in msg. */

@@ -62,13 +62,16 @@ for J in range(nt - 1):
     span = (en[live].max() - t0) * 1e-2
     tot += span
     # tile w = 0 of particle 0: block ids with (p, w) = (0, 0) in particle-fastest order, plus pieces
-    if mode == "predict":  # split-all: piece s of tile w at b = s * (nt - 1) + w
-        ids = [b for b in range(W) if live[b] and b % (nt - 1) == 0]
-    else:  # critical-tile split (csrc/gpfit_api.hip split_crit): pieces of particle 0 at b = s * P
+    ed = P if P * (nt - 1) <= 512 else 0  # early diagonal workgroups first (early_diag)
+    if mode == "predict":  # split-all: piece s of tile w at b = ed + s * (nt - 1) + w
+        ids = [b for b in range(ed, W) if live[b] and (b - ed) % (nt - 1) == 0]
+    else:  # critical-tile split (csrc/gpfit_api.hip split_crit): pieces of particle 0 at b = ed + s * P
         S = 1 if (J == 0 or J >= nt - 1 or nt < 4) else min(4, max(1, J * T // 16 // 16))
-        while S > 1 and P * (nt - 1) + P * (S - 1) > 512:
+        while S > 1 and P * (nt - 1) + P * (S - 1) + ed > 512:
             S -= 1
-        ids = [s * P for s in range(S) if live[s * P]]
+        ids = [ed + s * P for s in range(S) if live[ed + s * P]]
+    last = int(np.argmax(np.where(live, en, 0)))
+    dg = f" diag end {(en[0] - t0) * 1e-2:6.1f}" if ed else ""
     if not ids:
         print(f"{J:2d} {span:7.1f}")
         continue
@@ -77,6 +80,7 @@ for J in range(nt - 1):
     g_end = max(p0[b, 0] for b in ids if p0[b, 0] >= t0) if any(p0[b, 0] >= t0 for b in ids) else 0
     rel = lambda v: (v - t0) * 1e-2 if v >= t0 else float("nan")  # noqa: E731
     print(f"{J:2d} {span:7.1f}   | {len(ids):2d} pieces {rel(min(st[b] for b in ids)):6.1f}..{rel(g_end):6.1f}"
-          f"   {rel(p0[fin, 1]):6.1f} {rel(p0[fin, 2]):6.1f} {rel(p0[fin, 3]):6.1f} {rel(en[fin]):6.1f}")
+          f"   {rel(p0[fin, 1]):6.1f} {rel(p0[fin, 2]):6.1f} {rel(p0[fin, 3]):6.1f} {rel(en[fin]):6.1f}"
+          f"  |{dg}  last wg {last} ends {(en[last] - t0) * 1e-2:6.1f}")
 print(f"sum of launch spans {tot:.1f} us")
 ctx.close()

@@ -51,8 +51,8 @@ def test_every_tile_has_exactly_one_finisher(env, kv):
             st = gpfit.plan_check(pc, nt)
             assert st["launches"] == (nt * st["groups"] if nt > 1 else 0)
             assert st["whole_tiles"] + st["split_tiles"] == pc * (nt - 1) * nt  # every (J, p, w)
-            # early diagonal factor: one diagonal workgroup per particle in every launch J >= 1
-            assert st["diag_workgroups"] in (0, pc * (nt - 1))
+            # early diagonal factor: one diagonal workgroup per particle in every launch
+            assert st["diag_workgroups"] in (0, pc * nt if nt > 1 else 0)
             seen_split += st["split_tiles"] > 0
             seen_groups += st["groups"] > 1
     if kv.get("GPF_SPLIT_K") or kv.get("GPF_SPLIT_CRIT") or not kv:
@@ -74,15 +74,16 @@ def test_default_plans_of_the_baseline_configs(env):
     assert b["groups"] == 1 and b["S"] == 1 and b["Smax"] > 1 and b["split_tiles"] > 0
     one = gpfit.plan_check(1, 32)           # prediction: single particle, all tiles split
     assert one["S"] == 16 and one["whole_tiles"] == 31  # J = 0 has nothing to split
-    # early diagonal factor where launches leave slots idle (B, D's share, the prediction), the
-    # fused factor where they are slot-bound (C, E's share)
-    assert (c["diag_workgroups"], e["diag_workgroups"]) == (0, 0)
-    assert b["diag_workgroups"] == 32 * 7 and d["diag_workgroups"] == 32 * 31 and one["diag_workgroups"] == 31
+    # early diagonal factor where launches leave slots idle (B, the prediction), the fused factor
+    # where they are slot-bound (C, D's and E's shares)
+    assert e["diag_workgroups"] == 0
+    assert (c["diag_workgroups"], d["diag_workgroups"]) == (0, 0)
+    assert b["diag_workgroups"] == 32 * 8 and one["diag_workgroups"] == 32
 
 
 def test_early_diag_override(env):
     env({"GPF_EARLY_DIAG": "1"})
-    assert gpfit.plan_check(64, 32)["diag_workgroups"] == 64 * 31
+    assert gpfit.plan_check(64, 32)["diag_workgroups"] == 64 * 32
     env({"GPF_EARLY_DIAG": "0"})
     assert gpfit.plan_check(32, 8)["diag_workgroups"] == 0
 
