@@ -242,12 +242,13 @@ static int ensure_work(gpf_ctx* c, int want) {
 
 // Particle groups factorised on concurrent streams (GPF_GROUPS overrides): they fill the tail
 // of each dependent block-column launch with another group's tiles. Measured on MI355X
-// (profiles/r1/groups_ab.txt): 2 groups +0.6% at N=4096 P=64, +4.6% at N=4096 P=32 (config D's
-// share of one GPU), -19% at N=1024 P=32, 4 groups worse everywhere. Default: 2 groups for
-// chunks of at most 32 particles with at least 16 block columns, else 1 (at 64 particles the
-// gain is within noise, and one stream keeps per-launch timing exact for the roofline).
+// (profiles/r1/groups_ab.txt, profiles/r2/groups_stagger_ab.txt): 2 groups +4.6% at N=4096 P=32
+// (config D's share of one GPU), +1.7% at N=4096 P=64 (config C, round 2: 1303 -> 1324
+// evals/s, same box), -19% at N=1024 P=32, 4 groups worse everywhere. Default: 2 groups for
+// chunks with at least 16 block columns, else 1. (With concurrent groups the per-launch times
+// overlap, so bench.py rates the whole factorisation phase instead: no gaps or overlap counted.)
 static int num_groups(int pc, int nt) {
-  int g = (pc <= 32 && nt >= 16) ? 2 : 1;
+  int g = nt >= 16 ? 2 : 1;
   if (const char* s = getenv("GPF_GROUPS")) g = atoi(s);
   g = std::max(1, std::min(g, MAX_GROUPS));
   while (g > 1 && pc / g < 8) --g;  // keep >= 8 particles (one per XCD) per group

@@ -64,8 +64,8 @@ def test_every_tile_has_exactly_one_finisher(env, kv):
 def test_default_plans_of_the_baseline_configs(env):
     """The schedules the bench and the GPU tests rely on."""
     env({})
-    c = gpfit.plan_check(64, 32)            # config C: one stream, no split
-    assert (c["groups"], c["Smax"]) == (1, 1)
+    c = gpfit.plan_check(64, 32)            # config C: two concurrent groups, no split
+    assert (c["groups"], c["Smax"]) == (2, 1)
     d = gpfit.plan_check(32, 32)            # config D's per-GPU share: two concurrent groups
     assert d["groups"] == 2
     e = gpfit.plan_check(16, 128)           # config E's per-GPU share at N=16384
