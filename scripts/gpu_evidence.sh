@@ -17,7 +17,9 @@ timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 
 for f in B D_share E_share torchrun1; do python -c "import json,sys; d=json.loads(open('$O/bench_$f.log').read().strip().splitlines()[-1]); r=d['roofline']; print('$f', round(d['value'],1), d['unit'], 'frac', round(r['frac'],3), r['timing'][:40])"; done
 B="python bench.py --steps 3 --warmup 1 --pso-steps 0 $BQ"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- $B > $O/prof.log 2>&1 || exit $?
-f=$(find $O/prof -name "*kernel_trace.csv" | head -1); python scripts/step_timeline.py $f 4096 > $O/timeline.txt; tail -1 $O/timeline.txt
+f=$(find $O/prof -name "*kernel_trace.csv" | head -1); python scripts/step_timeline.py $f 4096 > $O/timeline.txt
+python scripts/kernel_union.py $f 4096 64 3 | tee $O/kernel_union.txt
+tail -1 $O/prof.log | cut -c1-120 > /dev/null
 B2="python bench.py --steps 2 --warmup 1 --pso-steps 0 --no-profile $BQ"
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o f --output-format csv -- $B2 > $O/pmc_fetch.log 2>&1 || exit $?
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o w --output-format csv -- $B2 > $O/pmc_write.log 2>&1 || exit $?
