@@ -2,7 +2,9 @@
 
 usage: python scripts/step_timeline.py <kernel_trace.csv> N
 Prints, per J, the mean launch time and the algorithmic TF/s of the launch
-(same flop formula as run_factor), and the gaps between consecutive launches."""
+(same flop formula as run_factor), and the gaps between consecutive launches. With concurrent
+particle-group streams the launches of the groups overlap: the per-launch rate then counts one
+group's share while the other group shares the GPU (see kernel_union.py for the whole phase)."""
 import csv
 import sys
 from collections import defaultdict
@@ -25,20 +27,23 @@ def flops(J):
 
 dur, gap = defaultdict(list), defaultdict(list)
 P = None
-J = 0
+k = 0
+ngroups, builds, after_step = 1, 0, True
 prev_end = None
 for r in rows:
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
     name = r["Kernel_Name"]
-    if "k_build_cov" in name:
-        J = 0
+    if "k_build_cov" in name:  # the particle groups' K builds are adjacent: count them
+        builds = 1 if after_step else builds + 1
+        ngroups, k, after_step = builds, 0, False
     if "k_step" in name:
-        P = int(r["Grid_Size_X"]) // (int(r["Workgroup_Size_X"]) * (nt - 1)) if int(r["Grid_Size_Y"]) == 1 \
-            else int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"])
+        after_step = True
+        J = k // ngroups  # launches interleave the groups block column by block column
+        P = ngroups * (int(r["Grid_Size_X"]) // (int(r["Workgroup_Size_X"]) * (nt - 1)))
         dur[J].append((e - s) * 1e-6)
         if prev_end is not None:
             gap[J].append((s - prev_end) * 1e-6)
-        J += 1
+        k += 1
     prev_end = e
 tot_ms = tot_fl = 0.0
 for j in sorted(dur):
