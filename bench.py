@@ -345,7 +345,9 @@ def main():
     s, ex = sigma_grid()
     P = spg * world
 
-    ctx = gpfit.Context(local)
+    # one GPU per rank (LOCAL_RANK); GPFIT_DEVICE pins every rank to one device, for rehearsing
+    # the multi-rank path on a one-GPU box with GPF_COMM_TRANSPORT=host (RCCL needs a GPU per rank)
+    ctx = gpfit.Context(int(os.environ.get("GPFIT_DEVICE", local)))
     comm = gpfit.Comm.from_env(ctx) if world > 1 else None  # RCCL on this rank's GPU
     score = make_scorer(x, y, e, s, ex, lo, hi, ctx=ctx, comm=comm)
     rng = np.random.default_rng(args.seed + 1000)  # identical on every rank

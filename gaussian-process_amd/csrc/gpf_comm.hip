@@ -221,6 +221,15 @@ int gpf_comm_open(gpf_ctx* ctx, int rank, int nranks, const char* host, int port
   c->transport = transport;
   if (const char* s = getenv("GPF_COMM_TIMEOUT_S")) c->timeout_ms = std::max(1, atoi(s)) * 1000;
   int rc = nranks > 1 ? rendezvous(c, host, port) : GPF_OK;
+  if (rc == GPF_OK && transport == GPF_COMM_HOST && nranks > 1) {
+    // the host transport runs the same id hand-out as the RCCL one (a stand-in 128-byte id,
+    // checked on every rank), so the CPU tests exercise the broadcast the RCCL bootstrap relies on
+    unsigned char id[128];
+    for (int i = 0; i < 128; ++i) id[i] = (unsigned char)(rank == 0 ? (i * 37 + 11) & 255 : 0);
+    rc = host_bcast(c, id, sizeof(id));
+    for (int i = 0; rc == GPF_OK && i < 128; ++i)
+      if (id[i] != (unsigned char)((i * 37 + 11) & 255)) rc = comm_fail(c, "gpf_comm_open: id broadcast corrupted");
+  }
   if (rc == GPF_OK && transport == GPF_COMM_RCCL) {
     c->device = ctx->device;
     ncclUniqueId id;

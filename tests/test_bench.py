@@ -34,3 +34,19 @@ def test_gpus_flag_starts_that_many_ranks(n):
 def test_world_size_mismatch_is_an_error():
     r = _run(["--gpus", "3", "--plumbing"], env={"WORLD_SIZE": "2", "RANK": "0"})
     assert r.returncode == 2 and "--gpus 3" in r.stderr
+
+
+@pytest.mark.gpu
+def test_multi_rank_bench_on_one_gpu():
+    """bench.py --gpus 2 end to end on the GPU box: the rank processes it starts, the library's
+    communicator (host transport: RCCL needs one GPU per rank), gpf_eval_batch_sharded on the GPU,
+    the barrier and the max-over-ranks timing. Both ranks share device 0 (GPFIT_DEVICE)."""
+    r = _run(["--gpus", "2", "--steps", "2", "--warmup", "1", "--n", "1024", "--d", "2", "--no-cpu",
+              "--pso-steps", "1", "--predict-points", "0", "--no-hull", "--psurf-rows", "0"],
+             env={"GPFIT_DEVICE": "0", "GPF_COMM_TRANSPORT": "host"}, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["swarm"] == 64 and out["value"] > 0
+    assert out["config"]["swarm_per_gpu"] == 32
