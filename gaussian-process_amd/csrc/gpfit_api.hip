@@ -1271,7 +1271,7 @@ int gpf_gemm_bench(gpf_ctx* c, int mode, int Npad, int P, int tiles, int D, int 
   return GPF_OK;
 }
 
-// Debug hook: the unblocked-panel 64x64 factor on two matrices (2*4096 in, 4*4096 out).
+// Debug hook: the 64x64 diagonal-leaf factor on two matrices (2*4096 in, 4*4096 out).
 int gpf_debug_factor64(gpf_ctx* c, const double* in, double* out, int* bad) {
   if (!c || !in || !out || !bad) return GPF_BAD_ARG;
   hipSetDevice(c->device);

@@ -42,6 +42,7 @@ SIGNATURES = {
     "gpf_reset_profile": (ctypes.c_int, [_vp]),
     "gpf_selftest_mfma": (ctypes.c_int, [_vp, _dp, _dp, _dp]),
     "gpf_debug_factor": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _dp]),
+    "gpf_debug_factor64": (ctypes.c_int, [_vp, _dp, _dp, _ip]),
     "gpf_mfma_peak": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _dp]),
     "gpf_prob_surface": (ctypes.c_int, [_vp, _dp, ctypes.c_int64, ctypes.c_int, _dp, _dp,
                                         ctypes.POINTER(ctypes.c_int)]),
@@ -267,6 +268,14 @@ class Context:
         if rc not in (GPF_OK, GPF_NOT_PD):
             self._check(rc, "gpf_debug_factor")
         return L, U, z, al
+
+    def debug_factor64(self, a):
+        """factor64 on two 64x64 matrices a[2,64,64]: (L[2], X[2], bad[2]) (diagnostic)."""
+        a = np.ascontiguousarray(a, dtype=np.float64).reshape(2, 64, 64)
+        out = np.empty((4, 64, 64))
+        bad = np.zeros(2, dtype=np.int32)
+        self._check(self.lib.gpf_debug_factor64(self._h, _ptr(a), _ptr(out), bad.ctypes.data_as(_ip)), "gpf_debug_factor64")
+        return out[0::2], out[1::2], bad
 
     def mfma_peak(self, blocks=1024, iters=4096):
         out = ctypes.c_double(0.0)

@@ -576,3 +576,31 @@ def test_early_diagonal_factor_matches_fused(ctx, monkeypatch, N, d, P):
     mo, so = ref_cpu.GP_train_identity(x, y, e, Q[0]) if N <= 2049 else (None, None)
     if mo is not None:
         assert _rel(out["1"][1][0], mo) < RTOL_MU_SD and _rel(out["1"][2][0], so) < RTOL_MU_SD
+
+
+@pytest.mark.gpu
+def test_factor64_leaf(ctx):
+    """The 64x64 diagonal-leaf factor (csrc/gpf_factor.hip factor64) against LAPACK:
+    L = cholesky(A), X = L^-1, exact zeros above both diagonals, pivot failure flagged.
+    Matrices: a well-conditioned SPD one and a kernel-like one (SE covariance of 64 sorted
+    points + noise, the diagonal blocks k_step factors; cond ~1e8)."""
+    rng = np.random.default_rng(64)
+    g = rng.standard_normal((64, 64))
+    a0 = g @ g.T / 64 + np.eye(64)
+    t = np.sort(rng.uniform(size=64))
+    a1 = np.exp(-0.5 * (t[:, None] - t[None, :]) ** 2 / 0.2 ** 2) + np.diag(rng.uniform(1e-4, 1e-3, 64))
+    up = np.triu(np.full((64, 64), 7.0), 1)  # garbage above the diagonal must not be read
+    L, X, bad = ctx.debug_factor64(np.stack([np.tril(a0) + up, np.tril(a1) + up]))
+    assert bad.tolist() == [0, 0]
+    for k, a in enumerate((a0, a1)):
+        Lr = np.linalg.cholesky(a)
+        assert np.all(np.triu(L[k], 1) == 0) and np.all(np.triu(X[k], 1) == 0)
+        cond = np.linalg.cond(a)
+        assert np.abs(L[k] - Lr).max() <= 1e-13 * np.abs(Lr).max() * max(1.0, np.sqrt(cond))
+        assert np.abs(L[k] @ L[k].T - a).max() <= 1e-14 * 64 * np.abs(a).max()
+        assert np.abs(X[k] @ L[k] - np.eye(64)).max() <= 1e-15 * 64 * cond
+    # a pivot that is not > 0: flagged (numpy raises LinAlgError, GP_func.py:22)
+    a2 = a0.copy()
+    a2[40, 40] = -1.0
+    _, _, bad = ctx.debug_factor64(np.stack([np.tril(a0), np.tril(a2)]))
+    assert bad.tolist() == [0, 1]
