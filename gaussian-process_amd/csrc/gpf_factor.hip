@@ -157,7 +157,7 @@ __device__ __forceinline__ void f64_block(int id, bool& isx, int& bi, int& bj) {
   bj = t - bi * (bi + 1) / 2;
 }
 
-__device__ __forceinline__ bool factor64_panels(double* sA, int la, double* sX, int lx, double* buf) {
+__device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx, double* buf) {
   constexpr int PW = F64_PW, NS = 3;  // panel width, block slots per update wave
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -318,167 +318,6 @@ __device__ __forceinline__ bool factor64_panels(double* sA, int la, double* sX, 
   return bad;
 }
 
-// ----------------------------------------------------------------------------
-// 64x64 Cholesky + inverse in 16-wide leaves (same contract as factor64_panels).
-// Step k (diagonal block k, rows/columns 16k..16k+15):
-//   leaf  (wave 0):  A_kk = L_kk L_kk^T, X_kk = L_kk^-1 column by column in registers.
-//                    Lane (r = lane&15, g = lane>>4) holds row r, columns 4g..4g+3 of
-//                    A_kk and X_kk; column j of L and row j of X are broadcast through
-//                    32 doubles of LDS (one wave: in-order LDS, no barrier). The pivot of
-//                    column j+1 is formed from two readlanes as soon as column j is scaled,
-//                    so its reciprocal square root overlaps the broadcast of column j.
-//   panel (waves):   L_ik = A_ik X_kk^T (i > k) and X_kj = -X_kk sum_{m=j..k-1} L_km X_mj
-//                    (j < k): 3 independent 16x16 MFMA jobs.
-//   trailing:        A_ij -= L_ik L_jk^T (k < j <= i): up to 6 jobs.
-// The per-column operations (mul, then sub: -ffp-contract=off) are those of the
-// elimination; the blocked updates use the MFMA's fused accumulation, so the result is
-// not bitwise that of factor64_panels (both are within a few ulp of LAPACK's).
-// ----------------------------------------------------------------------------
-__device__ __forceinline__ bool factor64_leaf(double* sA, int la, double* sX, int lx, double* buf) {
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lr = lane & 15, lk = lane >> 4;  // MFMA operand row/col and depth index; C row base
-  bool bad = false;
-#pragma unroll 1
-  for (int k = 0; k < 4; ++k) {
-    const int b0 = 16 * k;
-    if (wave == 0) {
-      const int r = lr, g = lk;
-      double* colb = buf;       // column j of L_kk
-      double* xrw = buf + 16;   // row j of X_kk
-      double a[4], x[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int c = 4 * g + q;
-        a[q] = (c <= r) ? sA[(b0 + r) * la + b0 + c] : 0.0;
-        x[q] = (c == r) ? 1.0 : 0.0;
-      }
-      double p = readlane_f64(a[0], 0);
-      bad = bad | !(p > 0.0);
-      double inv = rsqrt_nr(p);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int gj = j >> 2, qj = j & 3;
-        const double lcol = (r > j) ? a[qj] * inv : ((r == j) ? p * inv : 0.0);  // L[r][j]
-        if (g == gj) a[qj] = lcol;
-        if (r == j) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) x[q] = x[q] * inv;
-        }
-        double pn = 1.0, invn = 1.0;
-        if (j < 15) {
-          // pivot of column j+1: A[j+1][j+1] - L[j+1][j] L[j+1][j], the update the owning
-          // lane applies below (same operands, same order)
-          const int j1 = j + 1;
-          const double d = readlane_f64(a[j1 & 3], j1 + 16 * (j1 >> 2));
-          const double e = readlane_f64(a[qj], j1 + 16 * gj);
-          pn = d - e * e;
-          bad = bad | !(pn > 0.0);
-          invn = rsqrt_nr(pn);
-        }
-        if (g == gj) colb[r] = lcol;
-        if (r == j) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) xrw[4 * g + q] = x[q];
-        }
-        const double lrow = colb[r];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int c = 4 * g + q;
-          const double lc = colb[c], xj = xrw[c];
-          if (c > j && r >= c) a[q] = a[q] - lrow * lc;
-          if (r > j) x[q] = x[q] - lrow * xj;
-        }
-        p = pn;
-        inv = invn;
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        sA[(b0 + r) * la + b0 + 4 * g + q] = a[q];
-        sX[(b0 + r) * lx + b0 + 4 * g + q] = x[q];
-      }
-    }
-    __syncthreads();
-    // panel jobs: t < 3-k -> L_ik, i = k+1+t; else X_kj, j = t-(3-k)
-    if (wave < 3) {
-      const int t = wave;
-      d4 acc = d4{0.0, 0.0, 0.0, 0.0};
-      if (t < 3 - k) {
-        const int bi = k + 1 + t;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const double av = sA[(16 * bi + lr) * la + b0 + 4 * s + lk];
-          const double bv = sX[(b0 + lr) * lx + b0 + 4 * s + lk];  // X_kk^T[k'][c] = X_kk[c][k']
-          acc = mfma(av, bv, acc);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) sA[(16 * bi + lk + 4 * e) * la + b0 + lr] = acc[e];
-      } else {
-        const int bj = t - (3 - k);
-        for (int m = bj; m < k; ++m) {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            const double av = sA[(b0 + lr) * la + 16 * m + 4 * s + lk];
-            const double bv = sX[(16 * m + 4 * s + lk) * lx + 16 * bj + lr];
-            acc = mfma(av, bv, acc);
-          }
-        }
-        d4 xo = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) xo = mfma_neg_a(sX[(b0 + lr) * lx + b0 + 4 * s + lk], acc[s], xo);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) sX[(b0 + lk + 4 * e) * lx + 16 * bj + lr] = xo[e];
-      }
-    }
-    if (k == 3) break;
-    __syncthreads();
-    // trailing jobs (bi, bj), k < bj <= bi <= 3, in the order (k+1,k+1) (k+2,k+1) (k+2,k+2) ..
-    {
-      const int n = 3 - k, jobs = n * (n + 1) / 2;
-      if (wave < jobs) {
-        const int t = wave;
-        const int ii = (t >= 3) ? 2 : (t >= 1) ? 1 : 0;  // row within the trailing triangle
-        const int bi = k + 1 + ii, bj = k + 1 + (t - ii * (ii + 1) / 2);
-        d4 acc;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[e] = sA[(16 * bi + lk + 4 * e) * la + 16 * bj + lr];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const double av = sA[(16 * bi + lr) * la + b0 + 4 * s + lk];
-          const double bv = sA[(16 * bj + lr) * la + b0 + 4 * s + lk];
-          acc = mfma_neg_a(av, bv, acc);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) sA[(16 * bi + lk + 4 * e) * la + 16 * bj + lr] = acc[e];
-      }
-    }
-    __syncthreads();
-  }
-  // zeros in the upper blocks (0,1) (0,2) (0,3) (1,2) (1,3) (2,3) of L and X
-  if (wave >= 2) {
-    const int t = wave - 2;
-    const int bi = (t < 3) ? 0 : (t < 5) ? 1 : 2;
-    const int bj = (t < 3) ? t + 1 : (t < 5) ? t - 1 : 3;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      sA[(16 * bi + lk + 4 * e) * la + 16 * bj + lr] = 0.0;
-      sX[(16 * bi + lk + 4 * e) * lx + 16 * bj + lr] = 0.0;
-    }
-  }
-  return bad;
-}
-
-#ifndef GPF_F64_LEAF
-#define GPF_F64_LEAF 1
-#endif
-__device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx, double* buf) {
-#if GPF_F64_LEAF
-  return factor64_leaf(sA, la, sX, lx, buf);
-#else
-  return factor64_panels(sA, la, sX, lx, buf);
-#endif
-}
 
 // Fixed-order sum of the 8 partials scratch[q*64 + i], q = 0..7.
 __device__ __forceinline__ double sum8(const double* scratch, int i) {

@@ -2,7 +2,7 @@
 import ctypes, os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["GPFIT_LIB"] = os.path.join(ROOT, "gaussian-process_amd", "libgpfit_stamps.so")
+os.environ["GPFIT_LIB"] = os.path.join(ROOT, "gaussian-process_amd", os.environ.get("STAMPS_LIB", "libgpfit_stamps.so"))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "gaussian-process_amd")]
 import torch  # noqa
 import gpfit

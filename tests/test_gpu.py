@@ -579,7 +579,7 @@ def test_early_diagonal_factor_matches_fused(ctx, monkeypatch, N, d, P):
 
 
 @pytest.mark.gpu
-def test_factor64_leaf(ctx):
+def test_factor64(ctx):
     """The 64x64 diagonal-leaf factor (csrc/gpf_factor.hip factor64) against LAPACK:
     L = cholesky(A), X = L^-1, exact zeros above both diagonals, pivot failure flagged.
     Matrices: a well-conditioned SPD one and a kernel-like one (SE covariance of 64 sorted
