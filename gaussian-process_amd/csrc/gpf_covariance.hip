@@ -26,7 +26,7 @@ __global__ __launch_bounds__(NTHR) void k_build_cov(int N, int Npad, int d, cons
                                                     const double* __restrict__ y, const double* __restrict__ e,
                                                     const double* __restrict__ ls, double* __restrict__ Lb,
                                                     double* __restrict__ yb, int* __restrict__ info, int diag_only,
-                                                    int* __restrict__ dflag) {
+                                                    int* __restrict__ dflag, int* __restrict__ cflag) {
   __shared__ double ai[DMAX][BT];
   __shared__ double aj[DMAX][BT];
   __shared__ double ni[BT], nj[BT];
@@ -49,6 +49,7 @@ __global__ __launch_bounds__(NTHR) void k_build_cov(int N, int Npad, int d, cons
   if (idx == 0 && tid == 0) {
     info[p] = 0;  // the factorisation kernels only ever set it
     dflag[p] = -1;  // no diagonal block published yet (early diagonal factor, k_step)
+    cflag[p] = -1;  // no critical tile published yet (quadrant finish, k_step)
   }
 
   if (tid < 128) {

@@ -567,7 +567,7 @@ __host__ __device__ __forceinline__ void step_tile(int b, int P, int ntl, int gr
 }
 
 enum { SPLIT_NONE = 0, SPLIT_ALL = 1, SPLIT_CRIT = 2 };
-enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2, ROLE_DIAG = 3 };
+enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2, ROLE_DIAG = 3, ROLE_QUAD = 4 };
 
 // Early diagonal factor (k_step<SPLIT, ED = 1>; the host chooses it for launches that leave
 // workgroup slots idle): launch J starts with P extra workgroups that factor diagonal
@@ -579,13 +579,19 @@ enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2, ROLE_DIAG = 3 };
 // to -1). With ED = 0 the critical tile factors block J+1 itself (fused) and k_diag block 0.
 
 // Workgroup b of a k_step<SPLIT> launch (grid: [P diagonal workgroups if ed] + P*(nt-1)*S for
-// SPLIT_ALL, P*(nt-1) + P*(S-1) for SPLIT_CRIT, P*(nt-1) otherwise): its particle p, tile w,
-// split index sidx, and whether it factors the diagonal block (ROLE_DIAG, w = -1), runs the whole
-// tile, one depth range (piece sidx of S) of it, or nothing. The kernel and the host-side plan
-// check (gpf_plan_check) both decode through this function.
+// SPLIT_ALL, P*(nt-1) + P*(S-1) for SPLIT_CRIT, P*(nt-1) otherwise, + [4 P quadrant workgroups if
+// qf]): its particle p, tile w, split index sidx, and whether it factors the diagonal block
+// (ROLE_DIAG, w = -1), runs the whole tile, one depth range (piece sidx of S) of it, nothing, or
+// quadrant sidx of the critical tile's finish (ROLE_QUAD, w = -1). The kernel and the host-side
+// plan check (gpf_plan_check) both decode through this function.
 template <int SPLIT>
-__host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt, int grp, int S, int ed, int& p,
-                                                    int& w, int& sidx) {
+__host__ __device__ __forceinline__ int step_regular(int P, int nt, int S) {
+  return SPLIT == SPLIT_ALL ? P * (nt - 1) * S : SPLIT == SPLIT_CRIT ? P * (nt - 1) + P * (S - 1) : P * (nt - 1);
+}
+
+template <int SPLIT>
+__host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt, int grp, int S, int ed, int qf,
+                                                    int& p, int& w, int& sidx) {
   const int tiles = P * (nt - 1);
   sidx = 0;
   if (ed) {
@@ -595,6 +601,15 @@ __host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt,
       return ROLE_DIAG;
     }
     b -= P;
+  }
+  if (qf) {
+    const int reg = step_regular<SPLIT>(P, nt, S);
+    if (b >= reg) {  // particle fastest: quadrant q of every particle, then q + 1
+      p = (b - reg) % P;
+      sidx = (b - reg) / P;
+      w = -1;
+      return ROLE_QUAD;
+    }
   }
   if (SPLIT == SPLIT_ALL) {
     sidx = b / tiles;  // split-major dispatch
@@ -795,6 +810,132 @@ __device__ __forceinline__ void wait_diag(const int* flag, int J, int* info) {
   __syncthreads();
 }
 
+// ----------------------------------------------------------------------------
+// Quadrant finish of the critical tile (launches with the early diagonal factor; GPF_QUAD).
+// The critical tile I = J+1 closes every launch's dependency chain: C = A_IJ - L_I,<J L_J,<J^T,
+// then L_IJ = C U_JJ^T, then A_II -= L_IJ L_IJ^T and y_I -= L_IJ z_J, and the next launch's
+// diagonal workgroup factors A_II. On one workgroup the triangular multiply and the rank-128
+// update take ~40 us per launch at small N (profiles/r2/v2_crit_B.txt), so here the workgroup
+// that completes C publishes it (write-through to the particle's quadrant buffer, then cflag = J)
+// and four quadrant workgroups (rh, kh) in {0,1}^2, dispatched at the end of the launch, finish:
+//   L_IJ[rh][kh] = sum_{m <= kh} C[rh][m] U_JJ[kh][m]^T           (64x64, depth 64 or 128)
+//   Y[rh][kh]    = L_IJ[rh][kh] z_J[kh]                          (row partials)
+// the second of the pair (0,kh), (1,kh) to arrive (ticket) forms column half kh's share of the
+// rank-128 update for the three lower quadrants of A_II,
+//   P_kh = L_IJ[:,kh] L_IJ[:,kh]^T                               (depth 64)
+// and the second of the two pair finishers applies A_II -= (P_0 + P_1), y_I -= (Y[.][0] + Y[.][1]).
+// IEEE addition commutes, so the result does not depend on the arrival order. Hand-offs as in
+// split_part (write-through stores, drain, relaxed ticket, agent acquire by the second arriver);
+// the quadrant workgroups wait only on workgroups dispatched before them (the C producer and the
+// diagonal workgroup), so in-order dispatch cannot deadlock them.
+// Per-particle buffer (QSTRIDE doubles): C [128][128] | P [2][3][64][64] | Y [2][2][64].
+// ----------------------------------------------------------------------------
+constexpr int QSTRIDE = T * T + 6 * H * H + 4 * H;
+constexpr int QCNT = 4;  // arrival counters per particle: pair kh = 0, 1; the top
+
+// Second-arriver election on a zeroed counter (reset by the second arriver for the next launch).
+__device__ __forceinline__ bool pair_ticket(unsigned* cn, int* sflag) {
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(cn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int second = old == 1u;
+    if (second) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(cn, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *sflag = second;
+  }
+  __syncthreads();
+  return *sflag != 0;
+}
+
+__device__ void quad_item(int q, int J, int p, int Npad, double* __restrict__ Lb, const double* __restrict__ Ub,
+                          double* __restrict__ yb, int* __restrict__ info, const int* __restrict__ dflag,
+                          const int* __restrict__ cflag, double* __restrict__ qbuf, unsigned* __restrict__ qcnt,
+                          int* sflag, double* smem, double* small) {
+  const int tid = threadIdx.x;
+  const size_t ld = (size_t)Npad;
+  const int I = J + 1, rh = q >> 1, kh = q & 1;
+  double* Lp = Lb + (size_t)p * ld * ld;
+  const double* Ujj = Ub + (size_t)p * ld * ld + (size_t)J * T * ld + (size_t)J * T;
+  double* yp = yb + (size_t)p * Npad;
+  double* qb = qbuf + (size_t)p * QSTRIDE;
+  const double* Cb = qb;
+  double* Pb = qb + T * T;
+  double* Yb = Pb + 6 * H * H;
+  unsigned* qc = qcnt + (size_t)p * QCNT;
+  double* sA = smem;
+  double* sB = smem + H * LDH;
+  double* zs = smem + 2 * H * LDH;  // z_J[kh half]
+  const Quad<64> qd;
+  Acc<64> acc;
+  acc.zero();
+  wait_diag(cflag + p, J, info + p);  // C
+  tile64_to_lds(sA, LDH, Cb + (size_t)rh * H * T, T);
+  wait_diag(dflag + p, J, info + p);  // U_JJ, z_J
+  for (int m = 0; m <= kh; ++m) {
+    if (m > 0) tile64_to_lds(sA, LDH, Cb + (size_t)rh * H * T + m * H, T);
+    tile64_to_lds(sB, LDH, Ujj + (size_t)kh * H * ld + m * H, ld);
+    __syncthreads();
+    if (m == kh)
+      gemm_lds64<false, TRI_B_KLEC>(acc, sA, LDH, sB, LDH, qd);  // U_JJ[kh][kh]^T is upper triangular
+    else
+      gemm_lds64<false>(acc, sA, LDH, sB, LDH, qd);
+    __syncthreads();
+  }
+  // L_IJ[rh][kh]: to the particle's L (write-through: the pair sibling reads it) and to LDS
+  double* Lq = Lp + (size_t)I * T * ld + (size_t)J * T + (size_t)rh * H * ld + kh * H;
+  acc.foreach(qd, [&](int r, int c, double v) {
+    sA[r * LDH + c] = v;
+    gst<true>(&Lq[(size_t)r * ld + c], v);
+  });
+  if (tid < H) zs[tid] = yp[J * T + kh * H + tid];
+  __syncthreads();
+  rows_dot64(small, sA, LDH, zs, small + H, false);
+  if (tid < H) gst<true>(&Yb[(rh * 2 + kh) * H + tid], small[tid]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (!pair_ticket(qc + kh, sflag)) return;
+  // column half kh's share of the update: the sibling's rows from global
+  tile64_to_lds(sB, LDH, Lp + (size_t)I * T * ld + (size_t)J * T + (size_t)(1 - rh) * H * ld + kh * H, ld);
+  __syncthreads();
+  const double* Lt = rh == 0 ? sA : sB;  // rows 0..63 of L_IJ[:, kh]
+  const double* Lu = rh == 0 ? sB : sA;  // rows 64..127
+  Acc<64> p00, p10, p11;
+  p00.zero();
+  p10.zero();
+  p11.zero();
+  gemm_lds64<false, TRI_C_LOWER>(p00, Lt, LDH, Lt, LDH, qd);
+  gemm_lds64<false>(p10, Lu, LDH, Lt, LDH, qd);
+  gemm_lds64<false, TRI_C_LOWER>(p11, Lu, LDH, Lu, LDH, qd);
+  double* Pk = Pb + (size_t)kh * 3 * H * H;
+  p00.foreach(qd, [&](int r, int c, double v) { gst<true>(&Pk[r * H + c], v); });
+  p10.foreach(qd, [&](int r, int c, double v) { gst<true>(&Pk[H * H + r * H + c], v); });
+  p11.foreach(qd, [&](int r, int c, double v) { gst<true>(&Pk[2 * H * H + r * H + c], v); });
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (!pair_ticket(qc + 2, sflag)) return;
+  // A_II -= (P_0 + P_1) on the three lower quadrants (only the lower triangle is ever read)
+  const double* Po = Pb + (size_t)(1 - kh) * 3 * H * H;
+  double* Aii = Lp + (size_t)I * T * ld + (size_t)I * T;
+  p00.foreach(qd, [&](int r, int c, double v) {
+    double* a = &Aii[(size_t)r * ld + c];
+    *a = *a - (v + Po[r * H + c]);
+  });
+  p10.foreach(qd, [&](int r, int c, double v) {
+    double* a = &Aii[(size_t)(H + r) * ld + c];
+    *a = *a - (v + Po[H * H + r * H + c]);
+  });
+  p11.foreach(qd, [&](int r, int c, double v) {
+    double* a = &Aii[(size_t)(H + r) * ld + H + c];
+    *a = *a - (v + Po[2 * H * H + r * H + c]);
+  });
+  if (tid < T) {
+    const int h = tid >> 6, r = tid & (H - 1);
+    yp[I * T + tid] = yp[I * T + tid] - (Yb[(h * 2) * H + r] + Yb[(h * 2 + 1) * H + r]);
+  }
+}
+
 // Tile w of block column J of particle p (the unit of work of k_step); role from step_decode.
 template <int SPLIT, int ED>
 __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt, int Npad, double* __restrict__ Lb,
@@ -803,7 +944,8 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
                                           int* __restrict__ info, int N, const double* __restrict__ x,
                                           const double* __restrict__ ls, int d, int S, int sidx,
                                           double* __restrict__ part, unsigned* __restrict__ cnt, int* sflag,
-                                          const int* __restrict__ dflag, double* smem, double* small) {
+                                          const int* __restrict__ dflag, int* __restrict__ cflag,
+                                          double* __restrict__ qbuf, int qf, double* smem, double* small) {
   const int tid = threadIdx.x;
   const int nL = nt - 1 - J;
   const size_t ld = (size_t)Npad;
@@ -836,6 +978,13 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
       cov_tile_acc(acc, qd, x, ls + (size_t)p * d, d, N, I, J, smem);
       if (J > 0)
         step_gemm<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, J * T, smem, qd);
+    }
+    if (ED && qf && w == 0) {  // critical tile: publish C to the quadrant workgroups (quad_item)
+      acc.store_wt(qd, qbuf + (size_t)p * QSTRIDE, T);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(cflag + p, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
     }
     acc.store(qd, Aij, ld);  // C (the TRMM below streams it)
 #else
@@ -955,7 +1104,9 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
                                                   int* __restrict__ info, int P, int grp, int N,
                                                   const double* __restrict__ x, const double* __restrict__ ls,
                                                   int d, int S, double* __restrict__ part,
-                                                  unsigned* __restrict__ cnt, int* __restrict__ dflag, int ed) {
+                                                  unsigned* __restrict__ cnt, int* __restrict__ dflag, int ed,
+                                                  int* __restrict__ cflag, double* __restrict__ qbuf,
+                                                  unsigned* __restrict__ qcnt, int qf) {
   const int tid = threadIdx.x;
 #ifdef GPF_WG_TRACE
   if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) {
@@ -970,8 +1121,10 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
   __shared__ __attribute__((aligned(16))) double small[STEP_SMALL];
   __shared__ int sflag;
   int p, w, sidx;
-  const int role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, p, w, sidx);
-  if (ED && role == ROLE_DIAG) {
+  const int role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, ED && qf, p, w, sidx);
+  if (ED && role == ROLE_QUAD) {
+    quad_item(sidx, J, p, Npad, Lb, Ub, yb, info, dflag, cflag, qbuf, qcnt, &sflag, smem, small);
+  } else if (ED && role == ROLE_DIAG) {
     // diagonal block J of particle p (fully reduced by the previous launches' look-ahead): factor,
     // then publish to this launch's tiles (write-through stores drained, then the flag)
     const size_t ld = (size_t)Npad;
@@ -987,7 +1140,7 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
     if (tid == 0) __hip_atomic_store(dflag + p, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
     step_item<SPLIT, ED>(role, J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, sidx, part, cnt, &sflag,
-                     dflag, smem, small);
+                         dflag, cflag, qbuf, ED && qf, smem, small);
   }
 #ifdef GPF_WG_TRACE
   __syncthreads();

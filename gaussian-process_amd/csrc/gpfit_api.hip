@@ -87,6 +87,9 @@ struct gpf_ctx {
   double* d_loss = nullptr;
   int* d_info = nullptr;
   int* d_flag = nullptr;  // per particle: last diagonal block published in the running launch (early_diag)
+  int* d_cflag = nullptr;  // per particle: last critical-tile C published to the quadrant workgroups (quad_finish)
+  double* d_qbuf = nullptr;    // per particle: the quadrant finish's C, partial updates and row partials
+  unsigned* d_qcnt = nullptr;  // per particle: its arrival counters, kept zero
   int* d_hist = nullptr;
   // pinned host staging for the per-batch transfers (async DMA, capturable in graphs)
   double* h_ls = nullptr;
@@ -187,6 +190,12 @@ static void free_work(gpf_ctx* c) {
   hipFree(c->d_hist);
   hipFree(c->d_flag);
   c->d_flag = nullptr;
+  hipFree(c->d_cflag);
+  c->d_cflag = nullptr;
+  hipFree(c->d_qbuf);
+  c->d_qbuf = nullptr;
+  hipFree(c->d_qcnt);
+  c->d_qcnt = nullptr;
   hipFree(c->d_part); hipFree(c->d_cnt);
   c->d_part = nullptr;
   c->d_cnt = nullptr;
@@ -199,7 +208,8 @@ static void free_work(gpf_ctx* c) {
 
 static size_t bytes_per_particle(const gpf_ctx* c) {
   const size_t np = (size_t)c->Npad;
-  return 2 * np * np * 8 + (2 * (size_t)c->nt * np + 3 * np) * 8 + (size_t)(c->K + 1) * 4 + 64 * 8;
+  return 2 * np * np * 8 + (2 * (size_t)c->nt * np + 3 * np) * 8 + (size_t)(c->K + 1) * 4 + 64 * 8 +
+         (size_t)gpf::QSTRIDE * 8 + gpf::QCNT * 4 + 4;
 }
 
 // Chunk capacity from free HBM (GPF_MAX_CHUNK caps it, GPF_MEM_FRACTION scales the budget).
@@ -230,6 +240,10 @@ static int ensure_work(gpf_ctx* c, int want) {
   GPF_HIP(c, hipMalloc(&c->d_loss, (size_t)cap * 8));
   GPF_HIP(c, hipMalloc(&c->d_info, (size_t)cap * 4));
   GPF_HIP(c, hipMalloc(&c->d_flag, (size_t)cap * 4));  // reset by k_build_cov at every factorisation
+  GPF_HIP(c, hipMalloc(&c->d_cflag, (size_t)cap * 4));  // likewise
+  GPF_HIP(c, hipMalloc(&c->d_qbuf, (size_t)cap * gpf::QSTRIDE * 8));
+  GPF_HIP(c, hipMalloc(&c->d_qcnt, (size_t)cap * gpf::QCNT * 4));
+  GPF_HIP(c, hipMemsetAsync(c->d_qcnt, 0, (size_t)cap * gpf::QCNT * 4, c->stream));  // second arrivers re-zero
   GPF_HIP(c, hipMalloc(&c->d_hist, (size_t)cap * (c->K + 1) * 4));
   // on the library stream: the legacy null stream does not order against our non-blocking streams
   GPF_HIP(c, hipMemsetAsync(c->d_hist, 0, (size_t)cap * (c->K + 1) * 4, c->stream));  // k_score re-zeroes what it read
@@ -290,6 +304,15 @@ static bool early_diag(int pc, int nt) {
   return on && nt > 1;
 }
 
+// Quadrant finish of the critical tile (gpf::quad_item) in the launches with the early diagonal
+// factor: its triangular multiply and rank-128 update run on four extra workgroups per particle
+// instead of the one that completes the tile's GEMM. GPF_QUAD = 0 turns it off.
+static bool quad_finish(int pc, int nt) {
+  bool on = true;
+  if (const char* s = getenv("GPF_QUAD")) on = atoi(s) != 0;
+  return on && GPF_KFUSE && early_diag(pc, nt);
+}
+
 // Critical-tile split of block-column launch J (gpf::SPLIT_CRIT), for launches that leave
 // workgroup slots idle (small N: the launch time is the latency of the tile I = J+1, which runs
 // the depth-128J GEMM, the look-ahead update and the next diagonal factor in sequence): that
@@ -302,7 +325,8 @@ static bool early_diag(int pc, int nt) {
 static int split_crit(int pc, int nt, int J, int grp, int S_all) {
   // the last launch (J = nt-1) has no L tiles: its w = 0 is a U tile, which never splits
   if (S_all > 1 || grp > 0 || J == 0 || J >= nt - 1 || nt < 4 || !GPF_KFUSE) return 1;
-  const int slots = 512, tiles = pc * (nt - 1) + (early_diag(pc, nt) ? pc : 0);  // + the diagonal workgroups
+  // + the diagonal and the quadrant workgroups
+  const int slots = 512, tiles = pc * (nt - 1) + (early_diag(pc, nt) ? pc : 0) + (quad_finish(pc, nt) ? 4 * pc : 0);
   int S = 4, minch = 16;
   if (const char* s = getenv("GPF_SPLIT_CRIT")) S = std::max(1, std::min(32, atoi(s)));
   if (const char* s = getenv("GPF_SPLIT_CRIT_MIN")) minch = std::max(2, atoi(s));
@@ -360,6 +384,7 @@ static int split_plan(gpf_ctx* c, int pc, int& S, int& Smax) {
 // d_part / d_cnt). run_factor launches exactly this list; gpf_plan_check verifies it on the host.
 struct StepLaunch {
   int J, g, p0, gc, split, S, grp, ed;  // ed: the launch starts with gc diagonal workgroups
+  int qf;                               // qf: ... and ends with 4 gc quadrant workgroups
   unsigned grid;
   size_t part_off, cnt_off;
 };
@@ -367,7 +392,7 @@ struct StepLaunch {
 static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& out) {
   out.clear();
   const int ng = num_groups(pc, nt);
-  const bool ed = early_diag(pc, nt);
+  const bool ed = early_diag(pc, nt), qf = quad_finish(pc, nt);
   // block columns interleaved across groups so every stream has work queued early
   for (int J = 0; nt > 1 && J < nt; ++J) {
     for (int g = 0; g < ng; ++g) {
@@ -381,7 +406,8 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
       l.S = S > 1 ? S : Sc;  // pieces per split tile in this launch
       l.split = S > 1 ? gpf::SPLIT_ALL : Sc > 1 ? gpf::SPLIT_CRIT : gpf::SPLIT_NONE;
       l.ed = ed ? 1 : 0;
-      l.grid = (S > 1 ? l.gc * (nt - 1) * S : l.gc * (nt - 1) + l.gc * (Sc - 1)) + (l.ed ? l.gc : 0);
+      l.qf = (qf && J < nt - 1) ? 1 : 0;  // the last launch has no L tiles
+      l.grid = (S > 1 ? l.gc * (nt - 1) * S : l.gc * (nt - 1) + l.gc * (Sc - 1)) + (l.ed ? l.gc : 0) + (l.qf ? 4 * l.gc : 0);
       // one set of partial slots per group: groups run concurrently
       l.part_off = (size_t)l.p0 * (nt - 1) * Smax * T * T;
       l.cnt_off = (size_t)l.p0 * (nt - 1) * gpf::SPLIT_CNT;
@@ -448,7 +474,7 @@ static int run_factor(gpf_ctx* c, int pc) {
     const int nbuild = (GPF_KFUSE && nt > 1) ? 3 * nt : ntri;
     int rc = launch_on(c, st, PC_BUILD, 8.0 * nbuild * BT * BT * (double)gc, [&] {
       hipLaunchKernelGGL(gpf::k_build_cov, dim3(nbuild, gc), dim3(NTHR), 0, st, N, Np, c->d, c->d_x, c->d_y, c->d_e,
-                         lsg, Lg, yg, ig, (int)(nbuild != ntri), c->d_flag + p0);
+                         lsg, Lg, yg, ig, (int)(nbuild != ntri), c->d_flag + p0, c->d_cflag + p0);
     });
     if (rc) return rc;
     if (ed) continue;  // block 0 is factored by launch 0's diagonal workgroups
@@ -476,7 +502,9 @@ static int run_factor(gpf_ctx* c, int pc) {
       hipLaunchKernelGGL(kern, dim3(l.grid), dim3(gpf::STEP_NTH), 0, st, l.J, nt, Np, c->d_L + (size_t)p0 * ld * ld,
                          c->d_U + (size_t)p0 * ld * ld, c->d_yb + (size_t)p0 * ld, c->d_s2p + (size_t)p0 * nt * ld,
                          c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc, l.grp, N, c->d_x,
-                         c->d_ls + (size_t)p0 * c->d, c->d, l.S, partg, cntg, c->d_flag + p0, l.ed);
+                         c->d_ls + (size_t)p0 * c->d, c->d, l.S, partg, cntg, c->d_flag + p0, l.ed,
+                         c->d_cflag + p0, c->d_qbuf + (size_t)p0 * gpf::QSTRIDE, c->d_qcnt + (size_t)p0 * gpf::QCNT,
+                         l.qf);
     });
     if (rc) return rc;
     total += fl * gc;
@@ -958,8 +986,8 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
   // be disjoint (within a group the launches are ordered on its stream)
   std::vector<size_t> plo(MAX_GROUPS, SIZE_MAX), phi(MAX_GROUPS, 0), clo(MAX_GROUPS, SIZE_MAX), chi(MAX_GROUPS, 0);
   long long wgs = 0, whole_tiles = 0, split_tiles = 0;
-  std::vector<int> whole, piece, diag;
-  long long diag_wgs = 0;
+  std::vector<int> whole, piece, diag, quad;
+  long long diag_wgs = 0, quad_wgs = 0;
   if ((int)plan.size() != (nt > 1 ? nt * ng : 0)) return plan_fail(msg, msg_len, "plan has %d launches, want %d",
                                                               (int)plan.size(), nt * ng);
   for (const StepLaunch& l : plan) {
@@ -971,18 +999,29 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     whole.assign((size_t)tiles, 0);
     piece.assign((size_t)tiles * l.S, 0);
     diag.assign((size_t)l.gc, 0);
+    quad.assign((size_t)l.gc * 4, 0);
+    const unsigned qbase = l.grid - (l.qf ? 4u * l.gc : 0u);
+    if (l.qf && (!l.ed || l.J >= nt - 1)) return plan_fail(msg, msg_len, "J=%d: quadrant finish without its inputs", l.J);
     for (unsigned b = 0; b < l.grid; ++b) {
       int p = -1, w = -1, sidx = -1;
       const int role =
-          l.split == gpf::SPLIT_ALL    ? gpf::step_decode<gpf::SPLIT_ALL>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, p, w, sidx)
-          : l.split == gpf::SPLIT_CRIT ? gpf::step_decode<gpf::SPLIT_CRIT>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, p, w, sidx)
-                                       : gpf::step_decode<gpf::SPLIT_NONE>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, p, w, sidx);
+          l.split == gpf::SPLIT_ALL    ? gpf::step_decode<gpf::SPLIT_ALL>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.qf, p, w, sidx)
+          : l.split == gpf::SPLIT_CRIT ? gpf::step_decode<gpf::SPLIT_CRIT>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.qf, p, w, sidx)
+                                       : gpf::step_decode<gpf::SPLIT_NONE>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.qf, p, w, sidx);
       if (role == gpf::ROLE_DIAG) {  // one diagonal workgroup per particle, ahead of every tile of the launch
         if (!l.ed || p < 0 || p >= l.gc || (unsigned)p != b || diag[p]++)
           return plan_fail(msg, msg_len, "J=%d block %u: misplaced or duplicate diagonal workgroup (p=%d)", l.J, b, p);
         ++wgs;
         continue;
       }
+      if (role == gpf::ROLE_QUAD) {  // four per particle, after every other workgroup of the launch
+        if (!l.qf || p < 0 || p >= l.gc || sidx < 0 || sidx > 3 || b < qbase || quad[(size_t)p * 4 + sidx]++)
+          return plan_fail(msg, msg_len, "J=%d block %u: misplaced or duplicate quadrant workgroup (p=%d q=%d)", l.J, b,
+                           p, sidx);
+        ++wgs;
+        continue;
+      }
+      if (b >= qbase) return plan_fail(msg, msg_len, "J=%d block %u: a tile behind the quadrant workgroups", l.J, b);
       if (p < 0 || p >= l.gc || w < 0 || w >= ntl || sidx < 0 || sidx >= l.S)
         return plan_fail(msg, msg_len, "J=%d block %u decodes out of range (p=%d w=%d)", l.J, b, p, w);
       const int t = p * ntl + w;
@@ -1010,6 +1049,10 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     for (int q = 0; q < l.gc; ++q) {
       if (diag[q] != l.ed) return plan_fail(msg, msg_len, "J=%d particle %d: %d diagonal workgroups", l.J, q, diag[q]);
       diag_wgs += diag[q];
+      for (int k = 0; k < 4; ++k)
+        if (quad[(size_t)q * 4 + k] != l.qf)
+          return plan_fail(msg, msg_len, "J=%d particle %d: quadrant %d run %d times", l.J, q, k, quad[(size_t)q * 4 + k]);
+      quad_wgs += 4 * l.qf;
     }
     for (int t = 0; t < tiles; ++t) {
       int np = 0;
@@ -1038,6 +1081,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     stats[5] = Smax;
     stats[6] = ng;
     stats[7] = diag_wgs;
+    stats[8] = quad_wgs;
   }
   return GPF_OK;
 }

@@ -100,12 +100,13 @@ def plan_check(particles, nt):
     """Host-side check of the k_step dispatch plan (gpf_plan_check); raises AssertionError
     naming the first violation, else returns the stats dict. Reads the GPF_* environment."""
     lib = load_library()
-    stats = (ctypes.c_longlong * 8)()
+    stats = (ctypes.c_longlong * 9)()
     msg = ctypes.create_string_buffer(256)
     rc = lib.gpf_plan_check(int(particles), int(nt), stats, msg, 256)
     if rc != GPF_OK:
         raise AssertionError(f"plan_check(pc={particles}, nt={nt}): {msg.value.decode()}")
-    keys = ("launches", "workgroups", "whole_tiles", "split_tiles", "S", "Smax", "groups", "diag_workgroups")
+    keys = ("launches", "workgroups", "whole_tiles", "split_tiles", "S", "Smax", "groups", "diag_workgroups",
+            "quad_workgroups")
     return dict(zip(keys, list(stats)))
 
 

@@ -198,9 +198,12 @@ const char* gpf_build_info(void);
  * on a zeroed counter elect exactly one finisher), that pieces stay inside the split-K buffers,
  * and that concurrent particle groups never share partial slots or counters.
  * With the early diagonal factor it also checks that every launch starts with exactly one
- * diagonal workgroup per particle, ahead of all tiles.
- * stats (nullable, 8 entries): launches, workgroups, whole tiles, split tiles, S (all-tile
- * split factor), largest split factor, particle groups, diagonal workgroups. Returns GPF_OK, or
+ * diagonal workgroup per particle, ahead of all tiles, and with the quadrant finish of the
+ * critical tile that every launch but the last ends with exactly four quadrant workgroups per
+ * particle, behind all tiles.
+ * stats (nullable, 9 entries): launches, workgroups, whole tiles, split tiles, S (all-tile
+ * split factor), largest split factor, particle groups, diagonal workgroups, quadrant
+ * workgroups. Returns GPF_OK, or
  * GPF_BAD_ARG with a description of the first violation in msg. */
 int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len);
 

@@ -27,13 +27,15 @@ ENVS = [
     {"GPF_STEP_GROUP": "1"}, {"GPF_STEP_GROUP": "2", "GPF_GROUPS": "2"},
     {"GPF_EARLY_DIAG": "1"}, {"GPF_EARLY_DIAG": "0"},
     {"GPF_EARLY_DIAG": "1", "GPF_SPLIT_CRIT": "8", "GPF_SPLIT_CRIT_MIN": "2", "GPF_GROUPS": "3"},
+    {"GPF_QUAD": "0"}, {"GPF_QUAD": "0", "GPF_EARLY_DIAG": "1"},
 ]
 
 
 @pytest.fixture
 def env(monkeypatch):
     def apply(kv):
-        for k in ("GPF_GROUPS", "GPF_SPLIT_K", "GPF_SPLIT_CRIT", "GPF_SPLIT_CRIT_MIN", "GPF_STEP_GROUP", "GPF_EARLY_DIAG"):
+        for k in ("GPF_GROUPS", "GPF_SPLIT_K", "GPF_SPLIT_CRIT", "GPF_SPLIT_CRIT_MIN", "GPF_STEP_GROUP", "GPF_EARLY_DIAG",
+                  "GPF_QUAD"):
             monkeypatch.delenv(k, raising=False)
         for k, v in kv.items():
             monkeypatch.setenv(k, v)
@@ -53,6 +55,9 @@ def test_every_tile_has_exactly_one_finisher(env, kv):
             assert st["whole_tiles"] + st["split_tiles"] == pc * (nt - 1) * nt  # every (J, p, w)
             # early diagonal factor: one diagonal workgroup per particle in every launch
             assert st["diag_workgroups"] in (0, pc * nt if nt > 1 else 0)
+            # quadrant finish: four workgroups per particle in every launch but the last
+            assert st["quad_workgroups"] in (0, 4 * pc * (nt - 1))
+            assert st["quad_workgroups"] == 0 or st["diag_workgroups"] > 0
             seen_split += st["split_tiles"] > 0
             seen_groups += st["groups"] > 1
     if kv.get("GPF_SPLIT_K") or kv.get("GPF_SPLIT_CRIT") or not kv:
@@ -79,6 +84,9 @@ def test_default_plans_of_the_baseline_configs(env):
     assert e["diag_workgroups"] == 0
     assert (c["diag_workgroups"], d["diag_workgroups"]) == (0, 0)
     assert b["diag_workgroups"] == 32 * 8 and one["diag_workgroups"] == 32
+    # quadrant finish of the critical tile wherever the diagonal factor runs early
+    assert b["quad_workgroups"] == 4 * 32 * 7 and one["quad_workgroups"] == 4 * 31
+    assert (c["quad_workgroups"], d["quad_workgroups"], e["quad_workgroups"]) == (0, 0, 0)
 
 
 def test_early_diag_override(env):
@@ -86,6 +94,13 @@ def test_early_diag_override(env):
     assert gpfit.plan_check(64, 32)["diag_workgroups"] == 64 * 32
     env({"GPF_EARLY_DIAG": "0"})
     assert gpfit.plan_check(32, 8)["diag_workgroups"] == 0
+
+
+def test_quad_override(env):
+    env({"GPF_QUAD": "0"})
+    assert gpfit.plan_check(32, 8)["quad_workgroups"] == 0
+    env({"GPF_EARLY_DIAG": "1"})
+    assert gpfit.plan_check(64, 32)["quad_workgroups"] == 4 * 64 * 31
 
 
 def test_env_is_read_per_call(env):
