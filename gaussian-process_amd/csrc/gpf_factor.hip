@@ -945,7 +945,8 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
                                           const double* __restrict__ ls, int d, int S, int sidx,
                                           double* __restrict__ part, unsigned* __restrict__ cnt, int* sflag,
                                           const int* __restrict__ dflag, int* __restrict__ cflag,
-                                          double* __restrict__ qbuf, int qf, double* smem, double* small) {
+                                          double* __restrict__ qbuf, int qf, int deep, double* smem,
+                                          double* small) {
   const int tid = threadIdx.x;
   const int nL = nt - 1 - J;
   const size_t ld = (size_t)Npad;
@@ -1010,10 +1011,25 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
       const int c = qd.lane & 15;
       scratch[(qd.cb / 32) * T + qd.rb + 16 * (c >> 2) + (qd.lane >> 4) + 4 * (c & 3)] = acc_row_dot(acc, qd, zj);
     }
-    // look-ahead: A_II -= L_IJ L_IJ^T (the full tile; only its lower half is ever read)
-    acc.load(qd, Aii, ld);
-    step_gemm<false, true, TRI_C_LOWER>(acc, Aij, Npad, Aij, Npad, T, smem, qd);
-    acc.store(qd, Aii, ld);
+    if (!ED && deep) {
+      // deep update: A_II -= L_I,<=J L_I,<=J^T in one depth-128(J+1) GEMM by the critical tile
+      // only (A_II has not been touched since the K build); the other tiles skip the update. The
+      // additions run in the same order as the per-launch look-ahead's (k ascending, one MFMA k-step
+      // at a time, the exact fp64 store/load between launches dropped): bitwise the same A_II.
+      if (I == J + 1) {
+        acc.load(qd, Aii, ld);
+        step_gemm<false, true, TRI_C_LOWER>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)I * T * ld, Npad,
+                                            (J + 1) * T, smem, qd);
+        acc.store(qd, Aii, ld);
+      } else {
+        __syncthreads();
+      }
+    } else {
+      // look-ahead: A_II -= L_IJ L_IJ^T (the full tile; only its lower half is ever read)
+      acc.load(qd, Aii, ld);
+      step_gemm<false, true, TRI_C_LOWER>(acc, Aij, Npad, Aij, Npad, T, smem, qd);
+      acc.store(qd, Aii, ld);
+    }
     GPF_PHASE(2);
     if (tid < T)  // (the SYRK's barriers ordered the scratch writes)
       yp[I * T + tid] =
@@ -1106,7 +1122,7 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
                                                   int d, int S, double* __restrict__ part,
                                                   unsigned* __restrict__ cnt, int* __restrict__ dflag, int ed,
                                                   int* __restrict__ cflag, double* __restrict__ qbuf,
-                                                  unsigned* __restrict__ qcnt, int qf) {
+                                                  unsigned* __restrict__ qcnt, int qf, int deep) {
   const int tid = threadIdx.x;
 #ifdef GPF_WG_TRACE
   if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) {
@@ -1140,7 +1156,7 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
     if (tid == 0) __hip_atomic_store(dflag + p, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
     step_item<SPLIT, ED>(role, J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, sidx, part, cnt, &sflag,
-                         dflag, cflag, qbuf, ED && qf, smem, small);
+                         dflag, cflag, qbuf, ED && qf, deep, smem, small);
   }
 #ifdef GPF_WG_TRACE
   __syncthreads();

@@ -306,11 +306,29 @@ static bool early_diag(int pc, int nt) {
 
 // Quadrant finish of the critical tile (gpf::quad_item) in the launches with the early diagonal
 // factor: its triangular multiply and rank-128 update run on four extra workgroups per particle
-// instead of the one that completes the tile's GEMM. GPF_QUAD = 0 turns it off.
+// instead of the one that completes the tile's GEMM. Off by default (GPF_QUAD = 1 turns it on):
+// the extra hand-offs (C published write-through, two ticket levels, the partial updates read
+// back) cost more than the shorter chain saves — config B -8%, prediction factor -2%
+// (profiles/r2/quad_finish_ab_rejected.txt).
 static bool quad_finish(int pc, int nt) {
-  bool on = true;
+  bool on = false;
   if (const char* s = getenv("GPF_QUAD")) on = atoi(s) != 0;
   return on && GPF_KFUSE && early_diag(pc, nt);
+}
+
+// Deep diagonal update in the launches with the fused diagonal factor (slot-bound: configs C, D,
+// E): instead of every L tile applying its rank-128 look-ahead A_II -= L_IJ L_IJ^T (a depth-128
+// GEMM plus a read-modify-write of the 128 KiB A_II per tile and launch), the critical tile of
+// launch J applies A_II -= L_I,<=J L_I,<=J^T as one depth-128(J+1) GEMM right before it factors
+// the block (gpf::step_item). Same additions in the same order: bitwise equal. Off by default
+// (GPF_DEEP_SYRK = 1 turns it on): it lengthens the critical tile's chain, which then outlasts
+// launches that are not deeply slot-bound or whose critical tiles start late behind the other
+// group's launch — same box: C +0.9%, D's 32-particle share -13%, E's share -2%
+// (profiles/r2/deep_syrk_ab_rejected.txt). Launches with the early diagonal factor always keep
+// the look-ahead.
+static bool deep_syrk() {
+  if (const char* s = getenv("GPF_DEEP_SYRK")) return atoi(s) != 0;
+  return false;
 }
 
 // Critical-tile split of block-column launch J (gpf::SPLIT_CRIT), for launches that leave
@@ -433,7 +451,7 @@ static int run_factor(gpf_ctx* c, int pc) {
   //   L tile: depth-128J GEMM 2 T^3 J + triangular multiply T^3 + look-ahead syrk share T^3
   //   U tile: depth-128(J-K) GEMM with a triangular factor 2 T^3 (J-K) - T^3 + triangular multiply T^3
   //   diagonal block: 2/3 T^3 (block J+1 fused at the end of launch J, or block J early in it)
-  const bool ed = early_diag(pc, nt);
+  const bool ed = early_diag(pc, nt), deep = deep_syrk();
   auto step_flops = [&](int J) {
     double fl = 0.0;
     for (int w = 0; w < nt - 1; ++w) {
@@ -504,7 +522,7 @@ static int run_factor(gpf_ctx* c, int pc) {
                          c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc, l.grp, N, c->d_x,
                          c->d_ls + (size_t)p0 * c->d, c->d, l.S, partg, cntg, c->d_flag + p0, l.ed,
                          c->d_cflag + p0, c->d_qbuf + (size_t)p0 * gpf::QSTRIDE, c->d_qcnt + (size_t)p0 * gpf::QCNT,
-                         l.qf);
+                         l.qf, (int)(!ed && deep));
     });
     if (rc) return rc;
     total += fl * gc;

@@ -1,0 +1,284 @@
+// Feasibility probe (not product code): fp64-accurate GEMM emulated on the int8 matrix cores
+// (Ozaki-style fixed-point slicing), the "next" item of DESIGN.md §8.
+//
+//   C = A B^T, A [M][K], B [N][K] fp64 with entries bounded by 2^ea, 2^eb (the factor's L and
+//   U = L^-1 are: |L_ij| <= sqrt(1 + e_i^2), ||U||_2 <= 1 / min e). Each matrix is cut into S
+//   int8 digit planes, a = 2^(ea+1) sum_s d_s 2^(-7(s+1)), |d_s| <= 64 (round-to-nearest digits),
+//   and C = 2^(ea+eb+2) sum_{s+t<S} 2^(-7(s+t+2)) (D^A_s D^B_t^T): every digit product is exact in
+//   the int32 accumulators; products of equal weight (s + t = g) share one accumulator, S of them.
+//
+// Parts: (1) the v_mfma_i32_32x32x32_i8 operand map, checked with exact integers; (2) GEMM
+// throughput (fp64-equivalent TF/s) with digit planes streamed from HBM; (3) accuracy against a
+// long-double reference next to a plain fp64 GEMM of the same data.
+//
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/probes/ozaki_core.hip -o /tmp/ozaki_core
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#define CK(x)                                                                      \
+  do {                                                                             \
+    hipError_t e_ = (x);                                                           \
+    if (e_ != hipSuccess) {                                                        \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                     \
+    }                                                                              \
+  } while (0)
+
+typedef int v4i __attribute__((ext_vector_type(4)));    // 16 int8 operands
+typedef int v16i __attribute__((ext_vector_type(16)));  // 32x32 int32 accumulator fragment
+
+#ifndef NS
+#define NS 7  // digit planes per operand
+#endif
+
+// ---- (1) operand map -------------------------------------------------------------------
+// hypothesis: lane l holds A[r = l & 31][k = 16 (l >> 5) + j] and B[k = 16 (l >> 5) + j][c = l & 31]
+// in byte j = 0..15; C/D: col = l & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (l >> 5).
+__global__ void k_map(const int8_t* A, const int8_t* B, int* C) {  // A [32][32] (r, k), B [32][32] (c, k)
+  const int l = threadIdx.x;
+  v4i a, b;
+  int8_t* pa = (int8_t*)&a;
+  int8_t* pb = (int8_t*)&b;
+  for (int j = 0; j < 16; ++j) {
+    pa[j] = A[(l & 31) * 32 + 16 * (l >> 5) + j];
+    pb[j] = B[(l & 31) * 32 + 16 * (l >> 5) + j];
+  }
+  v16i acc = {};
+  acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc, 0, 0, 0);
+  for (int r = 0; r < 16; ++r) C[((r & 3) + 8 * (r >> 2) + 4 * (l >> 5)) * 32 + (l & 31)] = acc[r];
+}
+
+// ---- (2)/(3) GEMM ----------------------------------------------------------------------
+// Planes: A [NS][M][K], B [NS][N][K] int8, K contiguous. Workgroup tile 128 x 64, four waves
+// (one per SIMD), wave w: rows 32w..32w+31, two 32x32 column blocks. NS (NS+1)/2 digit
+// products per pair of fragments, NS int32 accumulators per output element.
+__global__ __launch_bounds__(256, 1) void k_ozaki(const int8_t* __restrict__ Ap, const int8_t* __restrict__ Bp,
+                                                 int M, int N, int K, double* __restrict__ C, int ea, int eb) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int mt = M / 128;
+  const int tm = blockIdx.x % mt, tn = blockIdx.x / mt;
+  const int kh = 16 * (l >> 5);
+  const int8_t* pa = Ap + (size_t)(tm * 128 + 32 * w + (l & 31)) * K + kh;
+  const int8_t* pb = Bp + (size_t)(tn * 64 + (l & 31)) * K + kh;
+  const size_t sa = (size_t)M * K, sb = (size_t)N * K;
+  v16i acc[NS][2];
+#pragma unroll
+  for (int g = 0; g < NS; ++g) acc[g][0] = acc[g][1] = v16i{};
+  v4i a[NS], b[NS][2];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    a[s] = *(const v4i*)(pa + s * sa);
+    b[s][0] = *(const v4i*)(pb + s * sb);
+    b[s][1] = *(const v4i*)(pb + s * sb + (size_t)32 * K);
+  }
+  for (int k0 = 0; k0 < K; k0 += 32) {
+    v4i an[NS], bn[NS][2];
+    const int kn = (k0 + 32 < K) ? k0 + 32 : k0;  // prefetch the next k-step (the last reloads)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      an[s] = *(const v4i*)(pa + s * sa + kn);
+      bn[s][0] = *(const v4i*)(pb + s * sb + kn);
+      bn[s][1] = *(const v4i*)(pb + s * sb + (size_t)32 * K + kn);
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int t = 0; t < NS - s; ++t) {
+        acc[s + t][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[s], b[t][0], acc[s + t][0], 0, 0, 0);
+        acc[s + t][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[s], b[t][1], acc[s + t][1], 0, 0, 0);
+      }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      a[s] = an[s];
+      b[s][0] = bn[s][0];
+      b[s][1] = bn[s][1];
+    }
+  }
+  // C = 2^(ea+eb+2) sum_g 2^(-7(g+2)) acc[g], smallest weight first
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      double v = 0.0;
+#pragma unroll
+      for (int g = NS - 1; g >= 0; --g) v = v + ldexp((double)acc[g][nb][r], -7 * (g + 2));
+      const int row = tm * 128 + 32 * w + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+      const int col = tn * 64 + nb * 32 + (l & 31);
+      C[(size_t)row * N + col] = ldexp(v, ea + eb + 2);
+    }
+}
+
+// plain fp64 GEMM C = A B^T on the FP64 MFMA (v_mfma_f64_16x16x4), operands from global: the
+// accuracy comparison's fp64 arm (same data, same sums), not a tuned kernel
+__global__ void k_f64(const double* A, const double* B, int M, int N, int K, double* C) {
+  const int l = threadIdx.x & 63;
+  const int row0 = blockIdx.x * 16, col0 = blockIdx.y * 16;
+  typedef double v4d __attribute__((ext_vector_type(4)));
+  v4d acc = {};
+  for (int k = 0; k < K; k += 4) {
+    const double a = A[(size_t)(row0 + (l & 15)) * K + k + (l >> 4)];
+    const double b = B[(size_t)(col0 + (l & 15)) * K + k + (l >> 4)];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+  for (int r = 0; r < 4; ++r) C[(size_t)(row0 + (l >> 4) + 4 * r) * N + col0 + (l & 15)] = acc[r];
+}
+
+static int exp_bound(const std::vector<double>& a) {
+  double m = 0;
+  for (double v : a) m = std::max(m, std::fabs(v));
+  int e;
+  std::frexp(m, &e);  // m < 2^e
+  return e;
+}
+
+// digits of a / 2^(e+1) (|.| <= 1/2): NS planes, round to nearest, |d| <= 64
+static void slice(const std::vector<double>& a, int e, int rows, int K, std::vector<int8_t>& planes) {
+  planes.assign((size_t)NS * rows * K, 0);
+  for (size_t i = 0; i < (size_t)rows * K; ++i) {
+    double r = std::ldexp(a[i], -(e + 1));
+    for (int s = 0; s < NS; ++s) {
+      r = r * 128.0;
+      const double d = std::nearbyint(r);
+      r -= d;
+      planes[(size_t)s * rows * K + i] = (int8_t)d;
+    }
+  }
+}
+
+// lower-triangular factor-like data: Cholesky of an SE covariance of sorted points + noise
+static std::vector<double> factor_like(int n, double ell, double noise, std::mt19937_64& g) {
+  std::uniform_real_distribution<double> u(0, 1);
+  std::vector<double> t(n), A((size_t)n * n), L((size_t)n * n, 0.0);
+  for (auto& v : t) v = u(g);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) A[(size_t)i * n + j] = std::exp(-0.5 * (t[i] - t[j]) * (t[i] - t[j]) / (ell * ell)) + (i == j ? noise * noise : 0.0);
+  for (int j = 0; j < n; ++j) {
+    double d = A[(size_t)j * n + j];
+    for (int k = 0; k < j; ++k) d -= L[(size_t)j * n + k] * L[(size_t)j * n + k];
+    d = std::sqrt(d);
+    L[(size_t)j * n + j] = d;
+    for (int i = j + 1; i < n; ++i) {
+      double s = A[(size_t)i * n + j];
+      for (int k = 0; k < j; ++k) s -= L[(size_t)i * n + k] * L[(size_t)j * n + k];
+      L[(size_t)i * n + j] = s / d;
+    }
+  }
+  return L;
+}
+
+int main(int argc, char** argv) {
+  // ---- (1) map
+  {
+    std::mt19937_64 g(1);
+    std::uniform_int_distribution<int> u(-100, 100);
+    std::vector<int8_t> A(1024), B(1024);
+    for (auto& v : A) v = (int8_t)u(g);
+    for (auto& v : B) v = (int8_t)u(g);
+    int8_t *dA, *dB;
+    int* dC;
+    CK(hipMalloc(&dA, 1024));
+    CK(hipMalloc(&dB, 1024));
+    CK(hipMalloc(&dC, 4096));
+    CK(hipMemcpy(dA, A.data(), 1024, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dB, B.data(), 1024, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_map, dim3(1), dim3(64), 0, 0, dA, dB, dC);
+    std::vector<int> C(1024);
+    CK(hipMemcpy(C.data(), dC, 4096, hipMemcpyDeviceToHost));
+    int bad = 0;
+    for (int r = 0; r < 32; ++r)
+      for (int c = 0; c < 32; ++c) {
+        int s = 0;
+        for (int k = 0; k < 32; ++k) s += A[r * 32 + k] * B[c * 32 + k];
+        bad += s != C[r * 32 + c];
+      }
+    printf("map: %d of 1024 entries differ from A B^T (0 = operand map confirmed)\n", bad);
+    if (bad) return 2;
+  }
+  // ---- (3) accuracy: L-like operands, C = L1 L2^T over K
+  {
+    const int M = 256, N = 128, K = 1024;
+    std::mt19937_64 g(7);
+    const std::vector<double> L1 = factor_like(K, 0.3, 0.1, g);
+    const std::vector<double> L2 = factor_like(K, 0.5, 0.1, g);
+    std::vector<double> A((size_t)M * K), B((size_t)N * K);
+    for (int i = 0; i < M; ++i)
+      for (int k = 0; k < K; ++k) A[(size_t)i * K + k] = L1[(size_t)(K - M + i) * K + k];
+    for (int i = 0; i < N; ++i)
+      for (int k = 0; k < K; ++k) B[(size_t)i * K + k] = L2[(size_t)(K - N - 64 + i) * K + k];
+    const int ea = exp_bound(A), eb = exp_bound(B);
+    std::vector<int8_t> pA, pB;
+    slice(A, ea, M, K, pA);
+    slice(B, eb, N, K, pB);
+    int8_t *dA, *dB;
+    double *dC, *dF, *dAd, *dBd;
+    CK(hipMalloc(&dA, pA.size()));
+    CK(hipMalloc(&dB, pB.size()));
+    CK(hipMalloc(&dC, (size_t)M * N * 8));
+    CK(hipMalloc(&dF, (size_t)M * N * 8));
+    CK(hipMalloc(&dAd, A.size() * 8));
+    CK(hipMalloc(&dBd, B.size() * 8));
+    CK(hipMemcpy(dA, pA.data(), pA.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(dB, pB.data(), pB.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(dAd, A.data(), A.size() * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dBd, B.data(), B.size() * 8, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_ozaki, dim3((M / 128) * (N / 64)), dim3(256), 0, 0, dA, dB, M, N, K, dC, ea, eb);
+    hipLaunchKernelGGL(k_f64, dim3(M / 16, N / 16), dim3(64), 0, 0, dAd, dBd, M, N, K, dF);
+    CK(hipDeviceSynchronize());
+    std::vector<double> Co((size_t)M * N), Cf((size_t)M * N);
+    CK(hipMemcpy(Co.data(), dC, Co.size() * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(Cf.data(), dF, Cf.size() * 8, hipMemcpyDeviceToHost));
+    double eo = 0, ef = 0, cmax = 0, rowabs = 0;
+    for (int i = 0; i < M; ++i)
+      for (int j = 0; j < N; ++j) {
+        long double s = 0, sa = 0;
+        for (int k = 0; k < K; ++k) {
+          s += (long double)A[(size_t)i * K + k] * B[(size_t)j * K + k];
+          sa += std::fabs((long double)A[(size_t)i * K + k] * B[(size_t)j * K + k]);
+        }
+        eo = std::max(eo, (double)std::fabs((long double)Co[(size_t)i * N + j] - s));
+        ef = std::max(ef, (double)std::fabs((long double)Cf[(size_t)i * N + j] - s));
+        cmax = std::max(cmax, (double)std::fabs(s));
+        rowabs = std::max(rowabs, (double)sa);
+      }
+    printf("accuracy (M=%d N=%d K=%d, factor-like operands, NS=%d digit planes): max|C-C_exact| ozaki %.3e  fp64 MFMA %.3e"
+           "  (max|C| %.3e, max sum|a b| %.3e)\n", M, N, K, NS, eo, ef, cmax, rowabs);
+    CK(hipFree(dA)); CK(hipFree(dB)); CK(hipFree(dC)); CK(hipFree(dF)); CK(hipFree(dAd)); CK(hipFree(dBd));
+  }
+  // ---- (2) throughput
+  {
+    const int M = 8192, N = 4096, K = argc > 1 ? atoi(argv[1]) : 2048;
+    int8_t *dA, *dB;
+    double* dC;
+    CK(hipMalloc(&dA, (size_t)NS * M * K));
+    CK(hipMalloc(&dB, (size_t)NS * N * K));
+    CK(hipMalloc(&dC, (size_t)M * N * 8));
+    CK(hipMemset(dA, 3, (size_t)NS * M * K));
+    CK(hipMemset(dB, 5, (size_t)NS * N * K));
+    const int grid = (M / 128) * (N / 64);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int w = 0; w < 2; ++w) hipLaunchKernelGGL(k_ozaki, dim3(grid), dim3(256), 0, 0, dA, dB, M, N, K, dC, 0, 0);
+    const int reps = 10;
+    CK(hipEventRecord(e0));
+    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k_ozaki, dim3(grid), dim3(256), 0, 0, dA, dB, M, N, K, dC, 0, 0);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= reps;
+    const double fl = 2.0 * M * N * K;
+    const double prods = NS * (NS + 1) / 2;
+    printf("throughput (M=%d N=%d K=%d, %d workgroups, %g digit products): %.3f ms  fp64-equivalent %.1f TF/s  int8 %.0f TOP/s"
+           "  planes streamed %.2f TB/s\n", M, N, K, grid, prods, ms, fl / ms * 1e-9, fl * prods / ms * 1e-9,
+           (double)NS * K * (128 + 64) * grid / ms * 1e-9);
+  }
+  return 0;
+}

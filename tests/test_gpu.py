@@ -551,12 +551,14 @@ def test_early_diagonal_factor_matches_fused(ctx, monkeypatch, N, d, P):
     start of launch J and handed to the tiles through a flag) against the fused factor at the end
     of the previous launch's critical tile: the same arithmetic, so bitwise equal scores, mean
     and sd, on the critical-split (N=1000), unsplit and all-tile-split (one particle) paths; and
-    the factor itself bitwise equal for the prediction path. With the quadrant finish of the
-    critical tile on (its default with the early factor: the triangular multiply and the rank-128
-    update in 64-wide quadrants on four workgroups, the update summed per column half) the
-    rounding differs: mean/sd within 1e-8 of the fused path and the factor within 1e-8 normwise
-    (two fp64 evaluations of a system with condition numbers up to ~1e6), scores within
-    RTOL_LOSS or threshold ties."""
+    the factor itself bitwise equal for the prediction path. The fused path's deep diagonal
+    update (GPF_DEEP_SYRK = 1, off by default: the critical tile applies A_II -= L_I,<=J L_I,<=J^T
+    in one GEMM) runs the look-ahead's additions in the same order: bitwise equal to the
+    per-launch look-ahead. With the quadrant finish of the critical tile on (GPF_QUAD = 1, off by default:
+    the triangular multiply and the rank-128 update in 64-wide quadrants on four workgroups, the
+    update summed per column half) the rounding differs: mean/sd within 1e-8 of the fused path
+    and the factor within 1e-8 normwise (two fp64 evaluations of a system with condition numbers
+    up to ~1e6), scores within RTOL_LOSS or threshold ties."""
     rng = np.random.default_rng(N + P)
     x = rng.uniform(size=(d, N))
     y = np.sin(5 * x[0]) + 0.1 * rng.standard_normal(N)
@@ -567,24 +569,28 @@ def test_early_diagonal_factor_matches_fused(ctx, monkeypatch, N, d, P):
     ctx.set_grid(s, ex, lo, hi)
     Q = rng.uniform(0.1, 0.5, size=(P, d))
     out = {}
-    for mode, ed, qf in (("fused", "0", "0"), ("ed", "1", "0"), ("quad", "1", "1")):
+    for mode, ed, qf, deep in (("fused", "0", "0", "0"), ("fused_deep", "0", "0", "1"), ("ed", "1", "0", "0"),
+                               ("quad", "1", "1", "0")):
         monkeypatch.setenv("GPF_EARLY_DIAG", ed)
         monkeypatch.setenv("GPF_QUAD", qf)
+        monkeypatch.setenv("GPF_DEEP_SYRK", deep)
         out[mode] = ctx.eval_batch(Q, want_mu_sd=True)
         if P == 1:
             out[mode + "f"] = ctx.debug_factor(Q[0])
-    monkeypatch.delenv("GPF_EARLY_DIAG")
-    monkeypatch.delenv("GPF_QUAD")
-    for a, b in zip(out["fused"], out["ed"]):
-        np.testing.assert_array_equal(a, b)
+    for k in ("GPF_EARLY_DIAG", "GPF_QUAD", "GPF_DEEP_SYRK"):
+        monkeypatch.delenv(k)
+    for other in ("fused_deep", "ed"):
+        for a, b in zip(out["fused"], out[other]):
+            np.testing.assert_array_equal(a, b)
+        if P == 1:
+            for a, b in zip(out["fusedf"], out[other + "f"]):
+                np.testing.assert_array_equal(np.tril(a) if a.ndim == 2 else a, np.tril(b) if b.ndim == 2 else b)
     loss_f, mu_f, sd_f = out["fused"]
     loss_q, mu_q, sd_q = out["quad"]
     assert _rel(mu_q, mu_f) < 1e-8 and _rel(sd_q, sd_f) < 1e-8
     for k in range(P):
         assert_loss_or_ties(loss_q[k], loss_f[k], mu_f[k], sd_f[k], y, s, what=k)
     if P == 1:
-        for a, b in zip(out["fusedf"], out["edf"]):
-            np.testing.assert_array_equal(np.tril(a) if a.ndim == 2 else a, np.tril(b) if b.ndim == 2 else b)
         for a, b in zip(out["fusedf"], out["quadf"]):
             a, b = (np.tril(a), np.tril(b)) if a.ndim == 2 else (a, b)
             assert np.abs(a - b).max() <= 1e-8 * np.abs(a).max()

@@ -27,7 +27,8 @@ ENVS = [
     {"GPF_STEP_GROUP": "1"}, {"GPF_STEP_GROUP": "2", "GPF_GROUPS": "2"},
     {"GPF_EARLY_DIAG": "1"}, {"GPF_EARLY_DIAG": "0"},
     {"GPF_EARLY_DIAG": "1", "GPF_SPLIT_CRIT": "8", "GPF_SPLIT_CRIT_MIN": "2", "GPF_GROUPS": "3"},
-    {"GPF_QUAD": "0"}, {"GPF_QUAD": "0", "GPF_EARLY_DIAG": "1"},
+    {"GPF_QUAD": "1"}, {"GPF_QUAD": "1", "GPF_EARLY_DIAG": "1"},
+    {"GPF_QUAD": "1", "GPF_EARLY_DIAG": "1", "GPF_SPLIT_CRIT": "8", "GPF_SPLIT_CRIT_MIN": "2", "GPF_GROUPS": "2"},
 ]
 
 
@@ -84,9 +85,8 @@ def test_default_plans_of_the_baseline_configs(env):
     assert e["diag_workgroups"] == 0
     assert (c["diag_workgroups"], d["diag_workgroups"]) == (0, 0)
     assert b["diag_workgroups"] == 32 * 8 and one["diag_workgroups"] == 32
-    # quadrant finish of the critical tile wherever the diagonal factor runs early
-    assert b["quad_workgroups"] == 4 * 32 * 7 and one["quad_workgroups"] == 4 * 31
-    assert (c["quad_workgroups"], d["quad_workgroups"], e["quad_workgroups"]) == (0, 0, 0)
+    # quadrant finish of the critical tile: off by default (GPF_QUAD, profiles/r2/quad_finish_ab_rejected.txt)
+    assert all(x["quad_workgroups"] == 0 for x in (b, c, d, e, one))
 
 
 def test_early_diag_override(env):
@@ -97,9 +97,11 @@ def test_early_diag_override(env):
 
 
 def test_quad_override(env):
-    env({"GPF_QUAD": "0"})
-    assert gpfit.plan_check(32, 8)["quad_workgroups"] == 0
-    env({"GPF_EARLY_DIAG": "1"})
+    env({"GPF_QUAD": "1"})
+    assert gpfit.plan_check(32, 8)["quad_workgroups"] == 4 * 32 * 7
+    assert gpfit.plan_check(1, 32)["quad_workgroups"] == 4 * 31
+    assert gpfit.plan_check(64, 32)["quad_workgroups"] == 0  # only with the early diagonal factor
+    env({"GPF_QUAD": "1", "GPF_EARLY_DIAG": "1"})
     assert gpfit.plan_check(64, 32)["quad_workgroups"] == 4 * 64 * 31
 
 
