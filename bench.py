@@ -74,7 +74,8 @@ def pmc_traffic(N, d, swarm):
         except (OSError, ValueError):
             continue
         if t.get("N") == N and t.get("d") == d and t.get("swarm") == swarm:
-            best = {"bytes_per_launch": t["bytes_per_launch"], "source": str(f.relative_to(ROOT))}
+            best = {"bytes_per_launch": t["bytes_per_launch"], "source": str(f.relative_to(ROOT)),
+                    "groups": t.get("particle_groups", 1)}
     return best
 
 
@@ -427,6 +428,10 @@ def main():
             "unit": "TFLOP/s", "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
             "traffic": traffic["bytes_per_launch"] if traffic else None,
             "traffic_source": traffic["source"] if traffic else None,
+            # per k_step launch, like flops_per_launch: with particle groups a launch covers one
+            # group's particles (the PMC pass ran the same schedule)
+            "traffic_per": (f"k_step launch of one of {traffic['groups']} particle groups"
+                            if traffic and traffic["groups"] > 1 else "k_step launch") if traffic else None,
             "timing": timing, "particle_groups": groups,
             "gemm_core_tflops": core,
             "frac_of_gemm_core": (achieved / core) if (achieved and core) else None,

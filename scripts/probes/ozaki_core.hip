@@ -115,6 +115,112 @@ __global__ __launch_bounds__(256, 1) void k_ozaki(const int8_t* __restrict__ Ap,
     }
 }
 
+// LDS-staged version: each 32-deep k-step the workgroup stages its NS planes of A (128 rows) and
+// B (64 rows) in LDS (double-buffered, 48 KB per buffer at NS = 8; layout [plane][k half][row][16 B]
+// so that a fragment read is 64 consecutive 16-byte words: no bank conflicts), the global loads
+// of the next step are issued before the MFMAs of this one. swz: XCD-aware tile order (the
+// workgroups of one XCD take a contiguous range of tiles, 4 tile rows x 8 tile columns at a time).
+template <int R>
+__device__ __forceinline__ int lds_off(int s, int kh, int row) { return ((s * 2 + kh) * R + row) * 16; }
+
+__global__ __launch_bounds__(256, 1) void k_ozaki_lds(const int8_t* __restrict__ Ap, const int8_t* __restrict__ Bp,
+                                                     int M, int N, int K, double* __restrict__ C, int ea, int eb,
+                                                     int swz) {
+  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+  constexpr int BUF = NS * 2 * (128 + 64) * 16;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int mt = M / 128, ntn = N / 64;
+  int tm, tn;
+  if (swz) {
+    const int per = (mt * ntn) / 8;
+    const int t = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    tm = (t / (4 * ntn)) * 4 + (t % 4);
+    tn = (t / 4) % ntn;
+  } else {
+    tm = blockIdx.x % mt;
+    tn = blockIdx.x / mt;
+  }
+  const size_t sa = (size_t)M * K, sb = (size_t)N * K;
+  // staging map: chunk c = (plane, row, k half), k half fastest; A: NS*256 chunks, B: NS*128
+  constexpr int NA = NS * 256 / 256, NB = NS * 128 / 256;
+  const int8_t* ga[NA];
+  int la[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const int c = tid + 256 * j, sp = c / 256, row = (c % 256) / 2, kh = c & 1;
+    ga[j] = Ap + sp * sa + (size_t)(tm * 128 + row) * K + 16 * kh;
+    la[j] = lds_off<128>(sp, kh, row);
+  }
+  const int8_t* gb[NB];
+  int lb[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int c = tid + 256 * j, sp = c / 128, row = (c % 128) / 2, kh = c & 1;
+    gb[j] = Bp + sp * sb + (size_t)(tn * 64 + row) * K + 16 * kh;
+    lb[j] = NS * 2 * 128 * 16 + lds_off<64>(sp, kh, row);
+  }
+  v4i ra[NA], rb[NB];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) ra[j] = *(const v4i*)ga[j];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) rb[j] = *(const v4i*)gb[j];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) *(v4i*)(lds + la[j]) = ra[j];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) *(v4i*)(lds + lb[j]) = rb[j];
+  __syncthreads();
+  v16i acc[NS][2];
+#pragma unroll
+  for (int g = 0; g < NS; ++g) acc[g][0] = acc[g][1] = v16i{};
+  const int fa = lds_off<128>(0, l >> 5, 32 * w + (l & 31));
+  const int fb = NS * 2 * 128 * 16 + lds_off<64>(0, l >> 5, l & 31);
+  const int nsteps = K / 32;
+  for (int i = 0; i < nsteps; ++i) {
+    const int8_t* cur = lds + (i & 1) * BUF;
+    int8_t* nxt = lds + ((i + 1) & 1) * BUF;
+    const bool more = i + 1 < nsteps;
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < NA; ++j) ra[j] = *(const v4i*)(ga[j] + 32 * (i + 1));
+#pragma unroll
+      for (int j = 0; j < NB; ++j) rb[j] = *(const v4i*)(gb[j] + 32 * (i + 1));
+    }
+    v4i a[NS], b[NS][2];
+#pragma unroll
+    for (int sp = 0; sp < NS; ++sp) {
+      a[sp] = *(const v4i*)(cur + fa + sp * 2 * 128 * 16);
+      b[sp][0] = *(const v4i*)(cur + fb + sp * 2 * 64 * 16);
+      b[sp][1] = *(const v4i*)(cur + fb + sp * 2 * 64 * 16 + 32 * 16);
+    }
+#pragma unroll
+    for (int sp = 0; sp < NS; ++sp)
+#pragma unroll
+      for (int t = 0; t < NS - sp; ++t) {
+        acc[sp + t][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[sp], b[t][0], acc[sp + t][0], 0, 0, 0);
+        acc[sp + t][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[sp], b[t][1], acc[sp + t][1], 0, 0, 0);
+      }
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < NA; ++j) *(v4i*)(nxt + la[j]) = ra[j];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) *(v4i*)(nxt + lb[j]) = rb[j];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      double v = 0.0;
+#pragma unroll
+      for (int g = NS - 1; g >= 0; --g) v = v + ldexp((double)acc[g][nb][r], -7 * (g + 2));
+      const int row = tm * 128 + 32 * w + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+      const int col = tn * 64 + nb * 32 + (l & 31);
+      C[(size_t)row * N + col] = ldexp(v, ea + eb + 2);
+    }
+}
+constexpr int OZ_LDS = 2 * NS * 2 * (128 + 64) * 16;
+
 // MFMA ceiling of the same digit-product sequence: operands loaded once, K/32 k-steps of MFMAs
 // (no operand traffic), same epilogue
 __global__ __launch_bounds__(256, 1) void k_ozaki_regs(const int8_t* __restrict__ Ap, const int8_t* __restrict__ Bp,
@@ -215,6 +321,7 @@ static std::vector<double> factor_like(int n, double ell, double noise, std::mt1
 }
 
 int main(int argc, char** argv) {
+  CK(hipFuncSetAttribute((const void*)k_ozaki_lds, hipFuncAttributeMaxDynamicSharedMemorySize, OZ_LDS));
   // ---- (1) map
   {
     std::mt19937_64 g(1);
@@ -272,8 +379,15 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(k_ozaki, dim3((M / 128) * (N / 64)), dim3(256), 0, 0, dA, dB, M, N, K, dC, ea, eb);
     hipLaunchKernelGGL(k_f64, dim3(M / 16, N / 16), dim3(64), 0, 0, dAd, dBd, M, N, K, dF);
     CK(hipDeviceSynchronize());
-    std::vector<double> Co((size_t)M * N), Cf((size_t)M * N);
+    std::vector<double> Co((size_t)M * N), Cf((size_t)M * N), Cl((size_t)M * N);
     CK(hipMemcpy(Co.data(), dC, Co.size() * 8, hipMemcpyDeviceToHost));
+    CK(hipMemset(dC, 0, (size_t)M * N * 8));
+    hipLaunchKernelGGL(k_ozaki_lds, dim3((M / 128) * (N / 64)), dim3(256), OZ_LDS, 0, dA, dB, M, N, K, dC, ea, eb, 0);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(Cl.data(), dC, Cl.size() * 8, hipMemcpyDeviceToHost));
+    CK(hipGetLastError());
+    printf("LDS-staged kernel vs register-streamed kernel: %s\n",
+           memcmp(Cl.data(), Co.data(), Cl.size() * 8) == 0 ? "bitwise equal" : "DIFFERENT");
     CK(hipMemcpy(Cf.data(), dF, Cf.size() * 8, hipMemcpyDeviceToHost));
     double eo = 0, ef = 0, cmax = 0, rowabs = 0;
     for (int i = 0; i < M; ++i)
@@ -320,6 +434,18 @@ int main(int argc, char** argv) {
     printf("throughput (M=%d N=%d K=%d, %d workgroups, %g digit products): %.3f ms  fp64-equivalent %.1f TF/s  int8 %.0f TOP/s"
            "  planes streamed %.2f TB/s\n", M, N, K, grid, prods, ms, fl / ms * 1e-9, fl * prods / ms * 1e-9,
            (double)NS * K * (128 + 64) * grid / ms * 1e-9);
+    for (int swz = 0; swz < 2; ++swz) {
+      hipLaunchKernelGGL(k_ozaki_lds, dim3(grid), dim3(256), OZ_LDS, 0, dA, dB, M, N, K, dC, 0, 0, swz);
+      CK(hipEventRecord(e0));
+      for (int r = 0; r < reps; ++r)
+        hipLaunchKernelGGL(k_ozaki_lds, dim3(grid), dim3(256), OZ_LDS, 0, dA, dB, M, N, K, dC, 0, 0, swz);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      ms /= reps;
+      printf("LDS-staged (%s tile order): %.3f ms  fp64-equivalent %.1f TF/s  int8 %.0f TOP/s\n",
+             swz ? "XCD-aware" : "plain", ms, fl / ms * 1e-9, fl * prods / ms * 1e-9);
+    }
     CK(hipEventRecord(e0));
     for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k_ozaki_regs, dim3(grid), dim3(256), 0, 0, dA, dB, M, N, K, dC);
     CK(hipEventRecord(e1));
