@@ -123,12 +123,15 @@ __global__ __launch_bounds__(256, 1) void k_ozaki(const int8_t* __restrict__ Ap,
 template <int R>
 __device__ __forceinline__ int lds_off(int s, int kh, int row) { return ((s * 2 + kh) * R + row) * 16; }
 
-__global__ __launch_bounds__(256, 1) void k_ozaki_lds(const int8_t* __restrict__ Ap, const int8_t* __restrict__ Bp,
-                                                     int M, int N, int K, double* __restrict__ C, int ea, int eb,
-                                                     int swz) {
+template <int WN, bool PF2 = false>  // 32 x (32 WN) per wave; 4 (2 / WN) waves: WN = 2 one wave per SIMD, WN = 1 two
+__global__ __launch_bounds__(128 * (2 / WN) * 2, 1) void k_ozaki_lds(const int8_t* __restrict__ Ap,
+                                                                    const int8_t* __restrict__ Bp, int M, int N, int K,
+                                                                    double* __restrict__ C, int ea, int eb, int swz) {
   extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+  constexpr int NTH = 256 * (2 / WN);
   constexpr int BUF = NS * 2 * (128 + 64) * 16;
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int wm = w & 3, wn = w >> 2;  // 32-row block, 32-column block (WN = 1)
   const int mt = M / 128, ntn = N / 64;
   int tm, tn;
   if (swz) {
@@ -142,12 +145,12 @@ __global__ __launch_bounds__(256, 1) void k_ozaki_lds(const int8_t* __restrict__
   }
   const size_t sa = (size_t)M * K, sb = (size_t)N * K;
   // staging map: chunk c = (plane, row, k half), k half fastest; A: NS*256 chunks, B: NS*128
-  constexpr int NA = NS * 256 / 256, NB = NS * 128 / 256;
+  constexpr int NA = (NS * 256 + NTH - 1) / NTH, NB = (NS * 128 + NTH - 1) / NTH;
   const int8_t* ga[NA];
   int la[NA];
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
-    const int c = tid + 256 * j, sp = c / 256, row = (c % 256) / 2, kh = c & 1;
+    const int c = min(tid + NTH * j, NS * 256 - 1), sp = c / 256, row = (c % 256) / 2, kh = c & 1;
     ga[j] = Ap + sp * sa + (size_t)(tm * 128 + row) * K + 16 * kh;
     la[j] = lds_off<128>(sp, kh, row);
   }
@@ -155,7 +158,7 @@ __global__ __launch_bounds__(256, 1) void k_ozaki_lds(const int8_t* __restrict__
   int lb[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    const int c = tid + 256 * j, sp = c / 128, row = (c % 128) / 2, kh = c & 1;
+    const int c = min(tid + NTH * j, NS * 128 - 1), sp = c / 128, row = (c % 128) / 2, kh = c & 1;
     gb[j] = Bp + sp * sb + (size_t)(tn * 64 + row) * K + 16 * kh;
     lb[j] = NS * 2 * 128 * 16 + lds_off<64>(sp, kh, row);
   }
@@ -165,39 +168,71 @@ __global__ __launch_bounds__(256, 1) void k_ozaki_lds(const int8_t* __restrict__
 #pragma unroll
   for (int j = 0; j < NB; ++j) rb[j] = *(const v4i*)gb[j];
 #pragma unroll
-  for (int j = 0; j < NA; ++j) *(v4i*)(lds + la[j]) = ra[j];
+  for (int j = 0; j < NA; ++j) *(v4i*)(lds + la[j]) = ra[j];  // (clamped duplicates store the same bytes)
 #pragma unroll
   for (int j = 0; j < NB; ++j) *(v4i*)(lds + lb[j]) = rb[j];
   __syncthreads();
-  v16i acc[NS][2];
+  v16i acc[NS][WN];
 #pragma unroll
-  for (int g = 0; g < NS; ++g) acc[g][0] = acc[g][1] = v16i{};
-  const int fa = lds_off<128>(0, l >> 5, 32 * w + (l & 31));
-  const int fb = NS * 2 * 128 * 16 + lds_off<64>(0, l >> 5, l & 31);
+  for (int g = 0; g < NS; ++g)
+#pragma unroll
+    for (int nb = 0; nb < WN; ++nb) acc[g][nb] = v16i{};
+  const int fa = lds_off<128>(0, l >> 5, 32 * wm + (l & 31));
+  const int fb = NS * 2 * 128 * 16 + lds_off<64>(0, l >> 5, 32 * wn + (l & 31));
   const int nsteps = K / 32;
+  // PF2: global loads issued two k-steps ahead into a second register set (written to LDS at
+  // the end of the following step), so that two steps of MFMAs cover their latency
+  v4i qa[NA], qb[NB];
+  if (PF2 && nsteps > 1) {
+#pragma unroll
+    for (int j = 0; j < NA; ++j) qa[j] = *(const v4i*)(ga[j] + 32);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) qb[j] = *(const v4i*)(gb[j] + 32);
+  }
   for (int i = 0; i < nsteps; ++i) {
     const int8_t* cur = lds + (i & 1) * BUF;
     int8_t* nxt = lds + ((i + 1) & 1) * BUF;
     const bool more = i + 1 < nsteps;
-    if (more) {
+    if (PF2) {
+      // ra <- step i+1 (already in qa), qa <- step i+2
+#pragma unroll
+      for (int j = 0; j < NA; ++j) ra[j] = qa[j];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) rb[j] = qb[j];
+      if (i + 2 < nsteps) {
+#pragma unroll
+        for (int j = 0; j < NA; ++j) qa[j] = *(const v4i*)(ga[j] + 32 * (i + 2));
+#pragma unroll
+        for (int j = 0; j < NB; ++j) qb[j] = *(const v4i*)(gb[j] + 32 * (i + 2));
+      }
+    } else if (more) {
 #pragma unroll
       for (int j = 0; j < NA; ++j) ra[j] = *(const v4i*)(ga[j] + 32 * (i + 1));
 #pragma unroll
       for (int j = 0; j < NB; ++j) rb[j] = *(const v4i*)(gb[j] + 32 * (i + 1));
     }
-    v4i a[NS], b[NS][2];
+    v4i a[NS], b[NS][WN];
 #pragma unroll
     for (int sp = 0; sp < NS; ++sp) {
       a[sp] = *(const v4i*)(cur + fa + sp * 2 * 128 * 16);
-      b[sp][0] = *(const v4i*)(cur + fb + sp * 2 * 64 * 16);
-      b[sp][1] = *(const v4i*)(cur + fb + sp * 2 * 64 * 16 + 32 * 16);
+#pragma unroll
+      for (int nb = 0; nb < WN; ++nb) b[sp][nb] = *(const v4i*)(cur + fb + sp * 2 * 64 * 16 + nb * 32 * 16);
     }
+    // products in order of the later plane they need (max(s, t)), so the first MFMAs wait only
+    // for the first planes' LDS reads (LDS returns in order: partial lgkmcnt waits)
 #pragma unroll
-    for (int sp = 0; sp < NS; ++sp)
+    for (int m = 0; m < NS; ++m)
 #pragma unroll
-      for (int t = 0; t < NS - sp; ++t) {
-        acc[sp + t][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[sp], b[t][0], acc[sp + t][0], 0, 0, 0);
-        acc[sp + t][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[sp], b[t][1], acc[sp + t][1], 0, 0, 0);
+      for (int sp = 0; sp <= m; ++sp) {
+        const int t = (sp == m) ? 0 : m;  // pairs (m, t <= m) and (sp < m, m)
+#pragma unroll
+        for (int u = 0; u <= (sp == m ? m : 0); ++u) {
+          const int s1 = sp, t1 = (sp == m) ? u : t;
+          if (s1 + t1 < NS)
+#pragma unroll
+            for (int nb = 0; nb < WN; ++nb)
+              acc[s1 + t1][nb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[s1], b[t1][nb], acc[s1 + t1][nb], 0, 0, 0);
+        }
       }
     if (more) {
 #pragma unroll
@@ -208,14 +243,14 @@ __global__ __launch_bounds__(256, 1) void k_ozaki_lds(const int8_t* __restrict__
     __syncthreads();
   }
 #pragma unroll
-  for (int nb = 0; nb < 2; ++nb)
+  for (int nb = 0; nb < WN; ++nb)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       double v = 0.0;
 #pragma unroll
       for (int g = NS - 1; g >= 0; --g) v = v + ldexp((double)acc[g][nb][r], -7 * (g + 2));
-      const int row = tm * 128 + 32 * w + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
-      const int col = tn * 64 + nb * 32 + (l & 31);
+      const int row = tm * 128 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+      const int col = tn * 64 + (WN == 2 ? nb : wn) * 32 + (l & 31);
       C[(size_t)row * N + col] = ldexp(v, ea + eb + 2);
     }
 }
@@ -321,7 +356,9 @@ static std::vector<double> factor_like(int n, double ell, double noise, std::mt1
 }
 
 int main(int argc, char** argv) {
-  CK(hipFuncSetAttribute((const void*)k_ozaki_lds, hipFuncAttributeMaxDynamicSharedMemorySize, OZ_LDS));
+  CK(hipFuncSetAttribute((const void*)k_ozaki_lds<2>, hipFuncAttributeMaxDynamicSharedMemorySize, OZ_LDS));
+  CK(hipFuncSetAttribute((const void*)k_ozaki_lds<1>, hipFuncAttributeMaxDynamicSharedMemorySize, OZ_LDS));
+  CK(hipFuncSetAttribute((const void*)k_ozaki_lds<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, OZ_LDS));
   // ---- (1) map
   {
     std::mt19937_64 g(1);
@@ -382,12 +419,20 @@ int main(int argc, char** argv) {
     std::vector<double> Co((size_t)M * N), Cf((size_t)M * N), Cl((size_t)M * N);
     CK(hipMemcpy(Co.data(), dC, Co.size() * 8, hipMemcpyDeviceToHost));
     CK(hipMemset(dC, 0, (size_t)M * N * 8));
-    hipLaunchKernelGGL(k_ozaki_lds, dim3((M / 128) * (N / 64)), dim3(256), OZ_LDS, 0, dA, dB, M, N, K, dC, ea, eb, 0);
-    CK(hipDeviceSynchronize());
-    CK(hipMemcpy(Cl.data(), dC, Cl.size() * 8, hipMemcpyDeviceToHost));
-    CK(hipGetLastError());
-    printf("LDS-staged kernel vs register-streamed kernel: %s\n",
-           memcmp(Cl.data(), Co.data(), Cl.size() * 8) == 0 ? "bitwise equal" : "DIFFERENT");
+    for (int wn = 0; wn <= 2; ++wn) {
+      CK(hipMemset(dC, 0, (size_t)M * N * 8));
+      if (wn == 0)
+        hipLaunchKernelGGL((k_ozaki_lds<1, true>), dim3((M / 128) * (N / 64)), dim3(512), OZ_LDS, 0, dA, dB, M, N, K, dC, ea, eb, 0);
+      else if (wn == 2)
+        hipLaunchKernelGGL(k_ozaki_lds<2>, dim3((M / 128) * (N / 64)), dim3(256), OZ_LDS, 0, dA, dB, M, N, K, dC, ea, eb, 0);
+      else
+        hipLaunchKernelGGL(k_ozaki_lds<1>, dim3((M / 128) * (N / 64)), dim3(512), OZ_LDS, 0, dA, dB, M, N, K, dC, ea, eb, 0);
+      CK(hipDeviceSynchronize());
+      CK(hipGetLastError());
+      CK(hipMemcpy(Cl.data(), dC, Cl.size() * 8, hipMemcpyDeviceToHost));
+      printf("LDS-staged kernel (%d waves%s) vs register-streamed kernel: %s\n", wn ? 8 / wn : 8, wn ? "" : ", loads two steps ahead",
+             memcmp(Cl.data(), Co.data(), Cl.size() * 8) == 0 ? "bitwise equal" : "DIFFERENT");
+    }
     CK(hipMemcpy(Cf.data(), dF, Cf.size() * 8, hipMemcpyDeviceToHost));
     double eo = 0, ef = 0, cmax = 0, rowabs = 0;
     for (int i = 0; i < M; ++i)
@@ -434,17 +479,26 @@ int main(int argc, char** argv) {
     printf("throughput (M=%d N=%d K=%d, %d workgroups, %g digit products): %.3f ms  fp64-equivalent %.1f TF/s  int8 %.0f TOP/s"
            "  planes streamed %.2f TB/s\n", M, N, K, grid, prods, ms, fl / ms * 1e-9, fl * prods / ms * 1e-9,
            (double)NS * K * (128 + 64) * grid / ms * 1e-9);
-    for (int swz = 0; swz < 2; ++swz) {
-      hipLaunchKernelGGL(k_ozaki_lds, dim3(grid), dim3(256), OZ_LDS, 0, dA, dB, M, N, K, dC, 0, 0, swz);
+    for (int v = 0; v < 5; ++v) {
+      const int swz = v == 4 ? 1 : v & 1, wn = (v >> 1) ? 1 : 2;
+      auto go = [&] {
+        if (v == 4)
+          hipLaunchKernelGGL((k_ozaki_lds<1, true>), dim3(grid), dim3(512), OZ_LDS, 0, dA, dB, M, N, K, dC, 0, 0, swz);
+        else if (wn == 2)
+          hipLaunchKernelGGL(k_ozaki_lds<2>, dim3(grid), dim3(256), OZ_LDS, 0, dA, dB, M, N, K, dC, 0, 0, swz);
+        else
+          hipLaunchKernelGGL(k_ozaki_lds<1>, dim3(grid), dim3(512), OZ_LDS, 0, dA, dB, M, N, K, dC, 0, 0, swz);
+      };
+      go();
       CK(hipEventRecord(e0));
-      for (int r = 0; r < reps; ++r)
-        hipLaunchKernelGGL(k_ozaki_lds, dim3(grid), dim3(256), OZ_LDS, 0, dA, dB, M, N, K, dC, 0, 0, swz);
+      for (int r = 0; r < reps; ++r) go();
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       CK(hipEventElapsedTime(&ms, e0, e1));
       ms /= reps;
-      printf("LDS-staged (%s tile order): %.3f ms  fp64-equivalent %.1f TF/s  int8 %.0f TOP/s\n",
-             swz ? "XCD-aware" : "plain", ms, fl / ms * 1e-9, fl * prods / ms * 1e-9);
+      printf("LDS-staged (%d waves, %s tile order%s): %.3f ms  fp64-equivalent %.1f TF/s  int8 %.0f TOP/s\n", 8 / wn,
+             swz ? "XCD-aware" : "plain", v == 4 ? ", loads two steps ahead" : "", ms, fl / ms * 1e-9,
+             fl * prods / ms * 1e-9);
     }
     CK(hipEventRecord(e0));
     for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k_ozaki_regs, dim3(grid), dim3(256), 0, 0, dA, dB, M, N, K, dC);
