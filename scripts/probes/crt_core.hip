@@ -10,7 +10,8 @@
 //   One accumulator set per pass (instead of one per digit weight) lets a workgroup hold a
 //   256x256 tile: half the operand bytes per flop of the digit form's 128x64.
 //
-// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/probes/crt_core.hip -o scripts/probes/crt_core
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off scripts/probes/crt_core.hip -o scripts/probes/crt_core
+// (-ffp-contract=off: the reconstruction's error-free sums must not be fused into FMAs)
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -173,6 +174,37 @@ __global__ void k_crt_garner(const uint8_t* __restrict__ R, size_t MN, double* _
   C[e] = ldexp(neg ? -d : d, -scale);
 }
 
+// Floating-point CRT reconstruction: X = sum_i c_i W_i mod M with W_i = M_i (M_i^-1 mod m_i);
+// X / M = frac(sum_i c_i q_i), q_i = W_i / M in [0, 1) as double-double constants; the sum
+// (< 2^12) in double-double keeps X / M to ~2^-94, then C = (X / M) M 2^-scale.
+__constant__ double c_qhi[NM], c_qlo[NM];
+__device__ __forceinline__ void two_sum(double a, double b, double& s, double& e) {
+  s = a + b;
+  const double bb = s - a;
+  e = (a - (s - bb)) + (b - bb);
+}
+__global__ void k_crt_fp(const uint8_t* __restrict__ R, size_t MN, double* __restrict__ C, double Mscaled) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= MN) return;
+  double sh = 0.0, sl = 0.0;
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    const double c = (double)R[(size_t)i * MN + e];
+    const double ph = c * c_qhi[i];
+    const double pe = fma(c, c_qhi[i], -ph);  // exact product error
+    double t, te;
+    two_sum(sh, ph, t, te);
+    sh = t;
+    sl += te + pe + c * c_qlo[i];
+  }
+  // frac, centred: subtract the nearest integer (exact), renormalise
+  const double n = rint(sh);
+  double h = sh - n, l = sl;
+  const double r = rint(h + l);  // the low part may carry past +-1/2
+  h -= r;
+  C[e] = (h + l) * Mscaled;
+}
+
 // plain fp64 GEMM on the FP64 MFMA: the accuracy comparison's fp64 arm
 __global__ void k_f64(const double* A, const double* B, int M, int N, int K, double* C) {
   const int l = threadIdx.x & 63;
@@ -229,11 +261,16 @@ static std::vector<double> factor_like(int n, double ell, double noise, std::mt1
   return L;
 }
 
-static void run_crt(const int8_t* dA, const int8_t* dB, int M, int N, int K, uint8_t* dR, double* dC, int scale) {
+static double g_M = 0;  // product of the moduli as a double
+static void run_crt(const int8_t* dA, const int8_t* dB, int M, int N, int K, uint8_t* dR, double* dC, int scale,
+                    bool fp = false) {
   const int grid = (M / TM) * (N / TN);
   for (int i = 0; i < NM; ++i) hipLaunchKernelGGL(k_crt_pass, dim3(grid), dim3(512), 0, 0, dA, dB, M, N, K, i, dR);
   const size_t MN = (size_t)M * N;
-  hipLaunchKernelGGL(k_crt_garner, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, 0, dR, MN, dC, scale);
+  if (fp)
+    hipLaunchKernelGGL(k_crt_fp, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, 0, dR, MN, dC, std::ldexp(g_M, -scale));
+  else
+    hipLaunchKernelGGL(k_crt_garner, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, 0, dR, MN, dC, scale);
 }
 
 int main(int argc, char** argv) {
@@ -247,9 +284,38 @@ int main(int argc, char** argv) {
             break;
           }
     CK(hipMemcpyToSymbol(HIP_SYMBOL(c_mod), h_mod, sizeof(h_mod)));
+    {  // q_i = W_i / M as double-double, by binary long division in 128-bit integers
+      typedef unsigned __int128 u128;
+      u128 Mb = 1;
+      for (int i = 0; i < NM; ++i) Mb *= (u128)h_mod[i];
+      double qh[NM], ql[NM];
+      for (int i = 0; i < NM; ++i) {
+        const u128 Mi = Mb / (u128)h_mod[i];
+        const int mi = h_mod[i];
+        const int r = (int)(Mi % (u128)mi);
+        int inv = 0;
+        for (int x = 1; x < mi; ++x)
+          if (r * x % mi == 1) { inv = x; break; }
+        u128 W = Mi * (u128)inv % Mb;  // < M
+        unsigned long long c1 = 0, c2 = 0;
+        for (int b = 0; b < 100; ++b) {  // 100 fraction bits of W / M
+          W <<= 1;  // W < M < 2^126: no overflow
+          const int bit = W >= Mb;
+          if (bit) W -= Mb;
+          if (b < 50) c1 = (c1 << 1) | bit; else c2 = (c2 << 1) | bit;
+        }
+        const double d1 = std::ldexp((double)c1, -50), d2 = std::ldexp((double)c2, -100);
+        qh[i] = d1 + d2;
+        ql[i] = d2 - (qh[i] - d1);
+      }
+      CK(hipMemcpyToSymbol(HIP_SYMBOL(c_qhi), qh, sizeof(qh)));
+      CK(hipMemcpyToSymbol(HIP_SYMBOL(c_qlo), ql, sizeof(ql)));
+    }
     CK(hipMemcpyToSymbol(HIP_SYMBOL(c_inv), inv, sizeof(inv)));
     double lg = 0;
     for (int i = 0; i < NM; ++i) lg += std::log2((double)h_mod[i]);
+    g_M = 1.0;
+    for (int i = 0; i < NM; ++i) g_M *= (double)h_mod[i];
     printf("moduli: %d, product 2^%.1f (needs > 2^%d at K = 4096, %d-bit operands)\n", NM, lg, 1 + 12 + 2 * BITS, BITS);
   }
   // ---- accuracy
@@ -285,9 +351,13 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(k_f64, dim3(M / 16, N / 16), dim3(64), 0, 0, dAd, dBd, M, N, K, dF);
     CK(hipDeviceSynchronize());
     CK(hipGetLastError());
-    std::vector<double> Cc((size_t)M * N), Cf((size_t)M * N);
+    std::vector<double> Cc((size_t)M * N), Cf((size_t)M * N), Cp((size_t)M * N);
     CK(hipMemcpy(Cc.data(), dC, Cc.size() * 8, hipMemcpyDeviceToHost));
     CK(hipMemcpy(Cf.data(), dF, Cf.size() * 8, hipMemcpyDeviceToHost));
+    run_crt(dA, dB, M, N, K, dR, dC, 2 * BITS - ea - eb, true);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(Cp.data(), dC, Cp.size() * 8, hipMemcpyDeviceToHost));
+    double ep = 0;
     double ec = 0, ef = 0, cmax = 0;
     for (int i = 0; i < M; ++i)
       for (int j = 0; j < N; ++j) {
@@ -295,10 +365,11 @@ int main(int argc, char** argv) {
         for (int k = 0; k < K; ++k) s += (long double)A[(size_t)i * K + k] * B[(size_t)j * K + k];
         ec = std::max(ec, (double)std::fabs((long double)Cc[(size_t)i * N + j] - s));
         ef = std::max(ef, (double)std::fabs((long double)Cf[(size_t)i * N + j] - s));
+        ep = std::max(ep, (double)std::fabs((long double)Cp[(size_t)i * N + j] - s));
         cmax = std::max(cmax, (double)std::fabs(s));
       }
     printf("accuracy (M=%d N=%d K=%d, factor-like operands, %d moduli, %d-bit operands): max|C-C_exact| crt %.3e  "
-           "fp64 MFMA %.3e  (max|C| %.3e)\n", M, N, K, NM, BITS, ec, ef, cmax);
+           "fp64 MFMA %.3e  (max|C| %.3e); floating-point reconstruction %.3e\n", M, N, K, NM, BITS, ec, ef, cmax, ep);
     CK(hipFree(dA)); CK(hipFree(dB)); CK(hipFree(dR)); CK(hipFree(dC)); CK(hipFree(dF)); CK(hipFree(dAd)); CK(hipFree(dBd));
   }
   // ---- throughput
@@ -326,7 +397,7 @@ int main(int argc, char** argv) {
       CK(hipEventRecord(e0));
       for (int i = 0; i < NM; ++i) hipLaunchKernelGGL(k_crt_pass, dim3(grid), dim3(512), 0, 0, dA, dB, M, N, K, i, dR);
       CK(hipEventRecord(e1));
-      hipLaunchKernelGGL(k_crt_garner, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, 0, dR, MN, dC, 0);
+      hipLaunchKernelGGL(k_crt_fp, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, 0, dR, MN, dC, 1.0);
       CK(hipEventRecord(e2));
       CK(hipEventSynchronize(e2));
       float a, b;
@@ -338,7 +409,7 @@ int main(int argc, char** argv) {
     ms_p /= reps;
     ms_g /= reps;
     const double fl = 2.0 * M * N * K;
-    printf("throughput (M=%d N=%d K=%d, %d workgroups of 256x256, %d passes): passes %.3f ms + Garner %.3f ms  "
+    printf("throughput (M=%d N=%d K=%d, %d workgroups of 256x256, %d passes): passes %.3f ms + reconstruction %.3f ms  "
            "fp64-equivalent %.1f TF/s (passes alone %.1f)  int8 %.0f TOP/s  residues streamed %.2f TB/s\n",
            M, N, K, grid, NM, ms_p, ms_g, fl / (ms_p + ms_g) * 1e-9, fl / ms_p * 1e-9, fl * NM / ms_p * 1e-9,
            (double)NM * K * (TM + TN) * grid / ms_p * 1e-9);
