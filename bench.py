@@ -278,6 +278,31 @@ def launch_ranks(n):
     return next((rc for rc in rcs if rc != 0), 0)
 
 
+def open_exchange(ctx, world, rank):
+    """The measured run's swarm exchange: libgpfit's RCCL communicator on this rank's GPU.
+
+    A host-transport side channel (TCP rendezvous, no device) first lets the ranks agree on
+    whether every rank opened RCCL; if any could not, all ranks use the host transport for the
+    (P + G)-double exchange and the JSON line says so (`exchange`), so a scaling run still
+    measures the sharded factorisations. GPF_COMM_TRANSPORT=host skips RCCL."""
+    import gpfit
+    base = int(os.environ.get("GPF_COMM_PORT", int(os.environ.get("MASTER_PORT", "29599")) + 1))
+    side = gpfit.Comm(rank, world, os.environ.get("MASTER_ADDR", "127.0.0.1"), base + 16, "host")
+    if os.environ.get("GPF_COMM_TRANSPORT", "rccl") == "host":
+        return side, {"transport": "host"}
+    rccl, err = None, ""
+    try:
+        rccl = gpfit.Comm.from_env(ctx, transport="rccl")
+    except gpfit.GPFitError as exc:  # reported below, on every rank's behalf by rank 0
+        err = str(exc)[:400]
+    if int(side.allreduce([1.0 if rccl is not None else 0.0])[0]) == world:
+        side.close()
+        return rccl, {"transport": "rccl"}
+    if rccl is not None:
+        rccl.close()
+    return side, {"transport": "host", "rccl_error": err or "another rank could not open RCCL"}
+
+
 def plumbing(args, world, rank):
     """CPU-only check of the multi-rank plumbing (`--plumbing`): the rank processes, the
     library's host-transport communicator, the barrier and the max-over-ranks timing, with a
@@ -350,7 +375,7 @@ def main():
     # one GPU per rank (LOCAL_RANK); GPFIT_DEVICE pins every rank to one device, for rehearsing
     # the multi-rank path on a one-GPU box with GPF_COMM_TRANSPORT=host (RCCL needs a GPU per rank)
     ctx = gpfit.Context(int(os.environ.get("GPFIT_DEVICE", local)))
-    comm = gpfit.Comm.from_env(ctx) if world > 1 else None  # RCCL on this rank's GPU
+    comm, exchange = open_exchange(ctx, world, rank) if world > 1 else (None, None)  # RCCL on this rank's GPU
     score = make_scorer(x, y, e, s, ex, lo, hi, ctx=ctx, comm=comm)
     rng = np.random.default_rng(args.seed + 1000)  # identical on every rank
 
@@ -475,7 +500,8 @@ def main():
             "config": {"workload": f"PSO objective, BASELINE config {letter}: synthetic N={N} d={d}, "
                                    f"swarm {spg}/GPU x {world} GPU = {P}",
                        "N": N, "d": d, "swarm": P, "swarm_per_gpu": spg, "global_batch": P, "seq_len": N,
-                       "parallelism": f"swarm-shard x{world} (libgpfit RCCL all-reduce)" if world > 1 else "single GPU",
+                       "parallelism": (f"swarm-shard x{world} (libgpfit {exchange['transport'].upper()} all-reduce)"
+                                       if world > 1 else "single GPU"),
                        "hetero_noise": bool(args.hetero),
                        "pso_iters_per_s": args.steps / dt, "particles": "interior l~U[0.05,0.6]^d (full work)"},
             "pso_loop": pso,
@@ -488,6 +514,7 @@ def main():
             "gpu_vs_cpu_all_cores": (value / cpu["all_cores"]["value"]) if cpu else None,
             "breakdown_ms": breakdown,
             "build": gpfit.build_info(),
+            "exchange": exchange,
         }
         print(json.dumps(line), flush=True)
     if comm is not None:

@@ -50,3 +50,22 @@ def test_multi_rank_bench_on_one_gpu():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["swarm"] == 64 and out["value"] > 0
     assert out["config"]["swarm_per_gpu"] == 32
+    assert out["exchange"] == {"transport": "host"}
+
+
+@pytest.mark.gpu
+def test_multi_rank_bench_rccl_agreement_on_one_gpu():
+    """bench.py --gpus 2 with the default RCCL exchange, both ranks on device 0: RCCL refuses two
+    ranks on one GPU, the ranks agree over the host side channel that RCCL is unavailable and
+    all of them run the host-transport exchange; the JSON line records the RCCL error. (On a
+    node with a GPU per rank the same agreement keeps RCCL.)"""
+    r = _run(["--gpus", "2", "--steps", "2", "--warmup", "1", "--n", "1024", "--d", "2", "--no-cpu",
+              "--pso-steps", "1", "--predict-points", "0", "--no-hull", "--psurf-rows", "0"],
+             env={"GPFIT_DEVICE": "0", "GPF_COMM_TIMEOUT_S": "60"}, timeout=150)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["n_gpus"] == 2 and out["value"] > 0
+    ex = out["exchange"]
+    assert ex["transport"] in ("rccl", "host")
+    if ex["transport"] == "host":
+        assert ex["rccl_error"]
