@@ -1011,7 +1011,24 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
       const int c = qd.lane & 15;
       scratch[(qd.cb / 32) * T + qd.rb + 16 * (c >> 2) + (qd.lane >> 4) + 4 * (c & 3)] = acc_row_dot(acc, qd, zj);
     }
-    if (!ED && deep) {
+    if (!ED && deep == 2) {
+      // pre-update (see deep_syrk in gpfit_api.hip): tile w = 1 (I = J+2) applies
+      // A_II -= L_I,<=J L_I,<=J^T to the untouched K block, the critical tile (w = 0) the last
+      // rank-128 term L_IJ L_IJ^T; the other tiles leave A_II alone. (J = 0: the critical tile's
+      // A_II is untouched and its one term is the whole update.)
+      if (w == 1) {
+        acc.load(qd, Aii, ld);
+        step_gemm<false, true, TRI_C_LOWER>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)I * T * ld, Npad,
+                                            (J + 1) * T, smem, qd);
+        acc.store(qd, Aii, ld);
+      } else if (w == 0) {
+        acc.load(qd, Aii, ld);
+        step_gemm<false, true, TRI_C_LOWER>(acc, Aij, Npad, Aij, Npad, T, smem, qd);
+        acc.store(qd, Aii, ld);
+      } else {
+        __syncthreads();
+      }
+    } else if (!ED && deep) {
       // deep update: A_II -= L_I,<=J L_I,<=J^T in one depth-128(J+1) GEMM by the critical tile
       // only (A_II has not been touched since the K build); the other tiles skip the update. The
       // additions run in the same order as the per-launch look-ahead's (k ascending, one MFMA k-step

@@ -326,9 +326,15 @@ static bool quad_finish(int pc, int nt) {
 // group's launch — same box: C +0.9%, D's 32-particle share -13%, E's share -2%
 // (profiles/r2/deep_syrk_ab_rejected.txt). Launches with the early diagonal factor always keep
 // the look-ahead.
-static bool deep_syrk() {
-  if (const char* s = getenv("GPF_DEEP_SYRK")) return atoi(s) != 0;
-  return false;
+// GPF_DEEP_SYRK = 2 (pre-update): tile w = 1 of launch J (I = J+2, not on the launch's critical
+// chain: it factors nothing) applies A_II -= L_I,<=J L_I,<=J^T in one deep GEMM, the critical tile
+// of launch J+1 then adds only the last rank-128 term before it factors the block, and the other L
+// tiles skip the update (no A_II read-modify-write per tile and launch). Same additions in the
+// same order: bitwise equal. Off too: same box, C neutral, D's share -3.7%, E's share -0.9% (tile
+// w = 1 becomes the launch's longest chain; profiles/r2/pre_update_syrk_ab_rejected.txt).
+static int deep_syrk() {
+  if (const char* s = getenv("GPF_DEEP_SYRK")) return std::max(0, std::min(2, atoi(s)));
+  return 0;
 }
 
 // Critical-tile split of block-column launch J (gpf::SPLIT_CRIT), for launches that leave
@@ -451,7 +457,8 @@ static int run_factor(gpf_ctx* c, int pc) {
   //   L tile: depth-128J GEMM 2 T^3 J + triangular multiply T^3 + look-ahead syrk share T^3
   //   U tile: depth-128(J-K) GEMM with a triangular factor 2 T^3 (J-K) - T^3 + triangular multiply T^3
   //   diagonal block: 2/3 T^3 (block J+1 fused at the end of launch J, or block J early in it)
-  const bool ed = early_diag(pc, nt), deep = deep_syrk();
+  const bool ed = early_diag(pc, nt);
+  const int deep = deep_syrk();
   auto step_flops = [&](int J) {
     double fl = 0.0;
     for (int w = 0; w < nt - 1; ++w) {
@@ -522,7 +529,7 @@ static int run_factor(gpf_ctx* c, int pc) {
                          c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc, l.grp, N, c->d_x,
                          c->d_ls + (size_t)p0 * c->d, c->d, l.S, partg, cntg, c->d_flag + p0, l.ed,
                          c->d_cflag + p0, c->d_qbuf + (size_t)p0 * gpf::QSTRIDE, c->d_qcnt + (size_t)p0 * gpf::QCNT,
-                         l.qf, (int)(!ed && deep));
+                         l.qf, ed ? 0 : deep);
     });
     if (rc) return rc;
     total += fl * gc;

@@ -554,7 +554,8 @@ def test_early_diagonal_factor_matches_fused(ctx, monkeypatch, N, d, P):
     the factor itself bitwise equal for the prediction path. The fused path's deep diagonal
     update (GPF_DEEP_SYRK = 1, off by default: the critical tile applies A_II -= L_I,<=J L_I,<=J^T
     in one GEMM) runs the look-ahead's additions in the same order: bitwise equal to the
-    per-launch look-ahead. With the quadrant finish of the critical tile on (GPF_QUAD = 1, off by default:
+    per-launch look-ahead; so does its pre-update (GPF_DEEP_SYRK = 2: tile I = J+2 applies the
+    terms k <= J in one GEMM one launch ahead, the critical tile the last one). With the quadrant finish of the critical tile on (GPF_QUAD = 1, off by default:
     the triangular multiply and the rank-128 update in 64-wide quadrants on four workgroups, the
     update summed per column half) the rounding differs: mean/sd within 1e-8 of the fused path
     and the factor within 1e-8 normwise (two fp64 evaluations of a system with condition numbers
@@ -569,8 +570,8 @@ def test_early_diagonal_factor_matches_fused(ctx, monkeypatch, N, d, P):
     ctx.set_grid(s, ex, lo, hi)
     Q = rng.uniform(0.1, 0.5, size=(P, d))
     out = {}
-    for mode, ed, qf, deep in (("fused", "0", "0", "0"), ("fused_deep", "0", "0", "1"), ("ed", "1", "0", "0"),
-                               ("quad", "1", "1", "0")):
+    for mode, ed, qf, deep in (("fused", "0", "0", "0"), ("fused_deep", "0", "0", "1"), ("fused_pre", "0", "0", "2"),
+                               ("ed", "1", "0", "0"), ("quad", "1", "1", "0")):
         monkeypatch.setenv("GPF_EARLY_DIAG", ed)
         monkeypatch.setenv("GPF_QUAD", qf)
         monkeypatch.setenv("GPF_DEEP_SYRK", deep)
@@ -579,7 +580,7 @@ def test_early_diagonal_factor_matches_fused(ctx, monkeypatch, N, d, P):
             out[mode + "f"] = ctx.debug_factor(Q[0])
     for k in ("GPF_EARLY_DIAG", "GPF_QUAD", "GPF_DEEP_SYRK"):
         monkeypatch.delenv(k)
-    for other in ("fused_deep", "ed"):
+    for other in ("fused_deep", "fused_pre", "ed"):
         for a, b in zip(out["fused"], out[other]):
             np.testing.assert_array_equal(a, b)
         if P == 1:
