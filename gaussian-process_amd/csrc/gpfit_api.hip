@@ -88,6 +88,10 @@ struct gpf_ctx {
   int* d_info = nullptr;
   int* d_flag = nullptr;  // per particle: last diagonal block published in the running launch (early_diag)
   int* d_cflag = nullptr;  // per particle: last critical-tile C published to the quadrant workgroups (quad_finish)
+  // gpf_predict's query-chunk buffers, kept between calls (grow-only; freed with the work buffers)
+  double *p_xf = nullptr, *p_ks = nullptr, *p_vsq = nullptr, *p_mu = nullptr, *p_sd = nullptr;
+  int64_t p_cols = 0, p_np = 0;
+  int p_d = 0, p_nt = 0;
   double* d_qbuf = nullptr;    // per particle: the quadrant finish's C, partial updates and row partials
   unsigned* d_qcnt = nullptr;  // per particle: its arrival counters, kept zero
   int* d_hist = nullptr;
@@ -180,8 +184,16 @@ static void clear_graphs(gpf_ctx* c) {
   c->graphs.clear();
 }
 
+static void free_pred(gpf_ctx* c) {
+  hipFree(c->p_xf); hipFree(c->p_ks); hipFree(c->p_vsq); hipFree(c->p_mu); hipFree(c->p_sd);
+  c->p_xf = c->p_ks = c->p_vsq = c->p_mu = c->p_sd = nullptr;
+  c->p_cols = c->p_np = 0;
+  c->p_d = c->p_nt = 0;
+}
+
 static void free_work(gpf_ctx* c) {
   clear_graphs(c);
+  free_pred(c);
   hipHostFree(c->h_ls); hipHostFree(c->h_loss); hipHostFree(c->h_info);
   c->h_ls = c->h_loss = nullptr;
   c->h_info = nullptr;
@@ -887,12 +899,22 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
   chunk = std::min<int64_t>(std::max<int64_t>(chunk, 16384), maxcols);
   chunk = std::min<int64_t>(chunk, M);
   const int64_t Cp = ((chunk + T - 1) / T) * T;
-  double *d_xf = nullptr, *d_ks = nullptr, *d_vsq = nullptr, *d_mu = nullptr, *d_sd = nullptr;
-  GPF_HIP(c, hipMalloc(&d_xf, (size_t)c->d * Cp * 8));
-  GPF_HIP(c, hipMalloc(&d_ks, (size_t)Np * Cp * 8));
-  GPF_HIP(c, hipMalloc(&d_vsq, (size_t)c->nt * Cp * 8));
-  GPF_HIP(c, hipMalloc(&d_mu, (size_t)Cp * 8));
-  GPF_HIP(c, hipMalloc(&d_sd, (size_t)Cp * 8));
+  // buffers kept from the previous call when they are large enough (a hipMalloc/hipFree of the
+  // Np x Cp cross-covariance per call cost ~1 ms of the call's wall time)
+  if (c->p_cols < Cp || c->p_np != Np || c->p_d != c->d || c->p_nt != c->nt) {
+    GPF_HIP(c, hipStreamSynchronize(c->stream));
+    free_pred(c);
+    GPF_HIP(c, hipMalloc(&c->p_xf, (size_t)c->d * Cp * 8));
+    GPF_HIP(c, hipMalloc(&c->p_ks, (size_t)Np * Cp * 8));
+    GPF_HIP(c, hipMalloc(&c->p_vsq, (size_t)c->nt * Cp * 8));
+    GPF_HIP(c, hipMalloc(&c->p_mu, (size_t)Cp * 8));
+    GPF_HIP(c, hipMalloc(&c->p_sd, (size_t)Cp * 8));
+    c->p_cols = Cp;
+    c->p_np = Np;
+    c->p_d = c->d;
+    c->p_nt = c->nt;
+  }
+  double *d_xf = c->p_xf, *d_ks = c->p_ks, *d_vsq = c->p_vsq, *d_mu = c->p_mu, *d_sd = c->p_sd;
   std::vector<double> hx((size_t)c->d * Cp);
   rc = GPF_OK;
   for (int64_t s = 0; s < M && rc == GPF_OK; s += chunk) {
@@ -931,7 +953,6 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
   }
   hipStreamSynchronize(c->stream);
   if (c->prof) harvest(c);
-  hipFree(d_xf); hipFree(d_ks); hipFree(d_vsq); hipFree(d_mu); hipFree(d_sd);
   return rc;
 }
 

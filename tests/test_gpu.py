@@ -274,6 +274,40 @@ def test_chunked_batches_equal_single_batch(f3, monkeypatch):
     np.testing.assert_array_equal(full, chunked)
 
 
+def test_predict_buffer_reuse_across_calls():
+    """gpf_predict keeps its query-chunk buffers in the context between calls (grow-only): a
+    call after a larger one runs with a smaller leading dimension inside the bigger buffers, a
+    call after set_data with another N reallocates. Every result equals that of a fresh context
+    bit for bit."""
+    import gpfit
+    rng = np.random.default_rng(17)
+    datasets = []
+    for N, d in ((300, 2), (700, 3)):
+        x = rng.uniform(size=(d, N))
+        y = np.sin(4 * x[0]) + 0.1 * rng.standard_normal(N)
+        datasets.append((x, y, rng.uniform(0.05, 0.2, size=N), rng.uniform(0.1, 0.5, size=d)))
+    calls = [(0, 200), (0, 3000), (0, 130), (1, 1000), (1, 64), (0, 500)]
+    a = gpfit.Context(0)
+    kept = []
+    cur = None
+    for k, m in calls:
+        x, y, e, ls = datasets[k]
+        if cur != k:
+            a.set_data(x, y, e)
+            cur = k
+        xf = rng.uniform(size=(x.shape[0], m))
+        kept.append((k, xf, a.predict(ls, xf)))
+    a.close()
+    for k, xf, (mu, sd) in kept:
+        x, y, e, ls = datasets[k]
+        b = gpfit.Context(0)
+        b.set_data(x, y, e)
+        mu0, sd0 = b.predict(ls, xf)
+        b.close()
+        np.testing.assert_array_equal(mu, mu0)
+        np.testing.assert_array_equal(sd, sd0)
+
+
 def test_graph_replay_equals_plain_launches(f2, monkeypatch):
     """Small batches (N <= 256) replay a captured HIP graph padded to all P slots; the scores
     equal the plain launch path bit for bit, across changing sentinel patterns and reuse."""
