@@ -7,6 +7,8 @@ MI355X (gpf_hull_fill, csrc/gpf_hull.hip). Same snapping rule and traversal orde
 convex_hull.py:13-224, so the grid is identical point for point (tests/test_host_glue.py,
 fixtures F6).
 """
+import functools
+
 import numpy as np
 from scipy.spatial import ConvexHull
 
@@ -21,9 +23,27 @@ def _decimals(res):
     return len(txt) - 1 - txt.index(".") if "." in txt else -1
 
 
+@functools.lru_cache(maxsize=64)
+def _trim(res):
+    """(decimals of res, 10.0 ** decimals) for the trim step of round_to_res."""
+    d = _decimals(res)
+    return d, 10.0 ** d
+
+
 def round_to_res(value, res):
     """Nearest multiple of res (Python round: half to even), then trimmed to res's
-    decimals when res < 1 (convex_hull.py:13-24)."""
+    decimals when res < 1 (convex_hull.py:13-24).
+
+    The trim is numpy's float rounding (np.around: multiply by 10**d, round half to even,
+    divide) done on the scalar directly; np.around on one scalar costs ~8 us, and the facet
+    rasterisation calls this once per coordinate of every point it walks
+    (tests/test_host_glue.py::test_host_rasterisation_matches_oracle pins it to the oracle's
+    np.around form)."""
+    if res < 1:
+        d, p10 = _trim(float(res))
+        if d >= 0:  # the same IEEE operations on Python floats
+            r = float(res)
+            return round(round(float(value) / r) * r * p10) / p10
     snapped = round(value / res) * res
     if res < 1:
         snapped = np.around(snapped, _decimals(res))
@@ -32,25 +52,27 @@ def round_to_res(value, res):
 
 def _unique_rows(rows):
     """Distinct rows in lexicographic order (the reference's sorted(set(tuples)))."""
-    return np.array(sorted({tuple(r) for r in rows}))
+    return np.array(sorted({tuple(r) for r in rows.tolist()}))
 
 
 def _segment(a, b, res):
     """Grid points from a to b, stepping along the dimension that needs most steps
-    (convex_hull.py:38-72)."""
+    (convex_hull.py:38-72). The walk runs on Python floats (same operations and order as the
+    reference's numpy scalars, a fraction of their per-operation cost)."""
     lead = int(np.argmax(np.abs((a - b) / res)))
     lo, hi = (a, b) if a[lead] < b[lead] else (b, a)
-    span = hi - lo
+    span = (hi - lo).tolist()
+    lo, hi, rs = lo.tolist(), hi.tolist(), np.asarray(res, dtype=np.float64).tolist()
+    others = [k for k in range(len(lo)) if k != lead]
     pts = [lo]
-    cur = np.array(lo, dtype=np.float64, copy=True)
+    cur = list(lo)
     while cur[lead] < hi[lead]:
-        cur[lead] = round_to_res(cur[lead] + res[lead], res[lead])
+        cur[lead] = round_to_res(cur[lead] + rs[lead], rs[lead])
         frac = (cur[lead] - lo[lead]) / span[lead]
-        for k in range(cur.shape[0]):
-            if k != lead:
-                cur[k] = round_to_res((frac * span[k]) + lo[k], res[k])
-        pts.append(cur.copy())
-    return np.array(pts)
+        for k in others:
+            cur[k] = round_to_res((frac * span[k]) + lo[k], rs[k])
+        pts.append(list(cur))
+    return np.array(pts, dtype=np.float64)
 
 
 def _polygon_outline(corners, res):
@@ -65,25 +87,24 @@ def _polygon_outline(corners, res):
 
 def _scanfill(axis, pts, res):
     """Fill the gaps between consecutive (sorted) points that differ only along
-    `axis`, stepping by res[axis] (convex_hull.py:122-155)."""
-    stride = np.zeros(pts.shape[1])
-    stride[axis] = res[axis]
-    others = [k for k in range(pts.shape[1]) if k != axis]
+    `axis`, stepping by res[axis] (convex_hull.py:122-155); Python floats, as in _segment."""
+    d = pts.shape[1]
+    rows, rs = pts.tolist(), np.asarray(res, dtype=np.float64).tolist()
+    stride = [rs[axis] if j == axis else 0.0 for j in range(d)]
+    others = [k for k in range(d) if k != axis]
     out = []
-    for k in range(len(pts) - 1):
-        a, b = pts[k], pts[k + 1]
-        if not np.all(a[others] == b[others]):
+    for k in range(len(rows) - 1):
+        a, b = rows[k], rows[k + 1]
+        if any(a[j] != b[j] for j in others):
             continue
-        cur = a.copy()
-        out.append(cur.copy())
+        cur = list(a)
+        out.append(cur)
         while cur[axis] < b[axis]:
-            cur = cur + stride
-            for j in range(cur.shape[0]):
-                cur[j] = round_to_res(cur[j], res[j])
-            out.append(cur.copy())
-        out.append(b.copy())
-    out.append(pts[-1])
-    return _unique_rows(np.concatenate((np.array(out), pts)))
+            cur = [round_to_res(cur[j] + stride[j], rs[j]) for j in range(d)]
+            out.append(cur)
+        out.append(list(b))
+    out.append(rows[-1])
+    return _unique_rows(np.concatenate((np.array(out, dtype=np.float64), pts)))
 
 
 def _facet_surface(corners, res):

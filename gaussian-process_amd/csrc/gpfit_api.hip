@@ -561,9 +561,14 @@ static int run_factor(gpf_ctx* c, int pc) {
 
 // ---- convex-hull grid fill helpers (convex_hull.py:122-155,203-224) ----
 namespace {
-struct DevBuf {  // owning device allocation
+struct DevBuf {  // owning device allocation, stream-ordered (no device-wide sync on free)
   void* p = nullptr;
-  ~DevBuf() { if (p) hipFree(p); }
+  hipStream_t st = nullptr;
+  hipError_t alloc(size_t bytes, hipStream_t s) {
+    st = s;
+    return hipMallocAsync(&p, bytes, s);
+  }
+  ~DevBuf() { if (p) hipFreeAsync(p, st); }
   template <typename V> V* as() { return static_cast<V*>(p); }
 };
 inline unsigned blocks_for(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + NTHR - 1) / NTHR); }
@@ -574,16 +579,16 @@ inline unsigned blocks_for(int64_t n) { return (unsigned)std::max<int64_t>(1, (n
 static int hull_sort_unique(gpf_ctx* c, DevBuf& rows, int64_t& n, int d, const int* order) {
   hipStream_t st = c->stream;
   DevBuf perm, perm2, key, key2, flag, pos, temp, out;
-  GPF_HIP(c, hipMalloc(&perm.p, std::max<int64_t>(n, 1) * 8));
-  GPF_HIP(c, hipMalloc(&perm2.p, std::max<int64_t>(n, 1) * 8));
-  GPF_HIP(c, hipMalloc(&key.p, std::max<int64_t>(n, 1) * 8));
-  GPF_HIP(c, hipMalloc(&key2.p, std::max<int64_t>(n, 1) * 8));
+  GPF_HIP(c, perm.alloc(std::max<int64_t>(n, 1) * 8, st));
+  GPF_HIP(c, perm2.alloc(std::max<int64_t>(n, 1) * 8, st));
+  GPF_HIP(c, key.alloc(std::max<int64_t>(n, 1) * 8, st));
+  GPF_HIP(c, key2.alloc(std::max<int64_t>(n, 1) * 8, st));
   hipLaunchKernelGGL(gpf::k_hull_iota, dim3(blocks_for(n)), dim3(NTHR), 0, st, perm.as<int64_t>(), n);
   size_t tb = 0, tb2 = 0;
   GPF_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key.as<uint64_t>(), key2.as<uint64_t>(),
                                                 perm.as<int64_t>(), perm2.as<int64_t>(), n, 0, 64, st));
   GPF_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, perm.as<int64_t>(), perm2.as<int64_t>(), n, st));
-  GPF_HIP(c, hipMalloc(&temp.p, std::max<size_t>(std::max(tb, tb2), 16)));
+  GPF_HIP(c, temp.alloc(std::max<size_t>(std::max(tb, tb2), 16), st));
   for (int q = d - 1; q >= 0; --q) {
     hipLaunchKernelGGL(gpf::k_hull_key, dim3(blocks_for(n)), dim3(NTHR), 0, st, rows.as<double>(),
                        perm.as<int64_t>(), n, d, order[q], key.as<uint64_t>());
@@ -591,8 +596,8 @@ static int hull_sort_unique(gpf_ctx* c, DevBuf& rows, int64_t& n, int d, const i
                                                   perm.as<int64_t>(), perm2.as<int64_t>(), n, 0, 64, st));
     std::swap(perm.p, perm2.p);
   }
-  GPF_HIP(c, hipMalloc(&flag.p, std::max<int64_t>(n, 1) * 8));
-  GPF_HIP(c, hipMalloc(&pos.p, std::max<int64_t>(n, 1) * 8));
+  GPF_HIP(c, flag.alloc(std::max<int64_t>(n, 1) * 8, st));
+  GPF_HIP(c, pos.alloc(std::max<int64_t>(n, 1) * 8, st));
   hipLaunchKernelGGL(gpf::k_hull_flag, dim3(blocks_for(n)), dim3(NTHR), 0, st, rows.as<double>(), perm.as<int64_t>(),
                      n, d, flag.as<int64_t>());
   GPF_HIP(c, hipcub::DeviceScan::ExclusiveSum(temp.p, tb2, flag.as<int64_t>(), pos.as<int64_t>(), n, st));
@@ -601,7 +606,7 @@ static int hull_sort_unique(gpf_ctx* c, DevBuf& rows, int64_t& n, int d, const i
   GPF_HIP(c, hipMemcpyAsync(&last[1], flag.as<int64_t>() + (n - 1), 8, hipMemcpyDeviceToHost, st));
   GPF_HIP(c, hipStreamSynchronize(st));
   const int64_t m = last[0] + last[1];
-  GPF_HIP(c, hipMalloc(&out.p, std::max<int64_t>(m, 1) * d * 8));
+  GPF_HIP(c, out.alloc(std::max<int64_t>(m, 1) * d * 8, st));
   hipLaunchKernelGGL(gpf::k_hull_compact, dim3(blocks_for(n)), dim3(NTHR), 0, st, rows.as<double>(),
                      perm.as<int64_t>(), flag.as<int64_t>(), pos.as<int64_t>(), n, d, out.as<double>());
   GPF_HIP(c, hipGetLastError());
@@ -1283,7 +1288,7 @@ int gpf_hull_fill(gpf_ctx* c, const double* shell, int64_t n, int d, const doubl
   }
   hipStream_t st = c->stream;
   DevBuf rows;
-  GPF_HIP(c, hipMalloc(&rows.p, (size_t)n * d * 8));
+  GPF_HIP(c, rows.alloc((size_t)n * d * 8, st));
   GPF_HIP(c, hipMemcpyAsync(rows.p, shell, (size_t)n * d * 8, hipMemcpyHostToDevice, st));
   std::vector<int> order(d);
   for (int j = 0; j < d; ++j) order[j] = j;
@@ -1293,20 +1298,20 @@ int gpf_hull_fill(gpf_ctx* c, const double* shell, int64_t n, int d, const doubl
     // pass i: the grid is sorted by columns i, i+1, .., i-1 (mod d); fill along the last of them
     hd.axis = (d - 1 + i) % d;
     DevBuf cnt, off, temp, grown;
-    GPF_HIP(c, hipMalloc(&cnt.p, (size_t)n * 8));
-    GPF_HIP(c, hipMalloc(&off.p, (size_t)n * 8));
+    GPF_HIP(c, cnt.alloc((size_t)n * 8, st));
+    GPF_HIP(c, off.alloc((size_t)n * 8, st));
     hipLaunchKernelGGL(gpf::k_hull_count, dim3(blocks_for(n)), dim3(NTHR), 0, st, rows.as<double>(), n, hd,
                        cnt.as<int64_t>());
     size_t tb = 0;
     GPF_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt.as<int64_t>(), off.as<int64_t>(), n, st));
-    GPF_HIP(c, hipMalloc(&temp.p, std::max<size_t>(tb, 16)));
+    GPF_HIP(c, temp.alloc(std::max<size_t>(tb, 16), st));
     GPF_HIP(c, hipcub::DeviceScan::ExclusiveSum(temp.p, tb, cnt.as<int64_t>(), off.as<int64_t>(), n, st));
     int64_t last[2] = {0, 0};
     GPF_HIP(c, hipMemcpyAsync(&last[0], off.as<int64_t>() + (n - 1), 8, hipMemcpyDeviceToHost, st));
     GPF_HIP(c, hipMemcpyAsync(&last[1], cnt.as<int64_t>() + (n - 1), 8, hipMemcpyDeviceToHost, st));
     GPF_HIP(c, hipStreamSynchronize(st));
     const int64_t add = last[0] + last[1];
-    GPF_HIP(c, hipMalloc(&grown.p, (size_t)(n + add) * d * 8));
+    GPF_HIP(c, grown.alloc((size_t)(n + add) * d * 8, st));
     GPF_HIP(c, hipMemcpyAsync(grown.p, rows.p, (size_t)n * d * 8, hipMemcpyDeviceToDevice, st));
     hipLaunchKernelGGL(gpf::k_hull_emit, dim3(blocks_for(n)), dim3(NTHR), 0, st, rows.as<double>(), n, hd,
                        off.as<int64_t>(), grown.as<double>() + (size_t)n * d);

@@ -61,6 +61,33 @@ def test_round_to_res_quirks():
     assert round_to_res(7.0, 2) == 8
 
 
+def test_host_rasterisation_matches_oracle():
+    """The drop-in's facet rasterisation (Python-float walks, scalar trim instead of np.around)
+    against the oracle's numpy-scalar restatement (oracle/ref_hull.py, pinned to the
+    reference's grids F6): round_to_res on random values and exact ties, and every facet's
+    shell of random off-grid hulls in 2-4 dimensions, bit for bit and in the same order."""
+    from scipy.spatial import ConvexHull
+    import convex_hull as ch
+    from oracle import ref_hull as rh
+    rng = np.random.default_rng(29)
+    resolutions = [0.005, 0.01, 0.02, 0.25, 0.1, 1e-05, 0.3, 1.0, 2.0, 0.125]
+    for r in resolutions:
+        vals = np.concatenate([rng.uniform(-3, 3, 200), (np.arange(-20, 20) + 0.5) * r,
+                               rng.integers(-50, 50, 40) * r, [0.0, -0.0]])
+        for v in vals:
+            got, want = ch.round_to_res(v, r), rh.round_to_res(v, r)
+            assert got == want and np.signbit(got) == np.signbit(want), (v, r)
+    cases = [(2, 15, [0.005, 0.01]), (2, 9, [0.25, 0.1]), (3, 10, [0.02, 0.05, 0.04]),
+             (3, 8, [0.1, 0.3, 0.2]), (4, 9, [0.1, 0.2, 0.25, 0.1]), (2, 7, [1.0, 2.0])]
+    for d, n, res in cases:
+        pts = rng.uniform(-1.0, 2.0, size=(n, d)) * (np.max(res) * 20 if max(res) >= 1 else 1.0)
+        res = np.asarray(res)
+        for simplex in ConvexHull(pts).simplices:
+            corners = pts[list(simplex)]
+            got, want = ch._facet_surface(corners, res), rh._facet_surface(corners, res)
+            assert got.shape == want.shape and np.array_equal(got, want), (d, n, list(res))
+
+
 def test_prob_surface_oracle_matches_reference(tmp_path):
     """The host restatement (checker of the GPU kernel), written through the same object-frame
     to_csv as calc_prob_surf.py:84-86, equals the reference's output file F7 bit for bit."""
