@@ -294,9 +294,13 @@ static int step_group(int pc) {
 // filling ~512 workgroup slots. Measured (profiles/r1/split_k_ab.txt): single-particle factor at
 // N=4096 11.3 -> 9.9 ms with S=16 (7.4 ms since the partials are stored write-through, with no
 // release fence); config B (224 tiles, S=2) 21.3k -> 14.3k evals/s with the fence, hence the
-// threshold. GPF_SPLIT_K overrides (1 = off). Not for tiny problems (nt < 4).
+// threshold. At most 8 pieces since round 2 (with the split-K reduction tree and the early
+// diagonal factor): an L tile's depth is 8J 16-deep chunks, so 8 pieces are always even while
+// 16 leave odd-J tiles uneven and J = 1 tiles with empty pieces — single-particle factor at
+// N=4096 4.17 -> 3.90 ms, N=2048 equal, N=8192 already 8 (512/63), S=16 there 16.4 vs 13.5 ms
+// (profiles/r2/predict_splitk_ab.txt). GPF_SPLIT_K overrides (1 = off). Not for tiny problems (nt < 4).
 static int split_k(int tiles, int nt) {
-  int S = (nt >= 4 && GPF_KFUSE && tiles <= 64) ? std::max(1, std::min(16, 512 / std::max(1, tiles))) : 1;
+  int S = (nt >= 4 && GPF_KFUSE && tiles <= 64) ? std::max(1, std::min(8, 512 / std::max(1, tiles))) : 1;
   if (const char* s = getenv("GPF_SPLIT_K")) S = std::max(1, std::min(32, atoi(s)));
   if (nt < 4 || !GPF_KFUSE) S = 1;
   return S;

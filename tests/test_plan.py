@@ -79,7 +79,7 @@ def test_default_plans_of_the_baseline_configs(env):
     b = gpfit.plan_check(32, 8)             # config B: critical-tile split
     assert b["groups"] == 1 and b["S"] == 1 and b["Smax"] > 1 and b["split_tiles"] > 0
     one = gpfit.plan_check(1, 32)           # prediction: single particle, all tiles split
-    assert one["S"] == 16 and one["whole_tiles"] == 31  # J = 0 has nothing to split
+    assert one["S"] == 8 and one["whole_tiles"] == 31  # J = 0 has nothing to split; 8 pieces (8J chunks)
     # early diagonal factor where launches leave slots idle (B, the prediction), the fused factor
     # where they are slot-bound (C, D's and E's shares)
     assert e["diag_workgroups"] == 0
