@@ -360,14 +360,18 @@ static int deep_syrk() {
 // Needs the particle-fastest tile order (grp = 0). pc: the particles of all concurrent groups
 // (they share the 512 workgroup slots). Pieces of at least 16 16-deep chunks: shorter ones lose
 // more to the partial round trip than they save (A/B, profiles/r1/split_crit_ab.txt: N=1024
-// P=32 +2.4%, -5..-12% with 8-chunk pieces; N=2048 P=32 +9%).
-// GPF_SPLIT_CRIT = maximum S (1 = off), GPF_SPLIT_CRIT_MIN = minimum chunks per piece.
+// P=32 +2.4%, -5..-12% with 8-chunk pieces; N=2048 P=32 +9%). Off by default since the end of
+// round 2: with the early diagonal factor these launches wait for the diagonal block, not for
+// the critical tile's GEMM, and the pieces' hand-offs only cost (same box, profiles/r2/
+// split_crit_off_ab.txt: N=1024 P=32 +1.4% off, N=3072 P=16 +3.0% off, N=1536/2048 P=32 within
+// 0.6%). GPF_SPLIT_CRIT = maximum S (default 1 = off; 4 was the round-1 default),
+// GPF_SPLIT_CRIT_MIN = minimum chunks per piece.
 static int split_crit(int pc, int nt, int J, int grp, int S_all) {
   // the last launch (J = nt-1) has no L tiles: its w = 0 is a U tile, which never splits
   if (S_all > 1 || grp > 0 || J == 0 || J >= nt - 1 || nt < 4 || !GPF_KFUSE) return 1;
   // + the diagonal and the quadrant workgroups
   const int slots = 512, tiles = pc * (nt - 1) + (early_diag(pc, nt) ? pc : 0) + (quad_finish(pc, nt) ? 4 * pc : 0);
-  int S = 4, minch = 16;
+  int S = 1, minch = 16;
   if (const char* s = getenv("GPF_SPLIT_CRIT")) S = std::max(1, std::min(32, atoi(s)));
   if (const char* s = getenv("GPF_SPLIT_CRIT_MIN")) minch = std::max(2, atoi(s));
   const int nch = J * T / gpf::DL_KC;

@@ -4,7 +4,8 @@
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/envab
 declare -A CFG=( [B]="--n 1024 --d 2 --swarm-per-gpu 32" [C]="--n 4096 --d 3 --swarm-per-gpu 64"
-                 [D]="--n 4096 --d 3 --swarm-per-gpu 32" [E]="--n 16384 --d 4 --swarm-per-gpu 16 --hetero" )
+                 [D]="--n 4096 --d 3 --swarm-per-gpu 32" [E]="--n 16384 --d 4 --swarm-per-gpu 16 --hetero"
+                 [F]="--n 2048 --d 3 --swarm-per-gpu 32" [G]="--n 1536 --d 2 --swarm-per-gpu 32" [H]="--n 3072 --d 3 --swarm-per-gpu 16" )
 for e in $ENV_LIST; do
   for c in ${CFGS:-C}; do
     tag=${e//[^A-Za-z0-9]/_}_${c}_$RANDOM

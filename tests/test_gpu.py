@@ -459,10 +459,11 @@ def test_critical_tile_split_matches_unsplit_and_oracle(ctx, monkeypatch, split)
 
 @pytest.mark.parametrize("N,d", [(700, 2), (1920, 3)])
 def test_default_critical_split_live_counts(ctx, monkeypatch, N, d):
-    """The default critical-tile split (on whenever a launch leaves slots idle, up to the last
-    block column, whose w = 0 tile is a U tile and must not be duplicated) across changing
-    live-particle counts (sentinels never run; buffers grow between batches): deterministic,
-    and within 1e-10 of the unsplit path (GPF_SPLIT_CRIT=1)."""
+    """The critical-tile split at its round-1 default (GPF_SPLIT_CRIT=4: on whenever a launch
+    leaves slots idle, up to the last block column, whose w = 0 tile is a U tile and must not be
+    duplicated; off by default since round 2) across changing live-particle counts (sentinels
+    never run; buffers grow between batches): deterministic, and within 1e-10 of the unsplit
+    path (GPF_SPLIT_CRIT=1, the default)."""
     rng = np.random.default_rng(N + d)
     x = rng.uniform(size=(d, N))
     y = np.sin(3 * x[0]) + 0.1 * rng.standard_normal(N)
@@ -477,12 +478,13 @@ def test_default_critical_split_live_counts(ctx, monkeypatch, N, d):
     for m in masks:
         Q = P.copy()
         Q[m, 0] = hi[0] + 1.0  # sentinels: outside the box
-        monkeypatch.delenv("GPF_SPLIT_CRIT", raising=False)
+        monkeypatch.setenv("GPF_SPLIT_CRIT", "4")
         g = ctx.eval_batch(Q)
         np.testing.assert_array_equal(g, ctx.eval_batch(Q))  # deterministic
         monkeypatch.setenv("GPF_SPLIT_CRIT", "1")
         w = ctx.eval_batch(Q)
         monkeypatch.delenv("GPF_SPLIT_CRIT", raising=False)
+        np.testing.assert_array_equal(w, ctx.eval_batch(Q))  # the default is the unsplit path
         assert np.all(g[m] == 1e13)
         assert _rel(g, w) < 1e-10
         got.append(g)
@@ -604,6 +606,7 @@ def test_early_diagonal_factor_matches_fused(ctx, monkeypatch, N, d, P):
     ctx.set_grid(s, ex, lo, hi)
     Q = rng.uniform(0.1, 0.5, size=(P, d))
     out = {}
+    monkeypatch.setenv("GPF_SPLIT_CRIT", "4")  # the critical-split path (off by default since round 2)
     for mode, ed, qf, deep in (("fused", "0", "0", "0"), ("fused_deep", "0", "0", "1"), ("fused_pre", "0", "0", "2"),
                                ("ed", "1", "0", "0"), ("quad", "1", "1", "0")):
         monkeypatch.setenv("GPF_EARLY_DIAG", ed)

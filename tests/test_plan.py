@@ -76,8 +76,12 @@ def test_default_plans_of_the_baseline_configs(env):
     assert d["groups"] == 2
     e = gpfit.plan_check(16, 128)           # config E's per-GPU share at N=16384
     assert e["groups"] == 2
-    b = gpfit.plan_check(32, 8)             # config B: critical-tile split
-    assert b["groups"] == 1 and b["S"] == 1 and b["Smax"] > 1 and b["split_tiles"] > 0
+    b = gpfit.plan_check(32, 8)             # config B: one group, no split (critical split off by default)
+    assert b["groups"] == 1 and b["S"] == 1 and b["Smax"] == 1 and b["split_tiles"] == 0
+    env({"GPF_SPLIT_CRIT": "4"})            # ... and with the critical-tile split asked for
+    bs = gpfit.plan_check(32, 8)
+    assert bs["S"] == 1 and bs["Smax"] > 1 and bs["split_tiles"] > 0
+    env({})
     one = gpfit.plan_check(1, 32)           # prediction: single particle, all tiles split
     assert one["S"] == 8 and one["whole_tiles"] == 31  # J = 0 has nothing to split; 8 pieces (8J chunks)
     # early diagonal factor where launches leave slots idle (B, the prediction), the fused factor
