@@ -38,8 +38,8 @@ template <int TM> struct TileCfg;
 #ifndef GPF_STEP_KC
 #define GPF_STEP_KC 16  // K depth per LDS stage of the 128-tile GEMMs (build-time tuning knob)
 #endif
-template <> struct TileCfg<128> {  // the factorisation / prediction GEMMs: 8 waves, 64x32 per wave
-  static constexpr int KC = GPF_STEP_KC, NW = 8, WR = 2, WC = 4;
+template <> struct TileCfg<128> {  // the factorisation / prediction GEMMs: 8 waves, 128x16 per wave
+  static constexpr int KC = GPF_STEP_KC, NW = 8, WR = 1, WC = 8;
 };
 template <> struct TileCfg<64> {   // LDS-resident 64x64 products inside the diagonal factor: 8 waves, 32x16 each
   static constexpr int KC = 32, NW = 8, WR = 2, WC = 4;
@@ -53,26 +53,18 @@ template <int TM> struct Geo {
   static constexpr int NTH = 64 * NW;
   static constexpr int MBR = TM / WR / 16;
   static constexpr int MBC = TM / WC / 16;
-  // [row][k] staging stride: odd, so 16 consecutive rows hit 16 distinct bank pairs both for
-  // ds_read_b64 (banks mod 64) and for the ds_read2_b64 the compiler pairs them into (mod 32)
-  static constexpr int RK = KC + 1;
-  static constexpr int KN = TM + 16;  // [k][col] staging stride (2*ld == 32 mod 64 dwords)
-  static constexpr int SA = TM * RK;
-  static constexpr int SB = (TM * RK > KC * KN) ? TM * RK : KC * KN;
-  static constexpr int STAGE = 2 * (SA + SB);  // double-buffered A + B chunks (doubles)
-  static constexpr int NLD = TM * KC / 2 / NTH;  // 16-byte loads per thread per operand per chunk
-  static_assert(NLD * 2 * NTH == TM * KC, "staging map");
   static_assert(WR * WC == NW, "wave grid");
 };
 
-// Wave -> sub-tile map. The waves of a workgroup are dealt round-robin over the CU's 4
-// SIMDs (wave w on SIMD w % 4), so with WC = 4 the two waves sharing a SIMD own the
-// same column slab in the two row halves. Under a triangular operand (TRI_B_*) or a
-// lower-only output (TRI_C_LOWER) the skipped MFMAs then pile onto the same SIMDs:
-// in the 128-wide TRMM one SIMD issues all of its blocks while another issues an
-// eighth. GPF_BAL mirrors the column slabs of the second row half (wc -> WC-1-wc), so
-// each SIMD pairs a light slab with a heavy one. Any map is a permutation of the same
-// per-element work: results are bitwise unchanged.
+// Wave -> sub-tile map. The 8 waves of a workgroup sit two to a SIMD: waves w and w + 4 share
+// one (the dispatcher deals them cyclically over the CU's 4 SIMDs). Under a triangular
+// operand or a lower-only output (Tri) the live MFMAs of a sub-tile depend on where it sits,
+// so the map pairs a light sub-tile with a heavy one on every SIMD:
+//   128-tiles (WR = 1, WC = 8): wave w owns all 128 rows of the 16-column slab w (w < 4) or
+//     11 - w (w >= 4), so SIMD s holds slabs s and 7 - s (a lower-only SYRK: 9 live 16x16
+//     blocks per SIMD for every s);
+//   64-tiles (WR = 2, WC = 4): the column slabs of the second row half are mirrored.
+// Any map is a permutation of the same per-element work: results are bitwise unchanged.
 #ifndef GPF_BAL
 #define GPF_BAL 1
 #endif
@@ -82,11 +74,15 @@ template <int TM> struct Quad {
     const int tid = threadIdx.x;
     lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar) tile origin
-    const int wr = w / Geo<TM>::WC, wc = w % Geo<TM>::WC;
-    rb = wr * (TM / Geo<TM>::WR);
-    cb = ((GPF_BAL && (wr & 1)) ? (Geo<TM>::WC - 1 - wc) : wc) * (TM / Geo<TM>::WC);
+    if constexpr (Geo<TM>::WR == 1) {
+      rb = 0;
+      cb = ((GPF_BAL && w >= 4) ? 11 - w : w) * (TM / Geo<TM>::WC);
+    } else {
+      const int wr = w / Geo<TM>::WC, wc = w % Geo<TM>::WC;
+      rb = wr * (TM / Geo<TM>::WR);
+      cb = ((GPF_BAL && (wr & 1)) ? (Geo<TM>::WC - 1 - wc) : wc) * (TM / Geo<TM>::WC);
+    }
   }
-  __device__ __forceinline__ int wrow() const { return (threadIdx.x >> 6) / Geo<TM>::WC; }
   __device__ __forceinline__ int row(int mi, int r) const { return rb + mi * 16 + (lane >> 4) + 4 * r; }
   __device__ __forceinline__ int col(int ni) const { return cb + ni * 16 + (lane & 15); }
 };
@@ -171,57 +167,6 @@ template <int TM> struct Acc {
   }
 };
 
-// ----------------------------------------------------------------------------
-// Streaming tile GEMM: acc(TM x TM) += A(TM x K) * B(K x TM)
-//   A (r,k) at Ap[r*lda + k]                      (row panel, k contiguous)
-//   B (k,c) at Bp[c*ldb + k]   (!NN: B^T given as a row panel)
-//           at Bp[k*ldb + c]   ( NN: B given as a row panel)
-// K is a multiple of KC. Chunks are double-buffered through LDS: the global loads
-// of chunk t+1 are in flight while chunk t feeds the MFMAs; one barrier per chunk.
-// NEG stages A negated, i.e. acc -= A B (sign flips are exact: acc = C - A B
-// rounds exactly like a subtraction). Ends with a barrier, so the staging area
-// may be reused right after.
-// ----------------------------------------------------------------------------
-template <int TM, bool NN>
-__device__ __forceinline__ void stage_load(d2 (&ra)[Geo<TM>::NLD], d2 (&rb)[Geo<TM>::NLD],
-                                           const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
-                                           int ldb, int k0, int tid) {
-  constexpr int KC = Geo<TM>::KC;
-#pragma unroll
-  for (int u = 0; u < Geo<TM>::NLD; ++u) {
-    const int q = tid + Geo<TM>::NTH * u;
-    const int row = q / (KC / 2), c2 = q % (KC / 2);
-    ra[u] = *reinterpret_cast<const d2*>(Ap + (size_t)row * lda + k0 + 2 * c2);
-    if (!NN) {
-      rb[u] = *reinterpret_cast<const d2*>(Bp + (size_t)row * ldb + k0 + 2 * c2);
-    } else {
-      const int kr = q / (TM / 2), cc = q % (TM / 2);
-      rb[u] = *reinterpret_cast<const d2*>(Bp + (size_t)(k0 + kr) * ldb + 2 * cc);
-    }
-  }
-}
-
-template <int TM, bool NN, bool NEG>
-__device__ __forceinline__ void stage_store(double* sA, double* sB, const d2 (&ra)[Geo<TM>::NLD],
-                                            const d2 (&rb)[Geo<TM>::NLD], int tid) {
-  constexpr int KC = Geo<TM>::KC, RK = Geo<TM>::RK, KN = Geo<TM>::KN;
-#pragma unroll
-  for (int u = 0; u < Geo<TM>::NLD; ++u) {
-    const int q = tid + Geo<TM>::NTH * u;
-    const int row = q / (KC / 2), c2 = q % (KC / 2);
-    const d2 va = NEG ? -ra[u] : ra[u];
-    sA[row * RK + 2 * c2] = va.x;  // odd stride: 8-byte aligned rows, two b64 stores
-    sA[row * RK + 2 * c2 + 1] = va.y;
-    if (!NN) {
-      sB[row * RK + 2 * c2] = rb[u].x;
-      sB[row * RK + 2 * c2 + 1] = rb[u].y;
-    } else {
-      const int kr = q / (TM / 2), cc = q % (TM / 2);
-      *reinterpret_cast<d2*>(sB + kr * KN + 2 * cc) = rb[u];
-    }
-  }
-}
-
 // Known-zero structure of a GEMM's operands or unneeded output: MFMAs whose
 // 16x16x4 block is entirely zero (or whose output block is never read) are
 // skipped by a wave-uniform branch. Skipping adds of exact zeros leaves every
@@ -242,59 +187,6 @@ __device__ __forceinline__ bool tri_live(int R0, int C0, int k) {
   if (TRI == TRI_A_KLER) return k <= R0 + 15;
   if (TRI == TRI_C_LOWER) return C0 <= R0 + 15;
   return true;
-}
-
-template <int TM, bool NN, int TRI = TRI_NONE>
-__device__ __forceinline__ void stage_mma(Acc<TM>& acc, const double* sA, const double* sB, const Quad<TM>& qd,
-                                          int k0 = 0) {
-  constexpr int KC = Geo<TM>::KC, RK = Geo<TM>::RK, KN = Geo<TM>::KN;
-  constexpr int MBR = Geo<TM>::MBR, MBC = Geo<TM>::MBC;
-  const int lr = qd.lane & 15, lk = qd.lane >> 4;
-#pragma unroll
-  for (int ks = 0; ks < KC; ks += 4) {
-    double a[MBR], b[MBC];
-#pragma unroll
-    for (int mi = 0; mi < MBR; ++mi) a[mi] = sA[(qd.rb + mi * 16 + lr) * RK + ks + lk];
-#pragma unroll
-    for (int ni = 0; ni < MBC; ++ni) {
-      if (!NN)
-        b[ni] = sB[(qd.cb + ni * 16 + lr) * RK + ks + lk];
-      else
-        b[ni] = sB[(ks + lk) * KN + qd.cb + ni * 16 + lr];
-    }
-#pragma unroll
-    for (int mi = 0; mi < MBR; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < MBC; ++ni)
-        if (tri_live<TRI>(qd.rb + mi * 16, qd.cb + ni * 16, k0 + ks)) acc.v[mi][ni] = mfma(a[mi], b[ni], acc.v[mi][ni]);
-  }
-}
-
-template <int TM, bool NN, bool NEG = false, int TRI = TRI_NONE>
-__device__ void gemm_stream(Acc<TM>& acc, const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
-                            int ldb, int K, double* smem, const Quad<TM>& qd) {
-  constexpr int KC = Geo<TM>::KC, SA = Geo<TM>::SA, SB = Geo<TM>::SB, NLD = Geo<TM>::NLD;
-  const int tid = threadIdx.x;
-  const int nch = K / KC;
-  if (nch <= 0) return;
-  Ap = launder(Ap);
-  Bp = launder(Bp);
-  d2 ra[NLD], rb[NLD];
-  stage_load<TM, NN>(ra, rb, Ap, lda, Bp, ldb, 0, tid);
-  stage_store<TM, NN, NEG>(smem, smem + SA, ra, rb, tid);
-  __syncthreads();
-#pragma unroll 1
-  for (int t = 0; t < nch; ++t) {
-    const bool more = (t + 1) < nch;
-    if (more) stage_load<TM, NN>(ra, rb, Ap, lda, Bp, ldb, (t + 1) * KC, tid);
-    const double* cur = smem + (t & 1) * (SA + SB);
-    stage_mma<TM, NN, TRI>(acc, cur, cur + SA, qd, t * KC);
-    if (more) {
-      double* nxt = smem + ((t + 1) & 1) * (SA + SB);
-      stage_store<TM, NN, NEG>(nxt, nxt + SA, ra, rb, tid);
-    }
-    __syncthreads();
-  }
 }
 
 // ----------------------------------------------------------------------------
@@ -338,6 +230,13 @@ __device__ __forceinline__ void dl_load(const double* g, double* l) {
   __builtin_amdgcn_global_load_lds((const void*)g, (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 #endif
 }
+// The same transfer in the saddr form: a wave-uniform 64-bit base in SGPRs plus a 32-bit per-lane
+// byte offset, so the streamed GEMMs keep one VGPR per transfer stream instead of forming a 64-bit
+// address per lane and transfer.
+__device__ __forceinline__ void dl_load_s(const void* base, uint32_t off, double* l) {
+  const uint32_t m = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)l;
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(base), "{m0}"(m) : "memory");
+}
 
 // Slot swizzle of the [r][k] panels: k-pair kp of row r sits in slot kp ^ dl_sw(r). An MFMA
 // operand read takes 16 consecutive rows at one k per half-wave; rows r and r+8 share a bank
@@ -349,31 +248,39 @@ __device__ __forceinline__ void dl_load(const double* g, double* l) {
 #endif
 __device__ __forceinline__ int dl_sw(int r) { return GPF_DL_SW ? ((r >> 1) & 7) : (r & 7); }
 
-// Dense chunks [t0, t1) (every MFMA block live) with no VALU address work inside the loop:
-// VALU ops do not overlap the FP64 MFMAs of their SIMD, so each one costs issue time. The per-lane
-// LDS byte offsets are formed once per call; the buffer parity is unrolled, so buffer, k-step and
-// row/column-block displacements are ds_read immediates; the global sources are a scalar chunk
-// base plus a fixed 32-bit per-lane byte offset (the saddr form of global_load_lds).
+// Per-lane LDS byte offsets of an MFMA A-operand read from a [r][k] panel in the dl_sw layout
+// (rows r0 + (lane & 15), r0 a multiple of 16; depth 4 s + (lane >> 4) of a 16-deep chunk), for
+// the k-steps s = 0..3 of a chunk. Row-block and chunk displacements are added as immediates.
+__device__ __forceinline__ void dl_row_offsets(int lane, uint32_t (&o)[4]) {
+  const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) o[s] = 8u * (uint32_t)(lr * DL_KC + 2 * ((2 * s + (lk >> 1)) ^ dl_sw(lr)) + (lk & 1));
+}
+
+// Dense chunks [t0, t1) with no VALU address work inside the loop: VALU ops do not overlap the
+// FP64 MFMAs of their SIMD, so each one costs issue time. The per-lane LDS byte offsets are formed
+// once per call; the buffer parity is unrolled, so buffer, k-step and row-block displacements are
+// ds_read immediates; the global sources are a scalar chunk base plus a fixed 32-bit per-lane
+// byte offset (the saddr form of global_load_lds). Wave layout of the 128-tiles: all 128 rows
+// (8 row blocks) x one 16-column slab, so a k-step is 8 A reads, 1 B read and 8 MFMAs.
 template <bool NN, bool NEG>
 struct DenseRun {
-  uint32_t la[4], lb[4];  // LDS read offsets (bytes) per k-step: A rows, B^T rows (!NN) / B (NN, [0..1] per ni)
+  static constexpr int MBR = Geo<128>::MBR;  // 8
+  static_assert(Geo<128>::MBC == 1 && Geo<128>::WR == 1, "128-tile wave layout: all rows x one column slab");
+  uint32_t la[4], lb[4];  // LDS read offsets (bytes) per k-step: A rows, B^T rows (!NN) / B (NN, [0] only)
   uint32_t ga[2], gb[2];  // global byte offsets of the two 1 KiB blocks per operand this wave fills
   int blk0;               // first block index of this wave
 
   __device__ __forceinline__ DenseRun(const Quad<128>& qd, int lda, int ldb, int wave) {
     const int lane = qd.lane, lr = lane & 15, lk = lane >> 4;
+    dl_row_offsets(lane, la);
+    if (!NN) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int kp = 2 * s + (lk >> 1);
-      la[s] = 8u * (uint32_t)((qd.rb + lr) * DL_KC + 2 * (kp ^ dl_sw(lr)) + (lk & 1));
-      if (!NN) lb[s] = 8u * (uint32_t)(128 * DL_KC + (qd.cb + lr) * DL_KC + 2 * (kp ^ dl_sw(lr)) + (lk & 1));
-    }
-    if (NN) {
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni) {
-        const int col = qd.cb + ni * 16 + lr;
-        lb[ni] = 8u * (uint32_t)(128 * DL_KC + lk * 128 + 2 * ((col >> 1) ^ (8 * (lk & 3))) + (col & 1));
-      }
+      for (int s = 0; s < 4; ++s) lb[s] = la[s] + 8u * (uint32_t)(128 * DL_KC + qd.cb * DL_KC);  // dl_sw(cb + lr) = dl_sw(lr)
+    } else {
+      const int col = qd.cb + lr;
+      lb[0] = 8u * (uint32_t)(128 * DL_KC + lk * 128 + 2 * ((col >> 1) ^ (8 * (lk & 3))) + (col & 1));
+      lb[1] = lb[2] = lb[3] = lb[0];
     }
     blk0 = 2 * wave;
 #pragma unroll
@@ -392,67 +299,65 @@ struct DenseRun {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int blk = blk0 + u;
-      dl_load((const double*)(Ac + ga[u]), sbuf + blk * 8 * DL_KC);
-      dl_load((const double*)(Bc + gb[u]), sbuf + 128 * DL_KC + (NN ? blk * 128 : blk * 8 * DL_KC));
+      dl_load_s(Ac, ga[u], sbuf + blk * 8 * DL_KC);
+      dl_load_s(Bc, gb[u], sbuf + 128 * DL_KC + (NN ? blk * 128 : blk * 8 * DL_KC));
     }
   }
 
-  // operand reads of k-step s; only rows mi >= MLO and the live columns (patterns as in dl_mma_live)
-  template <int M0 = 0, int M1 = 0>
-  __device__ __forceinline__ void reads(const char* sb, int s, double (&a)[4], double (&b)[2]) const {
-    constexpr int MLO = M0 < M1 ? M0 : M1;
+  // operand reads of k-step s for the row blocks mi >= M0
+  template <int M0>
+  __device__ __forceinline__ void reads(const char* sb, int s, double (&a)[MBR], double& b) const {
 #pragma unroll
-    for (int mi = MLO; mi < 4; ++mi) a[mi] = *(const double*)(sb + la[s] + mi * 16 * DL_KC * 8);
-#pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
-      if ((ni == 0 ? M0 : M1) >= 4) continue;
-      b[ni] = NN ? *(const double*)(sb + lb[ni] + s * 512 * 8) : *(const double*)(sb + lb[s] + ni * 16 * DL_KC * 8);
-    }
+    for (int mi = M0; mi < MBR; ++mi) a[mi] = *(const double*)(sb + la[s] + mi * 16 * DL_KC * 8);
+    b = NN ? *(const double*)(sb + lb[0] + s * 512 * 8) : *(const double*)(sb + lb[s]);
   }
 
-  template <int BUF, int M0 = 0, int M1 = 0>
+  // the MFMAs of one chunk for the row blocks mi >= M0 (M0 = MBR: none). GPF_OPBUF = 2 reads the
+  // operands of k-step s+1 into a second register set before the MFMAs of step s; 1 (default)
+  // reuses one set (the 8 x 1 wave layout needs 9 operands per k-step, and the second set would
+  // push the accumulator-resident finishes over the 128-register budget of 4 waves per SIMD).
+#ifndef GPF_OPBUF
+#define GPF_OPBUF 1
+#endif
+  template <int BUF, int M0>
   __device__ __forceinline__ void mma(Acc<128>& acc, const double* smem) const {
-    if constexpr (M0 >= 4 && M1 >= 4) return;
-    constexpr int MLO = M0 < M1 ? M0 : M1;
+    if constexpr (M0 >= MBR) return;
     const char* sb = (const char*)smem + BUF * DL_BUF * 8;
-    // operands of k-step s+1 are read into the other register set before the MFMAs of step s
-    double a[2][4], b[2][2];
-    reads<M0, M1>(sb, 0, a[0], b[0]);
+    constexpr int NB = GPF_OPBUF;
+    double a[NB][MBR], b[NB];
+    reads<M0>(sb, 0, a[0], b[0]);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      if (s < 3) reads<M0, M1>(sb, s + 1, a[(s + 1) & 1], b[(s + 1) & 1]);
+      if (NB == 2 && s < 3) reads<M0>(sb, s + 1, a[(s + 1) % NB], b[(s + 1) % NB]);
 #pragma unroll
-      for (int mi = MLO; mi < 4; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-          if (mi >= (ni == 0 ? M0 : M1))
-            acc.v[mi][ni] = NEG ? mfma_neg_a(a[s & 1][mi], b[s & 1][ni], acc.v[mi][ni])
-                                : mfma(a[s & 1][mi], b[s & 1][ni], acc.v[mi][ni]);
+      for (int mi = M0; mi < MBR; ++mi)
+        acc.v[mi][0] = NEG ? mfma_neg_a(a[s % NB][mi], b[s % NB], acc.v[mi][0]) : mfma(a[s % NB][mi], b[s % NB], acc.v[mi][0]);
+      if (NB == 1 && s < 3) reads<M0>(sb, s + 1, a[0], b[0]);
     }
   }
 
-  template <int BUF, int M0 = 0, int M1 = 0>
+  template <int BUF, int M0>
   __device__ __forceinline__ void chunk(Acc<128>& acc, const double* Ap, const double* Bp, int ldb, int t, int nch,
                                         double* smem) const {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t + 1 < nch) issue<1 - BUF>(Ap, Bp, ldb, t + 1, smem);
-    mma<BUF, M0, M1>(acc, smem);
+    mma<BUF, M0>(acc, smem);
   }
 
-  // chunks [t0, t1) with one MFMA pattern (M0, M1 as in dl_mma_live; <4, 4> keeps only the
+  // chunks [t0, t1) with one MFMA pattern (row blocks mi >= M0; M0 = MBR keeps only the
   // transfers and barriers)
-  template <int M0 = 0, int M1 = 0>
+  template <int M0>
   __device__ __forceinline__ void run(Acc<128>& acc, const double* Ap, const double* Bp, int ldb, int t0, int t1,
                                       int nch, double* smem) const {
     int t = t0;
-    if (t < t1 && (t & 1)) chunk<1, M0, M1>(acc, Ap, Bp, ldb, t++, nch, smem);
+    if (t < t1 && (t & 1)) chunk<1, M0>(acc, Ap, Bp, ldb, t++, nch, smem);
 #pragma unroll 1
     for (; t + 1 < t1; t += 2) {
-      chunk<0, M0, M1>(acc, Ap, Bp, ldb, t, nch, smem);
-      chunk<1, M0, M1>(acc, Ap, Bp, ldb, t + 1, nch, smem);
+      chunk<0, M0>(acc, Ap, Bp, ldb, t, nch, smem);
+      chunk<1, M0>(acc, Ap, Bp, ldb, t + 1, nch, smem);
     }
-    if (t < t1) chunk<0, M0, M1>(acc, Ap, Bp, ldb, t, nch, smem);
+    if (t < t1) chunk<0, M0>(acc, Ap, Bp, ldb, t, nch, smem);
   }
 };
 
@@ -478,41 +383,168 @@ __device__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int
   // seed inside the K loop, where it also drains the asm-issued prefetch of the next chunk.
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
   // every run of this GEMM uses the one set of per-lane offsets formed above: no VALU address
-  // work in any of the loops, and no per-pattern copies of hoisted offsets competing for VGPRs
-#define GPF_RUN(m0, m1, a, b) dr.template run<m0, m1>(acc, Ar, Br, ldb, (a), (b), nch, smem)
+  // work in any of the loops
+#define GPF_RUN(m0, a, b) dr.template run<m0>(acc, Ar, Br, ldb, (a), (b), nch, smem)
+  const int slab = qd.cb / 16;  // wave-uniform
   if constexpr (TRI == TRI_NONE) {
-    GPF_RUN(0, 0, 0, nch);
-  } else if constexpr (TRI == TRI_B_KLEC) {  // column ni live iff 16 t <= cb + 16 ni
-    const int t1 = min(nch, qd.cb / 16 + 1), t2 = min(nch, t1 + 1);
-    GPF_RUN(0, 0, 0, t1);
-    GPF_RUN(4, 0, t1, t2);
-    GPF_RUN(4, 4, t2, nch);
-  } else if constexpr (TRI == TRI_B_KGEC) {  // column ni live iff 16 t >= cb + 16 ni
-    const int t1 = min(nch, qd.cb / 16), t2 = min(nch, t1 + 1);
-    GPF_RUN(4, 4, 0, t1);
-    GPF_RUN(0, 4, t1, t2);
-    GPF_RUN(0, 0, t2, nch);
-  } else if constexpr (TRI == TRI_A_KLER) {  // row block mi live iff 16 t <= rb + 16 mi
-    const int t1 = min(nch, qd.rb / 16 + 1);
-    const int t2 = min(nch, t1 + 1), t3 = min(nch, t1 + 2), t4 = min(nch, t1 + 3);
-    GPF_RUN(0, 0, 0, t1);
-    GPF_RUN(1, 1, t1, t2);
-    GPF_RUN(2, 2, t2, t3);
-    GPF_RUN(3, 3, t3, t4);
-    GPF_RUN(4, 4, t4, nch);
-  } else {  // TRI_C_LOWER: block live iff cb + 16 ni <= rb + 16 mi, for every chunk
+    GPF_RUN(0, 0, nch);
+  } else if constexpr (TRI == TRI_B_KGEC) {  // the slab's columns c >= 16 slab: chunks t < slab add zeros
+    const int t1 = min(nch, slab);
+    GPF_RUN(8, 0, t1);
+    GPF_RUN(0, t1, nch);
+  } else {  // TRI_C_LOWER: only the row blocks mi >= slab of the output are ever read
     static_assert(TRI == TRI_C_LOWER, "known-zero pattern");
-    // coarse patterns: the one dead block of the (0,1) and (2,3) sub-tiles is computed as well
-    // (upper-triangle output, never read; the live blocks see the same MFMA sequence), so the
-    // SYRK needs no pattern of its own (per-pattern and per-block variants measured slower,
-    // profiles/r1/gemm_loop_ab.txt)
-    const int dc = qd.cb - qd.rb;  // in {-64, -32, 0, 32, 64, 96}
-    if (dc <= 0) GPF_RUN(0, 0, 0, nch);
-    else if (dc <= 32) GPF_RUN(2, 2, 0, nch);
-    else GPF_RUN(4, 4, 0, nch);
+    switch (slab) {
+      case 0: GPF_RUN(0, 0, nch); break;
+      case 1: GPF_RUN(1, 0, nch); break;
+      case 2: GPF_RUN(2, 0, nch); break;
+      case 3: GPF_RUN(3, 0, nch); break;
+      case 4: GPF_RUN(4, 0, nch); break;
+      case 5: GPF_RUN(5, 0, nch); break;
+      case 6: GPF_RUN(6, 0, nch); break;
+      default: GPF_RUN(7, 0, nch); break;
+    }
   }
 #undef GPF_RUN
   __syncthreads();
+}
+
+// Symmetric rank-K update of a 128x128 tile: C -= A A^T for its lower triangle only, A (128 x K)
+// a [r][k] row panel streamed through the direct-to-LDS pipeline. The wave with column slab s
+// owns the row blocks mi >= s of its slab (the others lie above the diagonal and are never read):
+// it loads, updates and stores just those, so per pattern only its live accumulators are live.
+// WT: write-through stores (the result is handed to another workgroup of the launch).
+template <bool WT, int M0>
+__device__ __forceinline__ void syrk_rows(double* __restrict__ C, size_t ldc, const double* __restrict__ A, int lda,
+                                          int K, double* smem, const Quad<128>& qd) {
+  Acc<128> acc;
+  double* p0 = launder(C + (size_t)(qd.lane >> 4) * ldc + qd.cb + (qd.lane & 15));
+#pragma unroll
+  for (int mi = M0; mi < 8; ++mi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc.v[mi][0][r] = p0[(size_t)(mi * 16 + 4 * r) * ldc];
+  const int nch = K / DL_KC;
+  if (nch > 0) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const DenseRun<false, true> dr(qd, lda, lda, wave);
+    dr.template issue<0>(A, A, lda, 0, smem);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the seed loads retired outside the loop (gemm_stream_dl)
+    dr.template run<M0>(acc, A, A, lda, 0, nch, nch, smem);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int mi = M0; mi < 8; ++mi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double* q = p0 + (size_t)(mi * 16 + 4 * r) * ldc;
+      if (WT)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(q),
+                           (unsigned long long)__double_as_longlong(acc.v[mi][0][r]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      else
+        *q = acc.v[mi][0][r];
+    }
+}
+
+template <bool WT>
+__device__ __forceinline__ void syrk_tile(double* __restrict__ C, size_t ldc, const double* __restrict__ A, int lda,
+                                          int K, double* smem, const Quad<128>& qd) {
+  switch (qd.cb / 16) {  // wave-uniform
+    case 0: syrk_rows<WT, 0>(C, ldc, A, lda, K, smem, qd); break;
+    case 1: syrk_rows<WT, 1>(C, ldc, A, lda, K, smem, qd); break;
+    case 2: syrk_rows<WT, 2>(C, ldc, A, lda, K, smem, qd); break;
+    case 3: syrk_rows<WT, 3>(C, ldc, A, lda, K, smem, qd); break;
+    case 4: syrk_rows<WT, 4>(C, ldc, A, lda, K, smem, qd); break;
+    case 5: syrk_rows<WT, 5>(C, ldc, A, lda, K, smem, qd); break;
+    case 6: syrk_rows<WT, 6>(C, ldc, A, lda, K, smem, qd); break;
+    default: syrk_rows<WT, 7>(C, ldc, A, lda, K, smem, qd); break;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Triangular multiplies with the second operand in the accumulators (the L- and U-tile
+// finishes of k_step). A lower-triangular 128x128 U (the diagonal block U_JJ = L_JJ^-1) is
+// staged once in LDS as 8 column chunks of 16: chunk m holds rows [16 m, 128), row stride 17
+// doubles (the pad spreads an A-operand read — 16 rows x 4 consecutive k per half-wave — over
+// the banks: one 2-way pair). With the stride the read offsets of the 4 k-steps of a block are
+// immediates off one per-lane base. 36 blocks of 16 x 17 = 9792 doubles (76.5 KiB).
+// ----------------------------------------------------------------------------
+constexpr int TRI_LD = 17;
+constexpr int TRI_LDS = 36 * 16 * TRI_LD;  // doubles
+__host__ __device__ constexpr int tri_chunk(int m) { return 16 * TRI_LD * (8 * m - m * (m - 1) / 2); }  // chunk m's first double
+
+// U (row-major, leading dimension ld, lower triangle read) -> LDS: 576 chunk rows of 16 doubles,
+// 8 pairs each, 9 pairs per thread through registers (the odd stride rules out direct-to-LDS
+// transfers). Ends with a barrier.
+__device__ __forceinline__ void tri_to_lds(const double* __restrict__ U, size_t ld, double* s) {
+  const int tid = threadIdx.x;
+  d2 v[9];
+  int dst[9];
+#pragma unroll
+  for (int u = 0; u < 9; ++u) {
+    const int i = tid + DNTH * u, ri = i >> 3, kp = i & 7;  // chunk row ri (0..575), pair kp
+    int m = 0, base = 0;
+#pragma unroll
+    for (int mm = 0; mm < 7; ++mm)
+      if (ri >= base + 16 * (8 - m)) {
+        base += 16 * (8 - m);
+        ++m;
+      }
+    const int rr = ri - base;  // row 16 m + rr of U
+    v[u] = *reinterpret_cast<const d2*>(U + (size_t)(16 * m + rr) * ld + 16 * m + 2 * kp);
+    dst[u] = tri_chunk(m) + rr * TRI_LD + 2 * kp;
+  }
+#pragma unroll
+  for (int u = 0; u < 9; ++u) {
+    s[dst[u]] = v[u].x;
+    s[dst[u] + 1] = v[u].y;
+  }
+  __syncthreads();
+}
+
+// out[j] (+)= sum_{k <= i} U(i, k) X(k, n) for the row blocks ib = 2 P + j (i in [16 ib, 16 ib + 16))
+// and the wave's 16 columns n, NEG: -= (the MFMA's A-negate). X in the accumulator layout: the
+// register e of block mi of a lane (g = lane >> 4, c = lane & 15) holds X(16 mi + 4 e + g, cb + c),
+// which is exactly the B operand of k-step 16 mi + 4 e. Per output block the k-steps run in
+// ascending order (the two blocks' chains interleaved). Software-pipelined by one k-step: the A
+// operands of step q+1 are read before the MFMAs of step q; scheduling barriers keep the compiler
+// from hoisting more reads (their registers would spill X). Two output blocks per call keep the
+// finish within the 128-register budget of 4 waves per SIMD.
+template <int P, bool NEG>
+__device__ __forceinline__ void trmm_acc(d4 (&out)[2], const Acc<128>& X, const double* sU) {
+  constexpr int NQ = 4 * (2 * P + 2);  // k-steps (mi, e)
+  const int lane = threadIdx.x & 63;
+  // per-lane byte bases: row (lane & 15), k (lane >> 4); offsets past 32 KiB go through the
+  // second base (ds_read offsets are 16-bit), which is hidden from the optimiser so that it
+  // stays one register
+  const uint32_t b0 = 8u * (uint32_t)((lane & 15) * TRI_LD + (lane >> 4));
+  uint32_t b1 = b0 + 32768u;
+  asm volatile("" : "+v"(b1));
+  const char* u = (const char*)sU;
+  out[0] = d4{0.0, 0.0, 0.0, 0.0};
+  out[1] = d4{0.0, 0.0, 0.0, 0.0};
+  double a[2][2];
+  auto reads = [&](int q, double (&r)[2]) {
+    const int mi = q >> 2, e = q & 3;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (2 * P + j >= mi) {
+        const int off = 8 * (tri_chunk(mi) + (2 * P + j - mi) * 16 * TRI_LD + 4 * e);
+        r[j] = off < 32768 ? *(const double*)(u + b0 + off) : *(const double*)(u + b1 + (off - 32768));
+      }
+  };
+  reads(0, a[0]);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    if (q + 1 < NQ) reads(q + 1, a[(q + 1) & 1]);
+    __builtin_amdgcn_sched_barrier(0);
+    const int mi = q >> 2, e = q & 3;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (2 * P + j >= mi)
+        out[j] = NEG ? mfma_neg_a(a[q & 1][j], X.v[mi][0][e], out[j]) : mfma(a[q & 1][j], X.v[mi][0][e], out[j]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
 }
 
 // 64x64x64 GEMM with both operands resident in LDS (8 waves, 32x16 each):
@@ -612,36 +644,6 @@ __device__ __forceinline__ void zero_tile64(double* __restrict__ g, size_t gld) 
       *reinterpret_cast<d2*>(gp) = d2{0.0, 0.0};
     }
   }
-}
-
-// One butterfly step of acc_row_dot over the live list v[0 .. 2H): lanes with bit H of their
-// column index keep the upper half. Every index is a compile-time constant (pack expansion, no
-// loop): a loop over j left the selects to the optimiser, which turned them into a
-// lane-dependent index into v and lowered that as chains of 16 v_cndmask per element.
-template <int H, int... J>
-__device__ __forceinline__ void row_dot_step(double (&v)[16], bool up, std::integer_sequence<int, J...>) {
-  ((v[J] = (up ? v[J + H] : v[J]) + __shfl_xor(up ? v[J] : v[J + H], H)), ...);
-}
-
-// Row sums of the 128-tile accumulator times a column vector z (LDS, 128 entries) over this
-// wave's 32 columns: the two column blocks are combined in each lane, then the 16 lanes of a
-// lane group (same rows, different columns) by a butterfly reduce-scatter (15 shuffles instead
-// of 4 x 16). Returns, in lane (g = lane >> 4, c = lane & 15), the sum of row
-// rb + 16 (c >> 2) + g + 4 (c & 3) (accumulator index mi = c >> 2, r = c & 3). Fixed order.
-__device__ __forceinline__ double acc_row_dot(const Acc<128>& acc, const Quad<128>& qd, const double* z) {
-  static_assert(Acc<128>::MBR == 4 && Acc<128>::MBC == 2, "layout of the 128-tile accumulator");
-  const double z0 = z[qd.col(0)], z1 = z[qd.col(1)];
-  double v[16];
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[mi * 4 + r] = fma(acc.v[mi][1][r], z1, acc.v[mi][0][r] * z0);
-  const int c = qd.lane & 15;
-  row_dot_step<8>(v, (c & 8) != 0, std::make_integer_sequence<int, 8>{});
-  row_dot_step<4>(v, (c & 4) != 0, std::make_integer_sequence<int, 4>{});
-  row_dot_step<2>(v, (c & 2) != 0, std::make_integer_sequence<int, 2>{});
-  row_dot_step<1>(v, (c & 1) != 0, std::make_integer_sequence<int, 1>{});
-  return v[0];
 }
 
 // Sum over the 4 lane groups {l, l^16, l^32, l^48} of a wave; the result is

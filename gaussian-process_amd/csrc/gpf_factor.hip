@@ -10,7 +10,8 @@
 //
 // Blocking: 128-wide block columns J (T = 128). Launch J (k_step) advances every
 // particle of the chunk by one block column:
-//   L tiles (I > J):  L_IJ = (A_IJ - L_I,<J L_J,<J^T) U_JJ^T       streamed MFMA GEMM, depth 128 J
+//   L tiles (I > J):  L_IJ = (A_IJ - L_I,<J L_J,<J^T) U_JJ^T       streamed MFMA GEMM, depth 128 J,
+//                     computed transposed and finished from the registers (step_item)
 //                     A_II -= L_IJ L_IJ^T ; y_I -= L_IJ z_J         look-ahead (keeps A_II and y current)
 //   U tiles (K < J):  U_JK = -U_JJ (L_J,[K,J) U_[K,J),K)           streamed MFMA GEMM, depth 128 (J-K)
 // and the workgroup that finishes A_{J+1,J+1} factors it in the same launch (factor128:
@@ -567,7 +568,7 @@ __host__ __device__ __forceinline__ void step_tile(int b, int P, int ntl, int gr
 }
 
 enum { SPLIT_NONE = 0, SPLIT_ALL = 1, SPLIT_CRIT = 2 };
-enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2, ROLE_DIAG = 3, ROLE_QUAD = 4 };
+enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2, ROLE_DIAG = 3, ROLE_SYRK = 4 };
 
 // Early diagonal factor (k_step<SPLIT, ED = 1>; the host chooses it for launches that leave
 // workgroup slots idle): launch J starts with P extra workgroups that factor diagonal
@@ -578,20 +579,27 @@ enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2, ROLE_DIAG = 3, ROLE_QUAD =
 // tile (I = J+1) in series. Launch 0 factors block 0 the same way (k_build_cov resets the flags
 // to -1). With ED = 0 the critical tile factors block J+1 itself (fused) and k_diag block 0.
 
-// Workgroup b of a k_step<SPLIT> launch (grid: [P diagonal workgroups if ed] + P*(nt-1)*S for
-// SPLIT_ALL, P*(nt-1) + P*(S-1) for SPLIT_CRIT, P*(nt-1) otherwise, + [4 P quadrant workgroups if
-// qf]): its particle p, tile w, split index sidx, and whether it factors the diagonal block
-// (ROLE_DIAG, w = -1), runs the whole tile, one depth range (piece sidx of S) of it, nothing, or
-// quadrant sidx of the critical tile's finish (ROLE_QUAD, w = -1). The kernel and the host-side
-// plan check (gpf_plan_check) both decode through this function.
-template <int SPLIT>
-__host__ __device__ __forceinline__ int step_regular(int P, int nt, int S) {
-  return SPLIT == SPLIT_ALL ? P * (nt - 1) * S : SPLIT == SPLIT_CRIT ? P * (nt - 1) + P * (S - 1) : P * (nt - 1);
-}
+// Deferred diagonal update (defer = 1; the factorisations without the all-tile split): instead of
+// every L tile applying its rank-128 look-ahead A_II -= L_IJ L_IJ^T in every launch (a
+// read-modify-write of a 128 KiB tile per tile and launch, each a short triangular GEMM), launch J
+// starts with one SYRK workgroup per particle (1 <= J <= nt-2) that applies all the earlier terms
+// to the next diagonal block in one deep GEMM, S = A_{J+1,J+1} - L_{J+1,<J} L_{J+1,<J}^T (its
+// inputs are all from earlier launches), and publishes S (write-through, then a per-particle
+// flag); the critical tile I = J+1 adds the last term L_{J+1,J} L_{J+1,J}^T once its TRMM is done
+// (at J = 0 it is the whole update). The SYRK workgroup runs beside the critical tile's GEMM
+// (depth 128 J, ~9/16 of its MFMAs) and is done long before the tile needs S. The other L tiles
+// touch no diagonal block. Same MFMAs in the same order per element of A_II: bitwise the
+// per-launch look-ahead's values.
 
+// Workgroup b of a k_step<SPLIT> launch (grid: [P diagonal workgroups if ed] + [P SYRK workgroups
+// if sy] + P*(nt-1)*S for SPLIT_ALL, P*(nt-1) + P*(S-1) for SPLIT_CRIT, P*(nt-1) otherwise): its
+// particle p, tile w, split index sidx, and whether it factors the diagonal block (ROLE_DIAG,
+// w = -1), reduces the next diagonal block (ROLE_SYRK, w = -1), runs the whole tile, one depth
+// range (piece sidx of S) of it, or nothing. The kernel and the host-side plan check
+// (gpf_plan_check) both decode through this function.
 template <int SPLIT>
-__host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt, int grp, int S, int ed, int qf,
-                                                    int& p, int& w, int& sidx) {
+__host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt, int grp, int S, int ed, int sy, int& p,
+                                                    int& w, int& sidx) {
   const int tiles = P * (nt - 1);
   sidx = 0;
   if (ed) {
@@ -602,14 +610,13 @@ __host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt,
     }
     b -= P;
   }
-  if (qf) {
-    const int reg = step_regular<SPLIT>(P, nt, S);
-    if (b >= reg) {  // particle fastest: quadrant q of every particle, then q + 1
-      p = (b - reg) % P;
-      sidx = (b - reg) / P;
+  if (sy) {
+    if (b < P) {
+      p = b;
       w = -1;
-      return ROLE_QUAD;
+      return ROLE_SYRK;
     }
+    b -= P;
   }
   if (SPLIT == SPLIT_ALL) {
     sidx = b / tiles;  // split-major dispatch
@@ -631,11 +638,14 @@ __host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt,
   return (SPLIT == SPLIT_CRIT && sidx > 0) ? ROLE_IDLE : ROLE_WHOLE;  // U tiles never split in CRIT
 }
 
-constexpr int STEP_STAGE = (Geo<T>::STAGE > DL_STAGE) ? Geo<T>::STAGE : DL_STAGE;
-constexpr int STEP_SMEM = (STEP_STAGE > DIAG_BASE) ? STEP_STAGE : DIAG_BASE;  // ~72 KiB: two workgroups per CU
-constexpr int STEP_SMALL = (5 * T > DIAG_SMALL) ? 5 * T : DIAG_SMALL;  // z_J + reduction scratch, or the diagonal's
-static_assert(DIAG_BASE <= STEP_SMEM && DIAG_SMALL <= STEP_SMALL, "fused diagonal fits the step's LDS");
-constexpr int STEP_NTH = Geo<T>::NTH;     // 512 threads: 8 waves, 64x32 per wave
+// LDS of a k_step workgroup (doubles): the GEMM stages (DL_STAGE), the diagonal factor
+// (DIAG_BASE + DIAG_SMALL), the staged U_JJ of the triangular finishes (TRI_LDS) with z_J behind
+// it, or the coordinates of a covariance tile. ~77 KiB: two workgroups per CU.
+constexpr int STEP_ZJ = TRI_LDS;  // z_J (128 doubles) beside the staged U_JJ
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+constexpr int STEP_LDS = cmax(cmax(DL_STAGE, DIAG_BASE + DIAG_SMALL), cmax(STEP_ZJ + T, 2 * DMAX * T + 2 * T));
+static_assert(STEP_LDS * 8 <= 80 * 1024, "two k_step workgroups per CU (160 KiB of LDS)");
+constexpr int STEP_NTH = Geo<T>::NTH;     // 512 threads: 8 waves, 128x16 per wave
 static_assert(STEP_NTH == DNTH, "the fused diagonal runs on the step workgroup");
 
 #ifndef GPF_DIAG_PRIO
@@ -661,37 +671,25 @@ __device__ __forceinline__ unsigned long long realtime() {
 #define GPF_PHASE(k)
 #endif
 
-#ifndef GPF_DL
-#define GPF_DL 1  // direct-to-LDS staging in the block-column GEMMs (build-time A/B knob)
-#endif
-template <bool NN, bool NEG = false, int TRI = TRI_NONE>
-__device__ __forceinline__ void step_gemm(Acc<T>& acc, const double* Ap, int lda, const double* Bp, int ldb, int K,
-                                          double* smem, const Quad<T>& qd) {
-#if GPF_DL
-  gemm_stream_dl<NN, NEG, TRI>(acc, Ap, lda, Bp, ldb, K, smem, qd);
-#else
-  gemm_stream<T, NN, NEG, TRI>(acc, Ap, lda, Bp, ldb, K, smem, qd);
-#endif
-}
-
-// A_IJ (I > J: no diagonal entries, so no noise term) of one particle straight into the
-// accumulator layout, with k_build_cov's op order (bitwise the same values, kernel_func
-// GP_func.py:56-65): the scaled coordinates and squared norms of the tile's 128 rows and 128
-// columns are staged in LDS first. Replaces the write of the K tile in the K build and its read
-// back here; only the diagonal blocks are still built (k_build_cov, diag_only).
-static_assert(2 * DMAX * T + 2 * T <= STEP_SMEM, "coordinate staging fits the step's LDS");
+// K(R, C) block of one particle (R != C: no diagonal entries, so no noise term) straight into the
+// accumulator layout (rows from block R, columns from block C), with k_build_cov's op order
+// (bitwise the same values, kernel_func GP_func.py:56-65; the two blocks enter symmetrically —
+// commuting products and sums — so K(J, I) = K(I, J)^T bitwise): the scaled coordinates and
+// squared norms of the tile's 128 rows and 128 columns are staged in LDS first. Replaces the
+// write of the K tile in the K build and its read back; only the diagonal blocks are still built
+// (k_build_cov, diag_only).
 __device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, const double* __restrict__ x,
-                                             const double* __restrict__ lp, int d, int N, int I, int J,
+                                             const double* __restrict__ lp, int d, int N, int R, int C,
                                              double* smem) {
   const int tid = threadIdx.x;
-  double* sa = smem;              // [d][T] scaled coordinates of rows (block I)
-  double* sb = smem + d * T;      // [d][T] ... of columns (block J)
+  double* sa = smem;              // [d][T] scaled coordinates of rows (block R)
+  double* sb = smem + d * T;      // [d][T] ... of columns (block C)
   double* na = smem + 2 * d * T;  // [T] squared norms of rows
   double* nb = na + T;            // [T] ... of columns
   if (tid < 2 * T) {
     const int t = tid & (T - 1);
     const bool rows = tid < T;
-    const int g = (rows ? I : J) * T + t;
+    const int g = (rows ? R : C) * T + t;
     double* a = rows ? sa : sb;
     double nrm = 0.0;
     if (g < N) {
@@ -712,7 +710,7 @@ __device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, con
       for (int r = 0; r < 4; ++r) {
         const int row = qd.row(mi, r), col = qd.col(ni);
         double v = 0.0;
-        if (I * T + row < N && J * T + col < N) {
+        if (R * T + row < N && C * T + col < N) {
           double dot = sa[row] * sb[col];
           for (int k = 1; k < d; ++k) dot = fma(sa[k * T + row], sb[k * T + col], dot);
           double r2 = (na[row] + nb[col]) - 2.0 * dot;
@@ -793,150 +791,50 @@ __device__ bool split_part(Acc<T>& acc, const double* Ap, int lda, const double*
 // Consumer side of the early diagonal factor: wait until the launch's diagonal workgroup of this
 // particle has published block J (flag >= J), then an agent-scope acquire (its stores are
 // write-through, factor128<true>, so no L2 write-back fence was needed on its side). The spin is
-// bounded: on timeout (~1 s) info gets bit 2 and the host reports an error instead of the GPU
-// hanging.
-__device__ __forceinline__ void wait_diag(const int* flag, int J, int* info) {
+// bounded (`spins` polls of ~1 us; the host passes ~2M, i.e. ~2 s, or a debug bound): on timeout
+// info gets bit 2, the host reports an error, and the caller skips everything that would read the
+// unpublished block (returns true) so the launch still drains.
+__device__ __forceinline__ bool wait_diag(const int* flag, int J, int* info, int spins, int* sflag) {
   if (threadIdx.x == 0) {
-    int spins = 0;
+    int n = 0, late = 0;
     while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < J) {
-      __builtin_amdgcn_s_sleep(16);
-      if (++spins > (1 << 21)) {
+      if (n++ >= spins) {
         __hip_atomic_fetch_or(info, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        late = 1;
         break;
       }
+      __builtin_amdgcn_s_sleep(16);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-}
-
-// ----------------------------------------------------------------------------
-// Quadrant finish of the critical tile (launches with the early diagonal factor; GPF_QUAD).
-// The critical tile I = J+1 closes every launch's dependency chain: C = A_IJ - L_I,<J L_J,<J^T,
-// then L_IJ = C U_JJ^T, then A_II -= L_IJ L_IJ^T and y_I -= L_IJ z_J, and the next launch's
-// diagonal workgroup factors A_II. On one workgroup the triangular multiply and the rank-128
-// update take ~40 us per launch at small N (profiles/r2/v2_crit_B.txt), so here the workgroup
-// that completes C publishes it (write-through to the particle's quadrant buffer, then cflag = J)
-// and four quadrant workgroups (rh, kh) in {0,1}^2, dispatched at the end of the launch, finish:
-//   L_IJ[rh][kh] = sum_{m <= kh} C[rh][m] U_JJ[kh][m]^T           (64x64, depth 64 or 128)
-//   Y[rh][kh]    = L_IJ[rh][kh] z_J[kh]                          (row partials)
-// the second of the pair (0,kh), (1,kh) to arrive (ticket) forms column half kh's share of the
-// rank-128 update for the three lower quadrants of A_II,
-//   P_kh = L_IJ[:,kh] L_IJ[:,kh]^T                               (depth 64)
-// and the second of the two pair finishers applies A_II -= (P_0 + P_1), y_I -= (Y[.][0] + Y[.][1]).
-// IEEE addition commutes, so the result does not depend on the arrival order. Hand-offs as in
-// split_part (write-through stores, drain, relaxed ticket, agent acquire by the second arriver);
-// the quadrant workgroups wait only on workgroups dispatched before them (the C producer and the
-// diagonal workgroup), so in-order dispatch cannot deadlock them.
-// Per-particle buffer (QSTRIDE doubles): C [128][128] | P [2][3][64][64] | Y [2][2][64].
-// ----------------------------------------------------------------------------
-constexpr int QSTRIDE = T * T + 6 * H * H + 4 * H;
-constexpr int QCNT = 4;  // arrival counters per particle: pair kh = 0, 1; the top
-
-// Second-arriver election on a zeroed counter (reset by the second arriver for the next launch).
-__device__ __forceinline__ bool pair_ticket(unsigned* cn, int* sflag) {
-  if (threadIdx.x == 0) {
-    const unsigned old = __hip_atomic_fetch_add(cn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int second = old == 1u;
-    if (second) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(cn, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    *sflag = second;
+    *sflag = late;
   }
   __syncthreads();
   return *sflag != 0;
 }
 
-__device__ void quad_item(int q, int J, int p, int Npad, double* __restrict__ Lb, const double* __restrict__ Ub,
-                          double* __restrict__ yb, int* __restrict__ info, const int* __restrict__ dflag,
-                          const int* __restrict__ cflag, double* __restrict__ qbuf, unsigned* __restrict__ qcnt,
-                          int* sflag, double* smem, double* small) {
-  const int tid = threadIdx.x;
+// SYRK workgroup of launch J (deferred diagonal update, see step_decode): A_{J+1,J+1} -=
+// L_{J+1,<J} L_{J+1,<J}^T in one depth-128 J GEMM, published write-through with a per-particle flag.
+__device__ __forceinline__ void syrk_item(int J, int p, int Npad, double* __restrict__ Lb, int* __restrict__ yflag,
+                                          double* lds) {
   const size_t ld = (size_t)Npad;
-  const int I = J + 1, rh = q >> 1, kh = q & 1;
+  const int I = J + 1;
   double* Lp = Lb + (size_t)p * ld * ld;
-  const double* Ujj = Ub + (size_t)p * ld * ld + (size_t)J * T * ld + (size_t)J * T;
-  double* yp = yb + (size_t)p * Npad;
-  double* qb = qbuf + (size_t)p * QSTRIDE;
-  const double* Cb = qb;
-  double* Pb = qb + T * T;
-  double* Yb = Pb + 6 * H * H;
-  unsigned* qc = qcnt + (size_t)p * QCNT;
-  double* sA = smem;
-  double* sB = smem + H * LDH;
-  double* zs = smem + 2 * H * LDH;  // z_J[kh half]
-  const Quad<64> qd;
-  Acc<64> acc;
-  acc.zero();
-  wait_diag(cflag + p, J, info + p);  // C
-  tile64_to_lds(sA, LDH, Cb + (size_t)rh * H * T, T);
-  wait_diag(dflag + p, J, info + p);  // U_JJ, z_J
-  for (int m = 0; m <= kh; ++m) {
-    if (m > 0) tile64_to_lds(sA, LDH, Cb + (size_t)rh * H * T + m * H, T);
-    tile64_to_lds(sB, LDH, Ujj + (size_t)kh * H * ld + m * H, ld);
-    __syncthreads();
-    if (m == kh)
-      gemm_lds64<false, TRI_B_KLEC>(acc, sA, LDH, sB, LDH, qd);  // U_JJ[kh][kh]^T is upper triangular
-    else
-      gemm_lds64<false>(acc, sA, LDH, sB, LDH, qd);
-    __syncthreads();
-  }
-  // L_IJ[rh][kh]: to the particle's L (write-through: the pair sibling reads it) and to LDS
-  double* Lq = Lp + (size_t)I * T * ld + (size_t)J * T + (size_t)rh * H * ld + kh * H;
-  acc.foreach(qd, [&](int r, int c, double v) {
-    sA[r * LDH + c] = v;
-    gst<true>(&Lq[(size_t)r * ld + c], v);
-  });
-  if (tid < H) zs[tid] = yp[J * T + kh * H + tid];
-  __syncthreads();
-  rows_dot64(small, sA, LDH, zs, small + H, false);
-  if (tid < H) gst<true>(&Yb[(rh * 2 + kh) * H + tid], small[tid]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (!pair_ticket(qc + kh, sflag)) return;
-  // column half kh's share of the update: the sibling's rows from global
-  tile64_to_lds(sB, LDH, Lp + (size_t)I * T * ld + (size_t)J * T + (size_t)(1 - rh) * H * ld + kh * H, ld);
-  __syncthreads();
-  const double* Lt = rh == 0 ? sA : sB;  // rows 0..63 of L_IJ[:, kh]
-  const double* Lu = rh == 0 ? sB : sA;  // rows 64..127
-  Acc<64> p00, p10, p11;
-  p00.zero();
-  p10.zero();
-  p11.zero();
-  gemm_lds64<false, TRI_C_LOWER>(p00, Lt, LDH, Lt, LDH, qd);
-  gemm_lds64<false>(p10, Lu, LDH, Lt, LDH, qd);
-  gemm_lds64<false, TRI_C_LOWER>(p11, Lu, LDH, Lu, LDH, qd);
-  double* Pk = Pb + (size_t)kh * 3 * H * H;
-  p00.foreach(qd, [&](int r, int c, double v) { gst<true>(&Pk[r * H + c], v); });
-  p10.foreach(qd, [&](int r, int c, double v) { gst<true>(&Pk[H * H + r * H + c], v); });
-  p11.foreach(qd, [&](int r, int c, double v) { gst<true>(&Pk[2 * H * H + r * H + c], v); });
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (!pair_ticket(qc + 2, sflag)) return;
-  // A_II -= (P_0 + P_1) on the three lower quadrants (only the lower triangle is ever read)
-  const double* Po = Pb + (size_t)(1 - kh) * 3 * H * H;
   double* Aii = Lp + (size_t)I * T * ld + (size_t)I * T;
-  p00.foreach(qd, [&](int r, int c, double v) {
-    double* a = &Aii[(size_t)r * ld + c];
-    *a = *a - (v + Po[r * H + c]);
-  });
-  p10.foreach(qd, [&](int r, int c, double v) {
-    double* a = &Aii[(size_t)(H + r) * ld + c];
-    *a = *a - (v + Po[H * H + r * H + c]);
-  });
-  p11.foreach(qd, [&](int r, int c, double v) {
-    double* a = &Aii[(size_t)(H + r) * ld + H + c];
-    *a = *a - (v + Po[2 * H * H + r * H + c]);
-  });
-  if (tid < T) {
-    const int h = tid >> 6, r = tid & (H - 1);
-    yp[I * T + tid] = yp[I * T + tid] - (Yb[(h * 2) * H + r] + Yb[(h * 2 + 1) * H + r]);
-  }
+  const Quad<T> qd;
+  syrk_tile<true>(Aii, ld, Lp + (size_t)I * T * ld, Npad, J * T, lds, qd);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's part drained
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(yflag + p, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Tile w of block column J of particle p (the unit of work of k_step); role from step_decode.
+//   L tile (I = J+1+w):  D = A_IJ^T - L_J,<J L_I,<J^T  (the transposed panel C^T, so that each
+//                        wave holds all 128 k of the triangular multiply for its 16 rows of C)
+//                        L_IJ^T = U_JJ D               (trmm_acc, U_JJ staged in LDS)
+//                        A_II -= L_IJ L_IJ^T ; y_I -= L_IJ z_J
+//   U tile (K = w-nL):   W = L_J,[K,J) U_[K,J),K ; U_JK = -U_JJ W (trmm_acc); column partials
+// The products the finishes need never leave the registers: no C or W round trip through
+// memory, no streamed second operand, no barrier inside the triangular multiplies.
 template <int SPLIT, int ED>
 __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt, int Npad, double* __restrict__ Lb,
                                           double* __restrict__ Ub, double* __restrict__ yb,
@@ -944,9 +842,8 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
                                           int* __restrict__ info, int N, const double* __restrict__ x,
                                           const double* __restrict__ ls, int d, int S, int sidx,
                                           double* __restrict__ part, unsigned* __restrict__ cnt, int* sflag,
-                                          const int* __restrict__ dflag, int* __restrict__ cflag,
-                                          double* __restrict__ qbuf, int qf, int deep, double* smem,
-                                          double* small) {
+                                          const int* __restrict__ dflag, const int* __restrict__ yflag, int defer,
+                                          int spins, double* lds) {
   const int tid = threadIdx.x;
   const int nL = nt - 1 - J;
   const size_t ld = (size_t)Npad;
@@ -955,173 +852,135 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
   double* Up = Ub + (size_t)p * ld * ld;
   double* yp = yb + (size_t)p * Npad;
   const Quad<T> qd;
+  const int g = qd.lane >> 4, cl = qd.lane & 15;
   const double* Ujj = Up + (size_t)J * T * ld + (size_t)J * T;
-  double* zj = small;  // z_J (128), written by the previous launch's diagonal
-  double* scratch = small + T;
+  double* zj = lds + STEP_ZJ;  // z_J (128), written by the diagonal factor of block J
 
   if (w < nL) {
     const int I = J + 1 + w;
     double* Aij = Lp + (size_t)I * T * ld + (size_t)J * T;
     double* Aii = Lp + (size_t)I * T * ld + (size_t)I * T;
+    const double* lp = ls + (size_t)p * d;
     Acc<T> acc;
-    // C = A_IJ - L_I,<J L_J,<J^T (accumulator seeded with A_IJ, A operand staged negated)
-#if GPF_KFUSE
+    // D = C^T = A_JI - L_J,<J L_I,<J^T (accumulator seeded with the covariance tile, A operand
+    // negated through the MFMA modifier)
     if (SPLIT != SPLIT_NONE && role == ROLE_PIECE) {
-      // split-K: partial GEMMs, the last workgroup to arrive finishes the tile
+      // split-K: partial GEMMs, the last workgroup to arrive finishes the tile; piece 0 seeds
+      // its partial with the covariance tile (the unsplit path's accumulator seed)
       double* pt = part + (size_t)(p * (nt - 1) + w) * S * T * T;
-      // piece 0 seeds its partial with the covariance tile A_IJ (the unsplit path's accumulator seed)
-      if (!split_part<false, true, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad,
-                                         J * T / DL_KC, S, sidx, pt, cnt + (size_t)(p * (nt - 1) + w) * SPLIT_CNT, smem,
-                                         qd, sflag,
-                                         [&](Acc<T>& a) { cov_tile_acc(a, qd, x, ls + (size_t)p * d, d, N, I, J, smem); }))
-        return;  // (the finisher's accumulators hold A_IJ - L_I,<J L_J,<J^T)
+      if (!split_part<false, true, true>(acc, Lp + (size_t)J * T * ld, Npad, Lp + (size_t)I * T * ld, Npad,
+                                         J * T / DL_KC, S, sidx, pt, cnt + (size_t)(p * (nt - 1) + w) * SPLIT_CNT, lds,
+                                         qd, sflag, [&](Acc<T>& a) { cov_tile_acc(a, qd, x, lp, d, N, J, I, lds); }))
+        return;  // (the finisher's accumulators hold D)
     } else {
-      cov_tile_acc(acc, qd, x, ls + (size_t)p * d, d, N, I, J, smem);
+      cov_tile_acc(acc, qd, x, lp, d, N, J, I, lds);
       if (J > 0)
-        step_gemm<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, J * T, smem, qd);
+        gemm_stream_dl<false, true>(acc, Lp + (size_t)J * T * ld, Npad, Lp + (size_t)I * T * ld, Npad, J * T, lds, qd);
     }
-    if (ED && qf && w == 0) {  // critical tile: publish C to the quadrant workgroups (quad_item)
-      acc.store_wt(qd, qbuf + (size_t)p * QSTRIDE, T);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) __hip_atomic_store(cflag + p, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-    acc.store(qd, Aij, ld);  // C (the TRMM below streams it)
-#else
-    if (J > 0) {  // (at J = 0, C = A_IJ is already in place)
-      acc.load(qd, Aij, ld);
-      step_gemm<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, J * T, smem, qd);
-      acc.store(qd, Aij, ld);
-    }
-#endif
-    __syncthreads();
     GPF_PHASE(0);
-    if (ED) wait_diag(dflag + p, J, info + p);  // U_JJ, z_J (block 0 too: launch 0 has diagonal workgroups)
-    // L_IJ = C U_JJ^T
-    acc.zero();
-    step_gemm<false, false, TRI_B_KLEC>(acc, Aij, Npad, Ujj, Npad, T, smem, qd);
-    acc.store(qd, Aij, ld);
+    if (ED && wait_diag(dflag + p, J, info + p, spins, sflag)) return;  // U_JJ, z_J (launch 0 too)
     if (tid < T) zj[tid] = yp[J * T + tid];
-    __syncthreads();
-    GPF_PHASE(1);
-    // y_I -= L_IJ z_J, row sums straight from the accumulators: one partial per row and column
-    // slab of 32 (scratch[slab][row]), combined in slab order after the SYRK's barriers
-    {
-      const int c = qd.lane & 15;
-      scratch[(qd.cb / 32) * T + qd.rb + 16 * (c >> 2) + (qd.lane >> 4) + 4 * (c & 3)] = acc_row_dot(acc, qd, zj);
+    tri_to_lds(Ujj, ld, lds);  // (its barrier also publishes z_J)
+    // L_IJ^T = U_JJ D by row halves of L_IJ^T (= column halves of L_IJ): lane (g, c) of the wave
+    // with slab cb gets L(cb + c, 16 jb + 4 e + g), stores it and adds its share of row cb + c of
+    // L_IJ z_J (k ascending per lane, then the 4 lane groups)
+    double* lrow = launder(Aij + (size_t)(qd.cb + cl) * ld + g);
+    double yr = 0.0;
+#pragma unroll
+    for (int P = 0; P < 4; ++P) {
+      d4 o[2];
+      switch (P) {
+        case 0: trmm_acc<0, false>(o, acc, lds); break;
+        case 1: trmm_acc<1, false>(o, acc, lds); break;
+        case 2: trmm_acc<2, false>(o, acc, lds); break;
+        default: trmm_acc<3, false>(o, acc, lds); break;
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          lrow[16 * (2 * P + j) + 4 * e] = o[j][e];
+          yr = fma(o[j][e], zj[16 * (2 * P + j) + 4 * e + g], yr);
+        }
     }
-    if (!ED && deep == 2) {
-      // pre-update (see deep_syrk in gpfit_api.hip): tile w = 1 (I = J+2) applies
-      // A_II -= L_I,<=J L_I,<=J^T to the untouched K block, the critical tile (w = 0) the last
-      // rank-128 term L_IJ L_IJ^T; the other tiles leave A_II alone. (J = 0: the critical tile's
-      // A_II is untouched and its one term is the whole update.)
-      if (w == 1) {
-        acc.load(qd, Aii, ld);
-        step_gemm<false, true, TRI_C_LOWER>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)I * T * ld, Npad,
-                                            (J + 1) * T, smem, qd);
-        acc.store(qd, Aii, ld);
-      } else if (w == 0) {
-        acc.load(qd, Aii, ld);
-        step_gemm<false, true, TRI_C_LOWER>(acc, Aij, Npad, Aij, Npad, T, smem, qd);
-        acc.store(qd, Aii, ld);
-      } else {
-        __syncthreads();
-      }
-    } else if (!ED && deep) {
-      // deep update: A_II -= L_I,<=J L_I,<=J^T in one depth-128(J+1) GEMM by the critical tile
-      // only (A_II has not been touched since the K build); the other tiles skip the update. The
-      // additions run in the same order as the per-launch look-ahead's (k ascending, one MFMA k-step
-      // at a time, the exact fp64 store/load between launches dropped): bitwise the same A_II.
-      if (I == J + 1) {
-        acc.load(qd, Aii, ld);
-        step_gemm<false, true, TRI_C_LOWER>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)I * T * ld, Npad,
-                                            (J + 1) * T, smem, qd);
-        acc.store(qd, Aii, ld);
-      } else {
-        __syncthreads();
-      }
-    } else {
-      // look-ahead: A_II -= L_IJ L_IJ^T (the full tile; only its lower half is ever read)
-      acc.load(qd, Aii, ld);
-      step_gemm<false, true, TRI_C_LOWER>(acc, Aij, Npad, Aij, Npad, T, smem, qd);
-      acc.store(qd, Aii, ld);
+    yr = sum_lane_groups(yr);
+    if (g == 0) yp[I * T + qd.cb + cl] = yp[I * T + qd.cb + cl] - yr;  // y_I -= L_IJ z_J
+    GPF_PHASE(1);
+    __syncthreads();  // L_IJ stored (workgroup release) and the staged U_JJ read: LDS free
+    // look-ahead: A_II -= L_IJ L_IJ^T (the full tile; only its lower half is ever read). Deferred
+    // (SPLIT_ALL never defers): only the critical tile, on top of the launch's SYRK workgroup's S.
+    const bool defer_on = SPLIT != SPLIT_ALL && defer;
+    if (!defer_on || I == J + 1) {
+      if (defer_on && J > 0 && wait_diag(yflag + p, J, info + p, spins, sflag)) return;  // S published
+      syrk_tile<false>(Aii, ld, Aij, Npad, T, lds, qd);
     }
     GPF_PHASE(2);
-    if (tid < T)  // (the SYRK's barriers ordered the scratch writes)
-      yp[I * T + tid] =
-          yp[I * T + tid] - (((scratch[tid] + scratch[T + tid]) + scratch[2 * T + tid]) + scratch[3 * T + tid]);
     GPF_PHASE(3);
     if (!ED && I == J + 1) {  // fused diagonal factor of block J+1 (A_II, y_I fully reduced)
       __syncthreads();
-      const DiagSmem sm = carve_diag(smem, small);
       const size_t poff = ((size_t)p * nt + I) * Npad + (size_t)I * T;
 #if GPF_DIAG_PRIO
       __builtin_amdgcn_s_setprio(3);  // latency-critical: the next launch waits for this block
 #endif
-      factor128(Aii, Up + (size_t)I * T * ld + (size_t)I * T, ld, yp + I * T, s2p + poff, szp + poff, info + p, sm,
-                I * T + H >= N);
+      factor128(Aii, Up + (size_t)I * T * ld + (size_t)I * T, ld, yp + I * T, s2p + poff, szp + poff, info + p,
+                carve_diag(lds, lds + DIAG_BASE), I * T + H >= N);
     }
   } else {
     const int K = w - nL;
     double* Ujk = Up + (size_t)J * T * ld + (size_t)K * T;
     Acc<T> acc;
-    // W = L_J,[K,J) U_[K,J),K, parked in the U_JK slot
+    // W = L_J,[K,J) U_[K,J),K (U_KK is lower triangular: the wave's first chunks add zeros)
     if (SPLIT == SPLIT_ALL && role == ROLE_PIECE) {  // split-K (the triangular first block runs dense: its upper part holds zeros)
       double* pt = part + (size_t)(p * (nt - 1) + w) * S * T * T;
       if (!split_part<true, false, false>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
-                                   Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T / DL_KC, S, sidx, pt,
-                                   cnt + (size_t)(p * (nt - 1) + w) * SPLIT_CNT, smem, qd, sflag, [](Acc<T>&) {}))
+                                          Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T / DL_KC, S, sidx,
+                                          pt, cnt + (size_t)(p * (nt - 1) + w) * SPLIT_CNT, lds, qd, sflag,
+                                          [](Acc<T>&) {}))
         return;
     } else {
       acc.zero();
-      step_gemm<true, false, TRI_B_KGEC>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
-                                              Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T, smem, qd);
+      gemm_stream_dl<true, false, TRI_B_KGEC>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
+                                              Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T, lds, qd);
     }
-    acc.store(qd, Ujk, ld);
-    if (ED) wait_diag(dflag + p, J, info + p);  // U_JJ, z_J (U tiles exist for J > 0 only)
-    if (tid < T) zj[tid] = yp[J * T + tid];
-    __syncthreads();
     GPF_PHASE(0);
-    // U_JK = -U_JJ W (A operand staged negated)
-    acc.zero();
-    step_gemm<true, true, TRI_A_KLER>(acc, Ujj, Npad, Ujk, Npad, T, smem, qd);
-    acc.store(qd, Ujk, ld);
-    GPF_PHASE(1);
-    // column partials straight from the accumulators: sum over this wave's rows,
-    // then the 4 lane groups, then the two row-halves of the tile (fixed order)
-    constexpr int MBR = Geo<T>::MBR, MBC = Geo<T>::MBC;
-    double* half = scratch;  // [2 quantities][T cols] from the lower row-half waves
-    const int wr = qd.wrow();
+    if (ED && wait_diag(dflag + p, J, info + p, spins, sflag)) return;  // U_JJ, z_J (U tiles exist for J > 0 only)
+    if (tid < T) zj[tid] = yp[J * T + tid];
+    tri_to_lds(Ujj, ld, lds);
+    // U_JK = -U_JJ W by row halves; the column partials of colsum(U^2) and U^T z summed per half
+    // (rows ascending per lane, then the 4 lane groups), then upper half + lower half
+    double* ucol = launder(Ujk + (size_t)g * ld + qd.cb + cl);
+    double a2[2] = {0.0, 0.0}, az[2] = {0.0, 0.0};
 #pragma unroll
-    for (int ni = 0; ni < MBC; ++ni) {
-      double a2 = 0.0, az = 0.0;
+    for (int P = 0; P < 4; ++P) {
+      d4 o[2];
+      switch (P) {
+        case 0: trmm_acc<0, true>(o, acc, lds); break;
+        case 1: trmm_acc<1, true>(o, acc, lds); break;
+        case 2: trmm_acc<2, true>(o, acc, lds); break;
+        default: trmm_acc<3, true>(o, acc, lds); break;
+      }
+      const int h = P >> 1;
 #pragma unroll
-      for (int mi = 0; mi < MBR; ++mi)
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const double v = acc.v[mi][ni][r];
-          a2 = fma(v, v, a2);
-          az = fma(v, zj[qd.row(mi, r)], az);
+        for (int e = 0; e < 4; ++e) {
+          const int row = 16 * (2 * P + j) + 4 * e;  // + g
+          const double v = o[j][e];
+          ucol[(size_t)row * ld] = v;
+          a2[h] = fma(v, v, a2[h]);
+          az[h] = fma(v, zj[row + g], az[h]);
         }
-      a2 = sum_lane_groups(a2);
-      az = sum_lane_groups(az);
-      if (wr == 1 && (qd.lane >> 4) == 0) {
-        half[qd.col(ni)] = a2;
-        half[T + qd.col(ni)] = az;
-      }
-      acc.v[0][ni][0] = a2;  // park the upper-half sums (accumulators are dead now)
-      acc.v[0][ni][1] = az;
     }
-    __syncthreads();
-    if (wr == 0 && (qd.lane >> 4) == 0) {
-      const size_t poff = ((size_t)p * nt + J) * Npad + (size_t)K * T;
 #pragma unroll
-      for (int ni = 0; ni < MBC; ++ni) {
-        const int c = qd.col(ni);
-        s2p[poff + c] = acc.v[0][ni][0] + half[c];
-        szp[poff + c] = acc.v[0][ni][1] + half[T + c];
-      }
+    for (int h = 0; h < 2; ++h) {
+      a2[h] = sum_lane_groups(a2[h]);
+      az[h] = sum_lane_groups(az[h]);
+    }
+    GPF_PHASE(1);
+    if (g == 0) {
+      const size_t poff = ((size_t)p * nt + J) * Npad + (size_t)K * T + qd.cb + cl;
+      s2p[poff] = a2[0] + a2[1];
+      szp[poff] = az[0] + az[1];
     }
   }
 }
@@ -1138,8 +997,7 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
                                                   const double* __restrict__ x, const double* __restrict__ ls,
                                                   int d, int S, double* __restrict__ part,
                                                   unsigned* __restrict__ cnt, int* __restrict__ dflag, int ed,
-                                                  int* __restrict__ cflag, double* __restrict__ qbuf,
-                                                  unsigned* __restrict__ qcnt, int qf, int deep) {
+                                                  int* __restrict__ yflag, int defer, int sy, int spins) {
   const int tid = threadIdx.x;
 #ifdef GPF_WG_TRACE
   if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) {
@@ -1150,13 +1008,12 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
     g_wg_trace[J][blockIdx.x][2] = ((unsigned long long)xcc << 32) | hw;
   }
 #endif
-  __shared__ __attribute__((aligned(16))) double smem[STEP_SMEM];
-  __shared__ __attribute__((aligned(16))) double small[STEP_SMALL];
+  __shared__ __attribute__((aligned(16))) double lds[STEP_LDS];
   __shared__ int sflag;
   int p, w, sidx;
-  const int role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, ED && qf, p, w, sidx);
-  if (ED && role == ROLE_QUAD) {
-    quad_item(sidx, J, p, Npad, Lb, Ub, yb, info, dflag, cflag, qbuf, qcnt, &sflag, smem, small);
+  const int role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, SPLIT != SPLIT_ALL && sy, p, w, sidx);
+  if (SPLIT != SPLIT_ALL && role == ROLE_SYRK) {
+    syrk_item(J, p, Npad, Lb, yflag, lds);
   } else if (ED && role == ROLE_DIAG) {
     // diagonal block J of particle p (fully reduced by the previous launches' look-ahead): factor,
     // then publish to this launch's tiles (write-through stores drained, then the flag)
@@ -1167,13 +1024,13 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
     __builtin_amdgcn_s_setprio(3);  // the launch's tiles wait for this block
 #endif
     factor128<true>(Lb + off, Ub + off, ld, yb + (size_t)p * Npad + J * T, s2p + poff, szp + poff, info + p,
-                    carve_diag(smem, small), J * T + H >= N);
+                    carve_diag(lds, lds + DIAG_BASE), J * T + H >= N);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) __hip_atomic_store(dflag + p, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
     step_item<SPLIT, ED>(role, J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, sidx, part, cnt, &sflag,
-                         dflag, cflag, qbuf, ED && qf, deep, smem, small);
+                         dflag, yflag, defer, spins, lds);
   }
 #ifdef GPF_WG_TRACE
   __syncthreads();
@@ -1205,16 +1062,17 @@ __global__ __launch_bounds__(DNTH) void k_debug_factor64(const double* __restric
 
 // ----------------------------------------------------------------------------
 // Measurement hook (gpf_gemm_bench): the L-tile GEMM of k_step in isolation.
-// Workgroup b: particle p = b % P, tile w = b / P; C_w -= L_p[rows I, :D] L_p[rows J, :D]^T
+// Workgroup b: particle p = b % P, tile w = b / P; D_w -= L_p[rows J, :D] L_p[rows I, :D]^T
 // with I = J+1+w, J = D/T (mode 0), or every workgroup on the same operands (mode 1:
-// L2-resident, isolates the core from HBM). The tile goes to C + b*T*T.
+// L2-resident, isolates the core from HBM); +4: the U-tile shape (B given as a [k][c] row panel).
+// The tile goes to C + b*T*T.
 // ----------------------------------------------------------------------------
 __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_gemm_bench(int mode, int D, int Npad, int P,
                                                                                    const double* __restrict__ Lb,
                                                                                    double* __restrict__ C) {
-  __shared__ __attribute__((aligned(16))) double smem[STEP_SMEM];
+  __shared__ __attribute__((aligned(16))) double smem[DL_STAGE];
   const int b = blockIdx.x;
-  const bool shared = (mode & 1) != 0, direct = (mode & 2) != 0;  // 1/3: shared operands; 2/3: direct-to-LDS; +4: NN
+  const bool shared = (mode & 1) != 0;
   const int p = shared ? 0 : b % P, w = shared ? 0 : b / P;
   const size_t ld = (size_t)Npad;
   const int J = D / T, I = J + 1 + w;
@@ -1222,12 +1080,10 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_gemm_benc
   const Quad<T> qd;
   Acc<T> acc;
   acc.zero();
-  if (direct && (mode & 4))  // U-tile shape: B given as a [k][c] row panel (NN)
+  if (mode & 4)
     gemm_stream_dl<true, false>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)w * T, Npad, D, smem, qd);
-  else if (direct)
-    gemm_stream_dl<false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, D, smem, qd);
   else
-    gemm_stream<T, false, true>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)J * T * ld, Npad, D, smem, qd);
+    gemm_stream_dl<false, true>(acc, Lp + (size_t)J * T * ld, Npad, Lp + (size_t)I * T * ld, Npad, D, smem, qd);
   acc.store(qd, C + (size_t)b * T * T, T);
 }
 

@@ -9,40 +9,31 @@
 namespace gpf {
 
 // vsq[t][q*128 + c] = sum over the 128 rows of tile t of (U_t,<=t K_s[:, q-tile])^2.
+// Each wave holds all 128 rows of its 16 columns: the sum runs per lane over the rows of each
+// row half, then over the 4 lane groups, then upper half + lower half (fixed order).
 // grid: (nqt, nt)
 __global__ __launch_bounds__(Geo<T>::NTH, 4) void k_predict_vsq(int Npad, const double* __restrict__ U,
                                                          const double* __restrict__ Ks, int ldks,
                                                          double* __restrict__ vsq) {
   __shared__ __attribute__((aligned(16))) double smem[DL_STAGE];
-  __shared__ double half[T];
   const int q = blockIdx.x, t = blockIdx.y;
   const Quad<T> qd;
   Acc<T> acc;
   acc.zero();
   // U is lower triangular: row tile t needs columns [0, (t+1) * 128)
   gemm_stream_dl<true>(acc, U + (size_t)t * T * Npad, Npad, Ks + (size_t)q * T, ldks, (t + 1) * T, smem, qd);
-  constexpr int MBR = Geo<T>::MBR, MBC = Geo<T>::MBC;
-  const int wr = qd.wrow();
-  double part[MBC];
+  constexpr int MBR = Geo<T>::MBR;
+  double half[2];
 #pragma unroll
-  for (int ni = 0; ni < MBC; ++ni) {
+  for (int h = 0; h < 2; ++h) {
     double a2 = 0.0;
 #pragma unroll
-    for (int mi = 0; mi < MBR; ++mi)
+    for (int mi = h * MBR / 2; mi < (h + 1) * MBR / 2; ++mi)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) a2 = fma(acc.v[mi][ni][r], acc.v[mi][ni][r], a2);
-    a2 = sum_lane_groups(a2);
-    part[ni] = a2;
-    if (wr == 1 && (qd.lane >> 4) == 0) half[qd.col(ni)] = a2;
+      for (int r = 0; r < 4; ++r) a2 = fma(acc.v[mi][0][r], acc.v[mi][0][r], a2);
+    half[h] = sum_lane_groups(a2);
   }
-  __syncthreads();
-  if (wr == 0 && (qd.lane >> 4) == 0) {
-#pragma unroll
-    for (int ni = 0; ni < MBC; ++ni) {
-      const int c = qd.col(ni);
-      vsq[(size_t)t * ldks + (size_t)q * T + c] = part[ni] + half[c];
-    }
-  }
+  if ((qd.lane >> 4) == 0) vsq[(size_t)t * ldks + (size_t)q * T + qd.col(0)] = half[0] + half[1];
 }
 
 // mu_q = K_s[:, q]^T alpha (GP_func.py:36); var = clip(1 - sum v^2, 1e-12) (:39-40)

@@ -87,13 +87,11 @@ struct gpf_ctx {
   double* d_loss = nullptr;
   int* d_info = nullptr;
   int* d_flag = nullptr;  // per particle: last diagonal block published in the running launch (early_diag)
-  int* d_cflag = nullptr;  // per particle: last critical-tile C published to the quadrant workgroups (quad_finish)
+  int* d_cflag = nullptr;  // per particle: last diagonal block reduced by a SYRK workgroup (defer_syrk); reset by k_build_cov
   // gpf_predict's query-chunk buffers, kept between calls (grow-only; freed with the work buffers)
   double *p_xf = nullptr, *p_ks = nullptr, *p_vsq = nullptr, *p_mu = nullptr, *p_sd = nullptr;
   int64_t p_cols = 0, p_np = 0;
   int p_d = 0, p_nt = 0;
-  double* d_qbuf = nullptr;    // per particle: the quadrant finish's C, partial updates and row partials
-  unsigned* d_qcnt = nullptr;  // per particle: its arrival counters, kept zero
   int* d_hist = nullptr;
   // pinned host staging for the per-batch transfers (async DMA, capturable in graphs)
   double* h_ls = nullptr;
@@ -204,10 +202,6 @@ static void free_work(gpf_ctx* c) {
   c->d_flag = nullptr;
   hipFree(c->d_cflag);
   c->d_cflag = nullptr;
-  hipFree(c->d_qbuf);
-  c->d_qbuf = nullptr;
-  hipFree(c->d_qcnt);
-  c->d_qcnt = nullptr;
   hipFree(c->d_part); hipFree(c->d_cnt);
   c->d_part = nullptr;
   c->d_cnt = nullptr;
@@ -220,8 +214,7 @@ static void free_work(gpf_ctx* c) {
 
 static size_t bytes_per_particle(const gpf_ctx* c) {
   const size_t np = (size_t)c->Npad;
-  return 2 * np * np * 8 + (2 * (size_t)c->nt * np + 3 * np) * 8 + (size_t)(c->K + 1) * 4 + 64 * 8 +
-         (size_t)gpf::QSTRIDE * 8 + gpf::QCNT * 4 + 4;
+  return 2 * np * np * 8 + (2 * (size_t)c->nt * np + 3 * np) * 8 + (size_t)(c->K + 1) * 4 + 64 * 8 + 8;
 }
 
 // Chunk capacity from free HBM (GPF_MAX_CHUNK caps it, GPF_MEM_FRACTION scales the budget).
@@ -253,9 +246,6 @@ static int ensure_work(gpf_ctx* c, int want) {
   GPF_HIP(c, hipMalloc(&c->d_info, (size_t)cap * 4));
   GPF_HIP(c, hipMalloc(&c->d_flag, (size_t)cap * 4));  // reset by k_build_cov at every factorisation
   GPF_HIP(c, hipMalloc(&c->d_cflag, (size_t)cap * 4));  // likewise
-  GPF_HIP(c, hipMalloc(&c->d_qbuf, (size_t)cap * gpf::QSTRIDE * 8));
-  GPF_HIP(c, hipMalloc(&c->d_qcnt, (size_t)cap * gpf::QCNT * 4));
-  GPF_HIP(c, hipMemsetAsync(c->d_qcnt, 0, (size_t)cap * gpf::QCNT * 4, c->stream));  // second arrivers re-zero
   GPF_HIP(c, hipMalloc(&c->d_hist, (size_t)cap * (c->K + 1) * 4));
   // on the library stream: the legacy null stream does not order against our non-blocking streams
   GPF_HIP(c, hipMemsetAsync(c->d_hist, 0, (size_t)cap * (c->K + 1) * 4, c->stream));  // k_score re-zeroes what it read
@@ -320,37 +310,20 @@ static bool early_diag(int pc, int nt) {
   return on && nt > 1;
 }
 
-// Quadrant finish of the critical tile (gpf::quad_item) in the launches with the early diagonal
-// factor: its triangular multiply and rank-128 update run on four extra workgroups per particle
-// instead of the one that completes the tile's GEMM. Off by default (GPF_QUAD = 1 turns it on):
-// the extra hand-offs (C published write-through, two ticket levels, the partial updates read
-// back) cost more than the shorter chain saves — config B -8%, prediction factor -2%
-// (profiles/r2/quad_finish_ab_rejected.txt).
-static bool quad_finish(int pc, int nt) {
-  bool on = false;
-  if (const char* s = getenv("GPF_QUAD")) on = atoi(s) != 0;
-  return on && GPF_KFUSE && early_diag(pc, nt);
+// Deferred diagonal update (gpf::syrk_item; see gpf::step_decode) for every factorisation without
+// the all-tile split. GPF_DEFER_SYRK = 0 restores the per-tile look-ahead (A/B knob).
+static bool defer_syrk() {
+  bool on = true;
+  if (const char* s = getenv("GPF_DEFER_SYRK")) on = atoi(s) != 0;
+  return on;
 }
 
-// Deep diagonal update in the launches with the fused diagonal factor (slot-bound: configs C, D,
-// E): instead of every L tile applying its rank-128 look-ahead A_II -= L_IJ L_IJ^T (a depth-128
-// GEMM plus a read-modify-write of the 128 KiB A_II per tile and launch), the critical tile of
-// launch J applies A_II -= L_I,<=J L_I,<=J^T as one depth-128(J+1) GEMM right before it factors
-// the block (gpf::step_item). Same additions in the same order: bitwise equal. Off by default
-// (GPF_DEEP_SYRK = 1 turns it on): it lengthens the critical tile's chain, which then outlasts
-// launches that are not deeply slot-bound or whose critical tiles start late behind the other
-// group's launch — same box: C +0.9%, D's 32-particle share -13%, E's share -2%
-// (profiles/r2/deep_syrk_ab_rejected.txt). Launches with the early diagonal factor always keep
-// the look-ahead.
-// GPF_DEEP_SYRK = 2 (pre-update): tile w = 1 of launch J (I = J+2, not on the launch's critical
-// chain: it factors nothing) applies A_II -= L_I,<=J L_I,<=J^T in one deep GEMM, the critical tile
-// of launch J+1 then adds only the last rank-128 term before it factors the block, and the other L
-// tiles skip the update (no A_II read-modify-write per tile and launch). Same additions in the
-// same order: bitwise equal. Off too: same box, C neutral, D's share -3.7%, E's share -0.9% (tile
-// w = 1 becomes the launch's longest chain; profiles/r2/pre_update_syrk_ab_rejected.txt).
-static int deep_syrk() {
-  if (const char* s = getenv("GPF_DEEP_SYRK")) return std::max(0, std::min(2, atoi(s)));
-  return 0;
+// Bound of the early-diagonal hand-off spin (gpf::wait_diag, polls of ~1 us): ~2 s by default;
+// GPF_WAIT_SPINS lowers it to exercise the timeout report (tests/test_gpu.py).
+static int wait_spins() {
+  int n = 1 << 21;
+  if (const char* s = getenv("GPF_WAIT_SPINS")) n = std::max(0, atoi(s));
+  return n;
 }
 
 // Critical-tile split of block-column launch J (gpf::SPLIT_CRIT), for launches that leave
@@ -369,8 +342,8 @@ static int deep_syrk() {
 static int split_crit(int pc, int nt, int J, int grp, int S_all) {
   // the last launch (J = nt-1) has no L tiles: its w = 0 is a U tile, which never splits
   if (S_all > 1 || grp > 0 || J == 0 || J >= nt - 1 || nt < 4 || !GPF_KFUSE) return 1;
-  // + the diagonal and the quadrant workgroups
-  const int slots = 512, tiles = pc * (nt - 1) + (early_diag(pc, nt) ? pc : 0) + (quad_finish(pc, nt) ? 4 * pc : 0);
+  // + the diagonal and the SYRK workgroups
+  const int slots = 512, tiles = pc * (nt - 1) + (early_diag(pc, nt) ? pc : 0) + (defer_syrk() && J <= nt - 2 ? pc : 0);
   int S = 1, minch = 16;
   if (const char* s = getenv("GPF_SPLIT_CRIT")) S = std::max(1, std::min(32, atoi(s)));
   if (const char* s = getenv("GPF_SPLIT_CRIT_MIN")) minch = std::max(2, atoi(s));
@@ -428,7 +401,7 @@ static int split_plan(gpf_ctx* c, int pc, int& S, int& Smax) {
 // d_part / d_cnt). run_factor launches exactly this list; gpf_plan_check verifies it on the host.
 struct StepLaunch {
   int J, g, p0, gc, split, S, grp, ed;  // ed: the launch starts with gc diagonal workgroups
-  int qf;                               // qf: ... and ends with 4 gc quadrant workgroups
+  int defer, sy;                        // deferred diagonal update; sy: gc SYRK workgroups follow
   unsigned grid;
   size_t part_off, cnt_off;
 };
@@ -436,7 +409,7 @@ struct StepLaunch {
 static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& out) {
   out.clear();
   const int ng = num_groups(pc, nt);
-  const bool ed = early_diag(pc, nt), qf = quad_finish(pc, nt);
+  const bool ed = early_diag(pc, nt);
   // block columns interleaved across groups so every stream has work queued early
   for (int J = 0; nt > 1 && J < nt; ++J) {
     for (int g = 0; g < ng; ++g) {
@@ -450,8 +423,9 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
       l.S = S > 1 ? S : Sc;  // pieces per split tile in this launch
       l.split = S > 1 ? gpf::SPLIT_ALL : Sc > 1 ? gpf::SPLIT_CRIT : gpf::SPLIT_NONE;
       l.ed = ed ? 1 : 0;
-      l.qf = (qf && J < nt - 1) ? 1 : 0;  // the last launch has no L tiles
-      l.grid = (S > 1 ? l.gc * (nt - 1) * S : l.gc * (nt - 1) + l.gc * (Sc - 1)) + (l.ed ? l.gc : 0) + (l.qf ? 4 * l.gc : 0);
+      l.defer = (S == 1 && defer_syrk()) ? 1 : 0;  // the all-tile split keeps the per-tile look-ahead
+      l.sy = (l.defer && J >= 1 && J <= nt - 2) ? 1 : 0;
+      l.grid = (S > 1 ? l.gc * (nt - 1) * S : l.gc * (nt - 1) + l.gc * (Sc - 1)) + (l.ed ? l.gc : 0) + (l.sy ? l.gc : 0);
       // one set of partial slots per group: groups run concurrently
       l.part_off = (size_t)l.p0 * (nt - 1) * Smax * T * T;
       l.cnt_off = (size_t)l.p0 * (nt - 1) * gpf::SPLIT_CNT;
@@ -478,7 +452,7 @@ static int run_factor(gpf_ctx* c, int pc) {
   //   U tile: depth-128(J-K) GEMM with a triangular factor 2 T^3 (J-K) - T^3 + triangular multiply T^3
   //   diagonal block: 2/3 T^3 (block J+1 fused at the end of launch J, or block J early in it)
   const bool ed = early_diag(pc, nt);
-  const int deep = deep_syrk();
+  const int spins = wait_spins();
   auto step_flops = [&](int J) {
     double fl = 0.0;
     for (int w = 0; w < nt - 1; ++w) {
@@ -548,8 +522,7 @@ static int run_factor(gpf_ctx* c, int pc) {
                          c->d_U + (size_t)p0 * ld * ld, c->d_yb + (size_t)p0 * ld, c->d_s2p + (size_t)p0 * nt * ld,
                          c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc, l.grp, N, c->d_x,
                          c->d_ls + (size_t)p0 * c->d, c->d, l.S, partg, cntg, c->d_flag + p0, l.ed,
-                         c->d_cflag + p0, c->d_qbuf + (size_t)p0 * gpf::QSTRIDE, c->d_qcnt + (size_t)p0 * gpf::QCNT,
-                         l.qf, ed ? 0 : deep);
+                         c->d_cflag + p0, l.defer, l.sy, spins);
     });
     if (rc) return rc;
     total += fl * gc;
@@ -1045,8 +1018,8 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
   // be disjoint (within a group the launches are ordered on its stream)
   std::vector<size_t> plo(MAX_GROUPS, SIZE_MAX), phi(MAX_GROUPS, 0), clo(MAX_GROUPS, SIZE_MAX), chi(MAX_GROUPS, 0);
   long long wgs = 0, whole_tiles = 0, split_tiles = 0;
-  std::vector<int> whole, piece, diag, quad;
-  long long diag_wgs = 0, quad_wgs = 0;
+  std::vector<int> whole, piece, diag, syrk;
+  long long diag_wgs = 0, syrk_wgs = 0;
   if ((int)plan.size() != (nt > 1 ? nt * ng : 0)) return plan_fail(msg, msg_len, "plan has %d launches, want %d",
                                                               (int)plan.size(), nt * ng);
   for (const StepLaunch& l : plan) {
@@ -1058,29 +1031,29 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     whole.assign((size_t)tiles, 0);
     piece.assign((size_t)tiles * l.S, 0);
     diag.assign((size_t)l.gc, 0);
-    quad.assign((size_t)l.gc * 4, 0);
-    const unsigned qbase = l.grid - (l.qf ? 4u * l.gc : 0u);
-    if (l.qf && (!l.ed || l.J >= nt - 1)) return plan_fail(msg, msg_len, "J=%d: quadrant finish without its inputs", l.J);
+    syrk.assign((size_t)l.gc, 0);
+    if (l.sy && (!l.defer || l.J < 1 || l.J > nt - 2 || l.split == gpf::SPLIT_ALL))
+      return plan_fail(msg, msg_len, "J=%d: SYRK workgroups without a diagonal block to reduce", l.J);
+    if (l.defer && l.split == gpf::SPLIT_ALL)
+      return plan_fail(msg, msg_len, "J=%d: deferred diagonal update under the all-tile split", l.J);
     for (unsigned b = 0; b < l.grid; ++b) {
       int p = -1, w = -1, sidx = -1;
       const int role =
-          l.split == gpf::SPLIT_ALL    ? gpf::step_decode<gpf::SPLIT_ALL>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.qf, p, w, sidx)
-          : l.split == gpf::SPLIT_CRIT ? gpf::step_decode<gpf::SPLIT_CRIT>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.qf, p, w, sidx)
-                                       : gpf::step_decode<gpf::SPLIT_NONE>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.qf, p, w, sidx);
+          l.split == gpf::SPLIT_ALL    ? gpf::step_decode<gpf::SPLIT_ALL>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, 0, p, w, sidx)
+          : l.split == gpf::SPLIT_CRIT ? gpf::step_decode<gpf::SPLIT_CRIT>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.sy, p, w, sidx)
+                                       : gpf::step_decode<gpf::SPLIT_NONE>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.sy, p, w, sidx);
       if (role == gpf::ROLE_DIAG) {  // one diagonal workgroup per particle, ahead of every tile of the launch
         if (!l.ed || p < 0 || p >= l.gc || (unsigned)p != b || diag[p]++)
           return plan_fail(msg, msg_len, "J=%d block %u: misplaced or duplicate diagonal workgroup (p=%d)", l.J, b, p);
         ++wgs;
         continue;
       }
-      if (role == gpf::ROLE_QUAD) {  // four per particle, after every other workgroup of the launch
-        if (!l.qf || p < 0 || p >= l.gc || sidx < 0 || sidx > 3 || b < qbase || quad[(size_t)p * 4 + sidx]++)
-          return plan_fail(msg, msg_len, "J=%d block %u: misplaced or duplicate quadrant workgroup (p=%d q=%d)", l.J, b,
-                           p, sidx);
+      if (role == gpf::ROLE_SYRK) {  // one per particle, right behind the diagonal workgroups
+        if (!l.sy || p < 0 || p >= l.gc || (unsigned)p + (l.ed ? l.gc : 0) != b || syrk[p]++)
+          return plan_fail(msg, msg_len, "J=%d block %u: misplaced or duplicate SYRK workgroup (p=%d)", l.J, b, p);
         ++wgs;
         continue;
       }
-      if (b >= qbase) return plan_fail(msg, msg_len, "J=%d block %u: a tile behind the quadrant workgroups", l.J, b);
       if (p < 0 || p >= l.gc || w < 0 || w >= ntl || sidx < 0 || sidx >= l.S)
         return plan_fail(msg, msg_len, "J=%d block %u decodes out of range (p=%d w=%d)", l.J, b, p, w);
       const int t = p * ntl + w;
@@ -1108,10 +1081,8 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     for (int q = 0; q < l.gc; ++q) {
       if (diag[q] != l.ed) return plan_fail(msg, msg_len, "J=%d particle %d: %d diagonal workgroups", l.J, q, diag[q]);
       diag_wgs += diag[q];
-      for (int k = 0; k < 4; ++k)
-        if (quad[(size_t)q * 4 + k] != l.qf)
-          return plan_fail(msg, msg_len, "J=%d particle %d: quadrant %d run %d times", l.J, q, k, quad[(size_t)q * 4 + k]);
-      quad_wgs += 4 * l.qf;
+      if (syrk[q] != l.sy) return plan_fail(msg, msg_len, "J=%d particle %d: %d SYRK workgroups", l.J, q, syrk[q]);
+      syrk_wgs += syrk[q];
     }
     for (int t = 0; t < tiles; ++t) {
       int np = 0;
@@ -1140,7 +1111,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     stats[5] = Smax;
     stats[6] = ng;
     stats[7] = diag_wgs;
-    stats[8] = quad_wgs;
+    stats[8] = syrk_wgs;
   }
   return GPF_OK;
 }

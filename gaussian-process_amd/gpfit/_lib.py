@@ -106,7 +106,7 @@ def plan_check(particles, nt):
     if rc != GPF_OK:
         raise AssertionError(f"plan_check(pc={particles}, nt={nt}): {msg.value.decode()}")
     keys = ("launches", "workgroups", "whole_tiles", "split_tiles", "S", "Smax", "groups", "diag_workgroups",
-            "quad_workgroups")
+            "syrk_workgroups")
     return dict(zip(keys, list(stats)))
 
 

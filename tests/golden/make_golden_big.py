@@ -6,6 +6,10 @@ Run in the build container only (needs /root/reference, read-only), one fixture 
     PYTHONDONTWRITEBYTECODE=1 OMP_NUM_THREADS=8 OPENBLAS_NUM_THREADS=8 \
         python tests/golden/make_golden_big.py f9
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_big.py f10
+    PYTHONDONTWRITEBYTECODE=1 OMP_NUM_THREADS=1 OPENBLAS_NUM_THREADS=1 \
+        python tests/golden/make_golden_big.py f11   # the reference pool policy: 1 BLAS thread
+    PYTHONDONTWRITEBYTECODE=1 OMP_NUM_THREADS=8 OPENBLAS_NUM_THREADS=8 \
+        python tests/golden/make_golden_big.py f9b
 
 It reuses make_golden.py's loader: GP_func imported as shipped, find_len_scales executed with
 only its `smt` import dropped. What runs is the reference's own code:
@@ -16,6 +20,11 @@ only its `smt` import dropped. What runs is the reference's own code:
     wrapped to record the mean / sd it returned, so the fixture holds exactly the mu/sd the
     reference scored (one GP per particle instead of two). F9 is generated with 8 BLAS threads
     (single-threaded it takes ~25 min); threads change only the rounding of the LAPACK calls.
+  * F11 (config B data, N=1024 d=2, seed 0 as SURVEY.md §8d prescribes for B): evaluate_loss
+    and the recorded mean / sd for 8 interior particles, so config B's own timed schedule (a
+    32-particle batch on the early-diagonal path) is pinned to the reference.
+  * F9b: two more config E particles (particle seed 16384 + 8), same recording as F9, so the
+    default 16-particle E batch holds 4 reference-scored particles.
   * F10: the KMeans subsample of len_scale_opt (find_len_scales.py:25-47) at N = 300..4096:
     the reference's Pool is replaced by a stub whose map() captures the (x, y, e, bounds) the
     first fan-out ships (:76) and stops the run; the kept indices are recovered by matching
@@ -151,5 +160,9 @@ if __name__ == "__main__":
         make_scored("f8_configC", 4096, 3, False, 1, 4, 4096 + 7)
     if "f9" in what:
         make_scored("f9_configE", 16384, 4, True, 1, 2, 16384 + 7)
+    if "f9b" in what:
+        make_scored("f9b_configE", 16384, 4, True, 1, 2, 16384 + 8)
     if "f10" in what:
         make_f10()
+    if "f11" in what:
+        make_scored("f11_configB", 1024, 2, False, 0, 8, 1024 + 7)

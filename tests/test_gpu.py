@@ -565,18 +565,81 @@ def test_configD_share_two_groups_vs_reference(ctx, monkeypatch):
             assert_loss_or_ties(loss[k], w, m0, s0, y, s, what=k)
 
 
-def test_configE_share_two_groups_vs_reference(ctx, monkeypatch):
-    """Config E's per-GPU share (N=16384 d=4 heteroscedastic, 16 particles, 128 block columns)
-    on its default two-group schedule. The 2 particles of F9 (the reference's evaluate_loss at
-    this size, make_golden_big.py) among 14 others: mu/sd at 1e-6, objective at 1e-8 or
-    threshold ties; deterministic; bitwise equal to the one-group schedule."""
+def test_configC_full_swarm_vs_reference(ctx, monkeypatch):
+    """BASELINE config C exactly as bench.py times it: N=4096 d=3, one 64-particle batch on the
+    default schedule (two particle groups of 32 on concurrent streams, 992 workgroups per
+    launch, two slot rounds). The 4 particles of F8 (the reference's evaluate_loss and the GP()
+    mu/sd inside it, make_golden_big.py) sit among 60 others, two in each group: mu/sd at 1e-6,
+    objective at 1e-8 or threshold ties; deterministic; bitwise equal to the one-group
+    schedule; 4 further particles against the oracle's identity form."""
     import gpfit
     from conftest import load_golden
+    plan = gpfit.plan_check(64, 32)
+    assert plan["groups"] == 2 and plan["diag_workgroups"] == 0  # the slot-bound fused schedule
+    fx = load_golden("f8_configC.npz")
+    rng = np.random.default_rng(6464)
+    P = rng.uniform(0.05, 0.6, size=(64, 3))
+    slots = [0, 21, 40, 63]  # groups are particles [0, 32) and [32, 64)
+    P[slots] = fx["P"]
+    x, y, e, loss, mu, sd = _reference_share(ctx, monkeypatch, fx, P, slots)
+    s, ex, lo, hi = fx["sigma_vals"], fx["expected"], fx["lo"], fx["hi"]
+    with _blas_threads():
+        for k in (7, 31, 32, 55):
+            m0, s0 = ref_cpu.GP_train_identity(x, y, e, P[k])
+            assert _rel(mu[k], m0) < RTOL_MU_SD and _rel(sd[k], s0) < RTOL_MU_SD
+            w = ref_cpu.coverage_loss(m0, s0, y, s, ex) + 0.01 * ref_cpu.proximity_penalty(P[k], lo, hi)
+            assert_loss_or_ties(loss[k], w, m0, s0, y, s, what=k)
+
+
+def test_configB_schedule_vs_reference(ctx, monkeypatch):
+    """BASELINE config B exactly as bench.py times it: N=1024 d=2 with §8d's seed 0, one
+    32-particle batch on B's default schedule (the early diagonal factor: launch J starts with
+    one diagonal workgroup per particle that publishes block J through a flag; one group). The 8
+    particles of F11 (the reference's evaluate_loss and its GP() mu/sd on exactly this data,
+    make_golden_big.py) sit among 24 others: mu/sd at 1e-6, objective at 1e-8 or threshold ties;
+    deterministic across runs; and the 24 others against the oracle's identity form."""
+    import gpfit
+    from conftest import load_golden
+    plan = gpfit.plan_check(32, 8)
+    assert plan["diag_workgroups"] == 32 * 8 and plan["groups"] == 1 and plan["S"] == 1
+    fx = load_golden("f11_configB.npz")
+    rng = np.random.default_rng(1024)
+    P = rng.uniform(0.05, 0.6, size=(32, 2))
+    slots = [0, 3, 8, 13, 17, 22, 27, 31]
+    P[slots] = fx["P"]
+    x, y, e, loss, mu, sd = _reference_share(ctx, monkeypatch, fx, P, slots, rounds=3)
+    s, ex, lo, hi = fx["sigma_vals"], fx["expected"], fx["lo"], fx["hi"]
+    for k in (k for k in range(32) if k not in slots):
+        m0, s0 = ref_cpu.GP_train_identity(x, y, e, P[k])
+        assert _rel(mu[k], m0) < RTOL_MU_SD and _rel(sd[k], s0) < RTOL_MU_SD, k
+        w = ref_cpu.coverage_loss(m0, s0, y, s, ex) + 0.01 * ref_cpu.proximity_penalty(P[k], lo, hi)
+        assert_loss_or_ties(loss[k], w, m0, s0, y, s, what=k)
+
+
+def _config_e_fixture():
+    """F9 and F9b (two more reference-scored particles on the same data) as one fixture."""
+    from conftest import load_golden
+    a = load_golden("f9_configE.npz")
+    fx = {k: a[k] for k in a.files}
+    b = load_golden("f9b_configE.npz")
+    assert str(b["data_sha256"]) == str(fx["data_sha256"])
+    for k in ("P", "loss", "mu", "sd"):
+        fx[k] = np.concatenate([fx[k], b[k]])
+    return fx
+
+
+def test_configE_share_two_groups_vs_reference(ctx, monkeypatch):
+    """Config E's per-GPU share (N=16384 d=4 heteroscedastic, 16 particles, 128 block columns)
+    on its default two-group schedule. The 4 particles of F9 + F9b (the reference's
+    evaluate_loss at this size, make_golden_big.py), two in each group, among 12 others: mu/sd
+    at 1e-6, objective at 1e-8 or threshold ties; deterministic; bitwise equal to the one-group
+    schedule."""
+    import gpfit
     assert gpfit.plan_check(16, 128)["groups"] == 2
-    fx = load_golden("f9_configE.npz")
+    fx = _config_e_fixture()
     rng = np.random.default_rng(1604)
     P = rng.uniform(0.05, 0.6, size=(16, 4))
-    slots = [3, 12]
+    slots = [3, 6, 12, 15]
     P[slots] = fx["P"]
     _reference_share(ctx, monkeypatch, fx, P, slots)
 
@@ -587,15 +650,11 @@ def test_early_diagonal_factor_matches_fused(ctx, monkeypatch, N, d, P):
     start of launch J and handed to the tiles through a flag) against the fused factor at the end
     of the previous launch's critical tile: the same arithmetic, so bitwise equal scores, mean
     and sd, on the critical-split (N=1000), unsplit and all-tile-split (one particle) paths; and
-    the factor itself bitwise equal for the prediction path. The fused path's deep diagonal
-    update (GPF_DEEP_SYRK = 1, off by default: the critical tile applies A_II -= L_I,<=J L_I,<=J^T
-    in one GEMM) runs the look-ahead's additions in the same order: bitwise equal to the
-    per-launch look-ahead; so does its pre-update (GPF_DEEP_SYRK = 2: tile I = J+2 applies the
-    terms k <= J in one GEMM one launch ahead, the critical tile the last one). With the quadrant finish of the critical tile on (GPF_QUAD = 1, off by default:
-    the triangular multiply and the rank-128 update in 64-wide quadrants on four workgroups, the
-    update summed per column half) the rounding differs: mean/sd within 1e-8 of the fused path
-    and the factor within 1e-8 normwise (two fp64 evaluations of a system with condition numbers
-    up to ~1e6), scores within RTOL_LOSS or threshold ties."""
+    the factor itself bitwise equal for the prediction path. The deferred diagonal update (one
+    SYRK workgroup per particle and launch applies the earlier terms to the next diagonal block,
+    the critical tile the last one; GPF_DEFER_SYRK=0 restores the per-tile look-ahead) runs the
+    same MFMAs per element in the same order: bitwise equal to the look-ahead, with either
+    diagonal factor."""
     rng = np.random.default_rng(N + P)
     x = rng.uniform(size=(d, N))
     y = np.sin(5 * x[0]) + 0.1 * rng.standard_normal(N)
@@ -607,34 +666,48 @@ def test_early_diagonal_factor_matches_fused(ctx, monkeypatch, N, d, P):
     Q = rng.uniform(0.1, 0.5, size=(P, d))
     out = {}
     monkeypatch.setenv("GPF_SPLIT_CRIT", "4")  # the critical-split path (off by default since round 2)
-    for mode, ed, qf, deep in (("fused", "0", "0", "0"), ("fused_deep", "0", "0", "1"), ("fused_pre", "0", "0", "2"),
-                               ("ed", "1", "0", "0"), ("quad", "1", "1", "0")):
+    for mode, ed, defer in (("fused", "0", "1"), ("fused_lookahead", "0", "0"), ("ed", "1", "1"),
+                            ("ed_lookahead", "1", "0")):
         monkeypatch.setenv("GPF_EARLY_DIAG", ed)
-        monkeypatch.setenv("GPF_QUAD", qf)
-        monkeypatch.setenv("GPF_DEEP_SYRK", deep)
+        monkeypatch.setenv("GPF_DEFER_SYRK", defer)
         out[mode] = ctx.eval_batch(Q, want_mu_sd=True)
         if P == 1:
             out[mode + "f"] = ctx.debug_factor(Q[0])
-    for k in ("GPF_EARLY_DIAG", "GPF_QUAD", "GPF_DEEP_SYRK"):
+    for k in ("GPF_EARLY_DIAG", "GPF_DEFER_SYRK"):
         monkeypatch.delenv(k)
-    for other in ("fused_deep", "fused_pre", "ed"):
+    for other in ("fused_lookahead", "ed", "ed_lookahead"):
         for a, b in zip(out["fused"], out[other]):
             np.testing.assert_array_equal(a, b)
         if P == 1:
             for a, b in zip(out["fusedf"], out[other + "f"]):
                 np.testing.assert_array_equal(np.tril(a) if a.ndim == 2 else a, np.tril(b) if b.ndim == 2 else b)
-    loss_f, mu_f, sd_f = out["fused"]
-    loss_q, mu_q, sd_q = out["quad"]
-    assert _rel(mu_q, mu_f) < 1e-8 and _rel(sd_q, sd_f) < 1e-8
-    for k in range(P):
-        assert_loss_or_ties(loss_q[k], loss_f[k], mu_f[k], sd_f[k], y, s, what=k)
-    if P == 1:
-        for a, b in zip(out["fusedf"], out["quadf"]):
-            a, b = (np.tril(a), np.tril(b)) if a.ndim == 2 else (a, b)
-            assert np.abs(a - b).max() <= 1e-8 * np.abs(a).max()
-    mo, so = ref_cpu.GP_train_identity(x, y, e, Q[0]) if N <= 2049 else (None, None)
-    if mo is not None:
-        assert _rel(out["quad"][1][0], mo) < RTOL_MU_SD and _rel(out["quad"][2][0], so) < RTOL_MU_SD
+    if N <= 2049:
+        mo, so = ref_cpu.GP_train_identity(x, y, e, Q[0])
+        assert _rel(out["fused"][1][0], mo) < RTOL_MU_SD and _rel(out["fused"][2][0], so) < RTOL_MU_SD
+
+
+def test_handoff_timeout_is_reported(ctx, monkeypatch):
+    """The bounded spin of the in-launch hand-offs (gpf::wait_diag): with the bound forced to zero
+    polls (GPF_WAIT_SPINS=0) a tile that finds the diagonal block (or the SYRK workgroup's update)
+    not yet published gives up, skips the work that would read it, and the host reports the
+    timeout as a device error instead of scoring garbage; the next batch with the normal bound is
+    correct again."""
+    N, d = 1024, 2
+    rng = np.random.default_rng(77)
+    x = rng.uniform(size=(d, N))
+    y = np.sin(4 * x[0]) + 0.1 * rng.standard_normal(N)
+    e = np.full(N, 0.1)
+    s, ex = ref_cpu.sigma_grid()
+    lo, hi = ref_cpu.search_bounds(x)
+    ctx.set_data(x, y, e)
+    ctx.set_grid(s, ex, lo, hi)
+    P = rng.uniform(0.1, 0.5, size=(32, d))
+    want = ctx.eval_batch(P)
+    monkeypatch.setenv("GPF_WAIT_SPINS", "0")
+    with pytest.raises(RuntimeError, match="timed out"):
+        ctx.eval_batch(P)
+    monkeypatch.delenv("GPF_WAIT_SPINS")
+    np.testing.assert_array_equal(ctx.eval_batch(P), want)
 
 
 @pytest.mark.gpu

@@ -106,3 +106,30 @@ def test_pairwise_sum_order():
     for n in [1, 5, 8, 9, 127, 128, 129, 999, 1000, 4097]:
         a = rng.standard_normal(n) * 10.0 ** rng.integers(-8, 8, size=n)
         assert pairwise_sum(a) == a.sum()
+
+
+def test_evaluate_loss_bitwise_configB_fixture():
+    """F11 (the reference's evaluate_loss on config B's data, N=1024 d=2, seed 0): the oracle
+    reproduces the losses and the recorded GP() mean/sd bit for bit; the inputs regenerate
+    from the seed (sha256 stored with the fixture)."""
+    from conftest import fixture_data, load_golden
+    fx = load_golden("f11_configB.npz")
+    x, y, e = fixture_data(fx["meta"], fx["data_sha256"])
+    lo, hi = ref_cpu.search_bounds(x)
+    np.testing.assert_array_equal(lo, fx["lo"])
+    np.testing.assert_array_equal(hi, fx["hi"])
+    s, ex = fx["sigma_vals"], fx["expected"]
+    for k, p in enumerate(fx["P"][:3]):  # ~0.3 s each on one core
+        assert ref_cpu.evaluate_loss(p, x, y, e, s, ex, lo, hi) == fx["loss"][k], k
+        mu, sd = ref_cpu.GP(x, y, e, x, p, batch_size=x.shape[1])
+        np.testing.assert_array_equal(mu, fx["mu"][k])
+        np.testing.assert_array_equal(sd, fx["sd"][k])
+
+
+def test_configE_fixtures_share_inputs():
+    """F9 and F9b score particles on the same regenerated config-E inputs."""
+    from conftest import load_golden
+    a, b = load_golden("f9_configE.npz"), load_golden("f9b_configE.npz")
+    assert str(a["data_sha256"]) == str(b["data_sha256"])
+    np.testing.assert_array_equal(a["lo"], b["lo"])
+    assert b["mu"].shape == (2, 16384) and np.all(np.isfinite(b["loss"]))

@@ -27,8 +27,8 @@ ENVS = [
     {"GPF_STEP_GROUP": "1"}, {"GPF_STEP_GROUP": "2", "GPF_GROUPS": "2"},
     {"GPF_EARLY_DIAG": "1"}, {"GPF_EARLY_DIAG": "0"},
     {"GPF_EARLY_DIAG": "1", "GPF_SPLIT_CRIT": "8", "GPF_SPLIT_CRIT_MIN": "2", "GPF_GROUPS": "3"},
-    {"GPF_QUAD": "1"}, {"GPF_QUAD": "1", "GPF_EARLY_DIAG": "1"},
-    {"GPF_QUAD": "1", "GPF_EARLY_DIAG": "1", "GPF_SPLIT_CRIT": "8", "GPF_SPLIT_CRIT_MIN": "2", "GPF_GROUPS": "2"},
+    {"GPF_DEFER_SYRK": "0"}, {"GPF_DEFER_SYRK": "0", "GPF_EARLY_DIAG": "1"},
+    {"GPF_DEFER_SYRK": "0", "GPF_EARLY_DIAG": "1", "GPF_SPLIT_CRIT": "8", "GPF_SPLIT_CRIT_MIN": "2", "GPF_GROUPS": "2"},
 ]
 
 
@@ -36,7 +36,7 @@ ENVS = [
 def env(monkeypatch):
     def apply(kv):
         for k in ("GPF_GROUPS", "GPF_SPLIT_K", "GPF_SPLIT_CRIT", "GPF_SPLIT_CRIT_MIN", "GPF_STEP_GROUP", "GPF_EARLY_DIAG",
-                  "GPF_QUAD"):
+                  "GPF_DEFER_SYRK"):
             monkeypatch.delenv(k, raising=False)
         for k, v in kv.items():
             monkeypatch.setenv(k, v)
@@ -56,9 +56,10 @@ def test_every_tile_has_exactly_one_finisher(env, kv):
             assert st["whole_tiles"] + st["split_tiles"] == pc * (nt - 1) * nt  # every (J, p, w)
             # early diagonal factor: one diagonal workgroup per particle in every launch
             assert st["diag_workgroups"] in (0, pc * nt if nt > 1 else 0)
-            # quadrant finish: four workgroups per particle in every launch but the last
-            assert st["quad_workgroups"] in (0, 4 * pc * (nt - 1))
-            assert st["quad_workgroups"] == 0 or st["diag_workgroups"] > 0
+            # deferred diagonal update: one SYRK workgroup per particle in launches 1 .. nt-2,
+            # except under the all-tile split (which keeps the per-tile look-ahead)
+            assert st["syrk_workgroups"] in (0, pc * max(0, nt - 2))
+            assert st["syrk_workgroups"] == 0 or st["S"] == 1
             seen_split += st["split_tiles"] > 0
             seen_groups += st["groups"] > 1
     if kv.get("GPF_SPLIT_K") or kv.get("GPF_SPLIT_CRIT") or not kv:
@@ -89,8 +90,10 @@ def test_default_plans_of_the_baseline_configs(env):
     assert e["diag_workgroups"] == 0
     assert (c["diag_workgroups"], d["diag_workgroups"]) == (0, 0)
     assert b["diag_workgroups"] == 32 * 8 and one["diag_workgroups"] == 32
-    # quadrant finish of the critical tile: off by default (GPF_QUAD, profiles/r2/quad_finish_ab_rejected.txt)
-    assert all(x["quad_workgroups"] == 0 for x in (b, c, d, e, one))
+    # deferred diagonal update (one SYRK workgroup per particle and launch 1 .. nt-2) everywhere
+    # but the all-tile split of the prediction
+    assert (b["syrk_workgroups"], c["syrk_workgroups"]) == (32 * 6, 64 * 30)
+    assert (d["syrk_workgroups"], e["syrk_workgroups"], one["syrk_workgroups"]) == (32 * 30, 16 * 126, 0)
 
 
 def test_early_diag_override(env):
@@ -100,13 +103,12 @@ def test_early_diag_override(env):
     assert gpfit.plan_check(32, 8)["diag_workgroups"] == 0
 
 
-def test_quad_override(env):
-    env({"GPF_QUAD": "1"})
-    assert gpfit.plan_check(32, 8)["quad_workgroups"] == 4 * 32 * 7
-    assert gpfit.plan_check(1, 32)["quad_workgroups"] == 4 * 31
-    assert gpfit.plan_check(64, 32)["quad_workgroups"] == 0  # only with the early diagonal factor
-    env({"GPF_QUAD": "1", "GPF_EARLY_DIAG": "1"})
-    assert gpfit.plan_check(64, 32)["quad_workgroups"] == 4 * 64 * 31
+def test_defer_syrk_override(env):
+    env({"GPF_DEFER_SYRK": "0"})
+    assert gpfit.plan_check(32, 8)["syrk_workgroups"] == 0
+    assert gpfit.plan_check(64, 32)["syrk_workgroups"] == 0
+    env({"GPF_DEFER_SYRK": "1", "GPF_SPLIT_K": "4"})  # the all-tile split never defers
+    assert gpfit.plan_check(8, 16)["syrk_workgroups"] == 0
 
 
 def test_env_is_read_per_call(env):
