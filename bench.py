@@ -303,7 +303,11 @@ def open_exchange(ctx, world, rank):
         return rccl, {"transport": "rccl"}
     if rccl is not None:
         rccl.close()
-    return side, {"transport": "host", "rccl_error": err or "another rank could not open RCCL"}
+    why = err or "another rank could not open RCCL"
+    if rank == 0:
+        print(f"bench.py: RCCL unavailable on this node ({why}); the swarm exchange runs over the host "
+              f"transport and the JSON line says so (rccl: false)", file=sys.stderr, flush=True)
+    return side, {"transport": "host", "rccl_error": why}
 
 
 def plumbing(args, world, rank):
@@ -319,12 +323,15 @@ def plumbing(args, world, rank):
     local = np.sum(pos[lo_r:hi_r] ** 2, axis=1)
     full = comm.exchange_scores(P, local) if comm else local
     dt = time.perf_counter() - t0
+    xms = comm.stats()[0] if comm else 0.0
     ranks = int(comm.allreduce([1.0])[0]) if comm else 1
     dt = float(comm.allreduce([dt], op="max")[0]) if comm else dt
+    xms = float(comm.allreduce([xms], op="max")[0]) if comm else 0.0
     if rank == 0:
         print(json.dumps({"metric": "plumbing check (no GPU work)", "value": None, "unit": None, "n_gpus": world,
                           "ranks_joined": ranks, "swarm": P, "scores_ok": bool(np.array_equal(full, np.sum(pos ** 2, axis=1))),
-                          "ms": dt * 1e3}), flush=True)
+                          "ms": dt * 1e3, "rccl": False, "exchange": {"transport": "host"} if comm else None,
+                          "exchange_ms_per_step": xms if comm else None}), flush=True)
     if comm:
         comm.close()
 
@@ -399,6 +406,7 @@ def main():
         ctx.set_profiling(True)
     ctx.reset_profile()
     fence()
+    x0 = comm.stats()[0] if comm is not None else 0.0
     t0 = time.perf_counter()
     best = np.inf
     for _ in range(args.steps):
@@ -406,10 +414,13 @@ def main():
         best = min(best, float(sc[np.argmin(sc)]))
     fence()
     dt = time.perf_counter() - t0
+    xch = (comm.stats()[0] - x0) / args.steps if comm is not None else None  # exchange ms per step, this rank
     prof = ctx.profile()
     ctx.set_profiling(False)
     if comm is not None:
         dt = float(comm.allreduce([dt], op="max")[0])  # max over ranks
+        xch_max = float(comm.allreduce([xch], op="max")[0])
+        xch_min = -float(comm.allreduce([-xch], op="max")[0])
     evals = P * args.steps                # swarm x iterations, all of them full evaluations
     value = evals / dt
 
@@ -518,6 +529,12 @@ def main():
             "breakdown_ms": breakdown,
             "build": gpfit.build_info(),
             "exchange": exchange,
+            # the swarm exchange's own cost (time inside gpf_comm_exchange_scores per step: the
+            # all-reduce of P + G doubles, including the wait for the slowest rank), max and min
+            # over ranks; the min is the collective itself, the max adds the load imbalance
+            "rccl": (exchange["transport"] == "rccl") if exchange else None,
+            "exchange_ms_per_step": xch_max if comm is not None else None,
+            "exchange_ms_per_step_min_rank": xch_min if comm is not None else None,
         }
         print(json.dumps(line), flush=True)
     if comm is not None:

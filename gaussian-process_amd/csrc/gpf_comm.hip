@@ -41,6 +41,8 @@ struct gpf_comm {
   size_t cap = 0;
   int timeout_ms = 600000;
   std::string err;
+  double xch_ms = 0.0;  // wall time inside gpf_comm_exchange_scores (gpf_comm_stats)
+  long long xch_n = 0;
 };
 
 namespace {
@@ -150,6 +152,44 @@ int rendezvous(gpf_comm* c, const char* host, int port) {
   return GPF_OK;
 }
 
+// Every rank's status word to every rank over the rendezvous sockets (star through rank 0): the
+// ranks agree on each step of the RCCL bootstrap before the next, so a failure on one rank fails
+// all of them at that step instead of leaving the others blocked in ncclCommInitRank or in the
+// first all-reduce. Returns the number of ranks whose word was nonzero, or -1 on a socket error.
+int host_agree(gpf_comm* c, int32_t mine) {
+  int32_t bad = mine != 0;
+  if (c->nranks == 1) return bad;
+  if (c->rank == 0) {
+    for (int r = 1; r < c->nranks; ++r) {
+      int32_t w = 0;
+      if (!io_all(c->fd[r], &w, 4, false, c->timeout_ms)) return -1;
+      bad += w != 0;
+    }
+    for (int r = 1; r < c->nranks; ++r)
+      if (!io_all(c->fd[r], &bad, 4, true, c->timeout_ms)) return -1;
+  } else if (!io_all(c->fd[0], &mine, 4, true, c->timeout_ms) || !io_all(c->fd[0], &bad, 4, false, c->timeout_ms)) {
+    return -1;
+  }
+  return bad;
+}
+
+// Non-blocking communicator initialisation with a deadline: a rank whose peers never arrive (or
+// whose init fails) aborts its half-built communicator instead of waiting forever.
+ncclResult_t init_rank_deadline(gpf_comm* c, const ncclUniqueId& id) {
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  ncclResult_t nr = ncclCommInitRankConfig(&c->nccl, c->nranks, id, c->rank, &cfg);
+  if (nr != ncclSuccess && nr != ncclInProgress) return nr;
+  const auto t_end = std::chrono::steady_clock::now() + std::chrono::milliseconds(c->timeout_ms);
+  for (;;) {
+    ncclResult_t st = ncclInProgress;
+    if (ncclCommGetAsyncError(c->nccl, &st) != ncclSuccess) st = ncclInternalError;
+    if (st != ncclInProgress) return st;
+    if (std::chrono::steady_clock::now() > t_end) return ncclInProgress;
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  }
+}
+
 // Rank 0 -> everyone: n bytes (the ncclUniqueId).
 int host_bcast(gpf_comm* c, void* buf, size_t n) {
   if (c->rank == 0) {
@@ -195,8 +235,15 @@ int rccl_allreduce(gpf_comm* c, double* buf, int64_t n, int op) {
   std::memcpy(c->h_buf, buf, (size_t)n * 8);
   if (hipMemcpyAsync(c->d_buf, c->h_buf, (size_t)n * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess)
     return comm_fail(c, "all-reduce: upload failed");
-  const ncclResult_t nr = ncclAllReduce(c->d_buf, c->d_buf, (size_t)n, ncclFloat64, op == GPF_OP_MAX ? ncclMax : ncclSum,
-                                        c->nccl, c->stream);
+  ncclResult_t nr = ncclAllReduce(c->d_buf, c->d_buf, (size_t)n, ncclFloat64, op == GPF_OP_MAX ? ncclMax : ncclSum,
+                                  c->nccl, c->stream);
+  // the communicator is non-blocking (init_rank_deadline): an enqueue may report ncclInProgress
+  // until RCCL has issued it; the stream synchronisation below then orders the result
+  const auto t_end = std::chrono::steady_clock::now() + std::chrono::milliseconds(c->timeout_ms);
+  while (nr == ncclInProgress && std::chrono::steady_clock::now() < t_end) {
+    if (ncclCommGetAsyncError(c->nccl, &nr) != ncclSuccess) nr = ncclInternalError;
+    if (nr == ncclInProgress) std::this_thread::yield();
+  }
   if (nr != ncclSuccess) return comm_fail(c, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
   if (hipMemcpyAsync(c->h_buf, c->d_buf, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess)
@@ -231,21 +278,44 @@ int gpf_comm_open(gpf_ctx* ctx, int rank, int nranks, const char* host, int port
       if (id[i] != (unsigned char)((i * 37 + 11) & 255)) rc = comm_fail(c, "gpf_comm_open: id broadcast corrupted");
   }
   if (rc == GPF_OK && transport == GPF_COMM_RCCL) {
+    // bootstrap in agreed steps (host_agree after each): rank 0's id (with its status word),
+    // every rank's stream, then the communicator itself (non-blocking init with a deadline), so a
+    // failure on any rank fails every rank at the same step with that rank's message
     c->device = ctx->device;
-    ncclUniqueId id;
-    std::memset(&id, 0, sizeof(id));
+    struct {
+      int32_t status;
+      ncclUniqueId id;
+    } msg;
+    std::memset(&msg, 0, sizeof(msg));
     if (rank == 0) {
-      const ncclResult_t nr = ncclGetUniqueId(&id);
-      if (nr != ncclSuccess) rc = comm_fail(c, std::string("ncclGetUniqueId: ") + ncclGetErrorString(nr));
-    }
-    if (rc == GPF_OK && nranks > 1) rc = host_bcast(c, &id, sizeof(id));
-    if (rc == GPF_OK) {
-      if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-        rc = comm_fail(c, "gpf_comm_open: stream creation failed");
-      } else {
-        const ncclResult_t nr = ncclCommInitRank(&c->nccl, nranks, id, rank);
-        if (nr != ncclSuccess) rc = comm_fail(c, std::string("ncclCommInitRank: ") + ncclGetErrorString(nr));
+      const ncclResult_t nr = ncclGetUniqueId(&msg.id);
+      if (nr != ncclSuccess) {
+        msg.status = 1;
+        comm_fail(c, std::string("ncclGetUniqueId: ") + ncclGetErrorString(nr));
       }
+    }
+    if (nranks > 1) rc = host_bcast(c, &msg, sizeof(msg));
+    if (rc == GPF_OK && msg.status != 0) rc = comm_fail(c, rank == 0 ? c->err : "gpf_comm_open: rank 0 could not create the RCCL id");
+    int32_t mine = 0;
+    if (rc == GPF_OK &&
+        (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)) {
+      mine = 1;
+      comm_fail(c, "gpf_comm_open: stream creation failed");
+    }
+    if (rc == GPF_OK) {
+      const int nbad = host_agree(c, mine);
+      if (nbad != 0) rc = comm_fail(c, mine ? c->err : nbad < 0 ? "gpf_comm_open: rendezvous lost" : "gpf_comm_open: another rank could not create its stream");
+    }
+    if (rc == GPF_OK) {
+      const ncclResult_t nr = init_rank_deadline(c, msg.id);
+      mine = nr != ncclSuccess;
+      if (mine) {
+        comm_fail(c, std::string("ncclCommInitRank: ") + (nr == ncclInProgress ? "timed out" : ncclGetErrorString(nr)));
+        if (c->nccl) ncclCommAbort(c->nccl);
+        c->nccl = nullptr;
+      }
+      const int nbad = host_agree(c, mine);
+      if (nbad != 0) rc = comm_fail(c, mine ? c->err : nbad < 0 ? "gpf_comm_open: rendezvous lost" : "gpf_comm_open: ncclCommInitRank failed on another rank");
     }
   }
   if (rc != GPF_OK) {
@@ -270,6 +340,12 @@ void gpf_comm_close(gpf_comm* c) {
 }
 
 int gpf_comm_rank(const gpf_comm* c) { return c ? c->rank : -1; }
+int gpf_comm_stats(const gpf_comm* c, double* exchange_ms, long long* exchanges) {
+  if (!c) return GPF_BAD_ARG;
+  if (exchange_ms) *exchange_ms = c->xch_ms;
+  if (exchanges) *exchanges = c->xch_n;
+  return GPF_OK;
+}
 int gpf_comm_size(const gpf_comm* c) { return c ? c->nranks : -1; }
 const char* gpf_comm_last_error(const gpf_comm* c) { return c ? c->err.c_str() : "null communicator"; }
 
@@ -293,7 +369,11 @@ int gpf_comm_exchange_scores(gpf_comm* c, int P, const double* local, int local_
   } else {
     buf[(size_t)P + r] = local_rc == GPF_NOT_PD ? 1.0 + (double)(lo + std::max(local_bad, 0)) : -(double)local_rc;
   }
-  if (int rc = gpf_comm_allreduce(c, buf.data(), (int64_t)buf.size(), GPF_OP_SUM)) return rc;
+  const auto t0 = std::chrono::steady_clock::now();
+  const int arc = gpf_comm_allreduce(c, buf.data(), (int64_t)buf.size(), GPF_OP_SUM);
+  c->xch_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  ++c->xch_n;
+  if (arc) return arc;
   int bad = -1, failed = -1, code = GPF_OK;
   for (int q = 0; q < G; ++q) {
     const double s = buf[(size_t)P + q];

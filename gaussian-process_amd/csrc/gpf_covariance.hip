@@ -95,51 +95,66 @@ __global__ __launch_bounds__(NTHR) void k_build_cov(int N, int Npad, int d, cons
 
 // Rectangular cross-covariance kernel_func(x1, x2, l) (no noise) into
 // out[i*ldo + j] for i < R, j < C; entries with i >= N1 or j >= N2 are 0.
-// grid: (ceil(C/64), ceil(R/64))
+// One workgroup per 64 x 256 output block: the scaled coordinates and squared norms of its 64
+// rows and 256 columns are staged once in LDS (dynamic: d x 320 + 320 doubles), then every lane
+// writes 64 outputs, a wave covering 64 consecutive columns of one row (512 contiguous bytes;
+// 4 waves = one 2 KiB row segment). A write-bound kernel (8 B per output) once the exponential
+// per output is spread over enough resident waves: the LDS is sized by d, not DMAX.
+// grid: (ceil(C/256), ceil(R/64)), dynamic LDS cross_cov_lds(d) bytes
+constexpr int CC_R = 64, CC_C = 256;
+__host__ __device__ constexpr size_t cross_cov_lds(int d) { return (size_t)(d + 1) * (CC_R + CC_C) * 8; }
 __global__ __launch_bounds__(NTHR) void k_cross_cov(int N1, int N2, int R, int C, int d,
                                                     const double* __restrict__ x1, int ld1,
                                                     const double* __restrict__ x2, int ld2,
                                                     const double* __restrict__ l, double* __restrict__ out,
                                                     int64_t ldo) {
-  __shared__ double ai[DMAX][BT];
-  __shared__ double aj[DMAX][BT];
-  __shared__ double ni[BT], nj[BT];
+  extern __shared__ double cc_lds[];
+  double* ai = cc_lds;                  // [d][64]
+  double* aj = ai + (size_t)d * CC_R;   // [d][256]
+  double* ni = aj + (size_t)d * CC_C;   // [64]
+  double* nj = ni + CC_R;               // [256]
   const int tid = threadIdx.x;
   const int bi = blockIdx.y, bj = blockIdx.x;
-  if (tid < 128) {
-    const int t = tid & 63;
-    const bool first = tid < 64;
-    const int g = (first ? bi : bj) * BT + t;
+  for (int t = tid; t < CC_R + CC_C; t += NTHR) {
+    const bool first = t < CC_R;
+    const int tt = first ? t : t - CC_R;
+    const int g = first ? bi * CC_R + tt : bj * CC_C + tt;
     const int lim = first ? N1 : N2;
     const double* xs = first ? x1 : x2;
     const int ldx = first ? ld1 : ld2;
-    double(*a)[BT] = first ? ai : aj;
+    double* a = first ? ai : aj;
+    const int lda = first ? CC_R : CC_C;
     double nrm = 0.0;
     if (g < lim) {
       for (int k = 0; k < d; ++k) {
         const double v = xs[(size_t)k * ldx + g] / l[k];
-        a[k][t] = v;
+        a[k * lda + tt] = v;
         nrm = nrm + v * v;
       }
     }
-    if (first) ni[t] = nrm; else nj[t] = nrm;
+    (first ? ni : nj)[tt] = nrm;
   }
   __syncthreads();
+  const int c = tid & (CC_C - 1);  // this lane's column (the 4 waves cover 256 consecutive ones)
+  const int gj = bj * CC_C + c;
+  if (gj >= C) return;
+  const double* bcol = aj + c;  // column coordinates, stride CC_C
+  const double nc = nj[c];
+  double* op = out + gj;
+  const int r0 = bi * CC_R;
+  const int rmax = min(CC_R, R - r0);
 #pragma unroll 4
-  for (int u = 0; u < (BT * BT) / NTHR; ++u) {
-    const int q = tid + NTHR * u;
-    const int r = q >> 6, c = q & 63;
-    const int gi = bi * BT + r, gj = bj * BT + c;
-    if (gi >= R || gj >= C) continue;
+  for (int r = 0; r < rmax; ++r) {
+    const int gi = r0 + r;
     double v = 0.0;
     if (gi < N1 && gj < N2) {
-      double dot = ai[0][r] * aj[0][c];
-      for (int k = 1; k < d; ++k) dot = fma(ai[k][r], aj[k][c], dot);
-      double r2 = (ni[r] + nj[c]) - 2.0 * dot;
+      double dot = ai[r] * bcol[0];
+      for (int k = 1; k < d; ++k) dot = fma(ai[k * CC_R + r], bcol[k * CC_C], dot);
+      double r2 = (ni[r] + nc) - 2.0 * dot;
       r2 = r2 > 0.0 ? r2 : 0.0;
       v = exp(-0.5 * r2);
     }
-    out[(size_t)gi * ldo + gj] = v;
+    op[(size_t)gi * ldo] = v;
   }
 }
 

@@ -651,6 +651,9 @@ static_assert(STEP_NTH == DNTH, "the fused diagonal runs on the step workgroup")
 #ifndef GPF_DIAG_PRIO
 #define GPF_DIAG_PRIO 1
 #endif
+#ifndef GPF_WAVE_PRIO
+#define GPF_WAVE_PRIO 0  // build-time A/B knob
+#endif
 #ifndef GPF_STEP_WAVES_PER_SIMD
 #define GPF_STEP_WAVES_PER_SIMD 4  // 2 workgroups of 8 waves per CU
 #endif
@@ -1010,6 +1013,11 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
 #endif
   __shared__ __attribute__((aligned(16))) double lds[STEP_LDS];
   __shared__ int sflag;
+#if GPF_WAVE_PRIO
+  // static priority for the second half of the workgroup (waves 4-7 share their SIMDs with waves
+  // 0-3 and lose every arbitration by age otherwise; MI355X_MICROARCH "Two waves per SIMD" item 4)
+  if (__builtin_amdgcn_readfirstlane(tid >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
   int p, w, sidx;
   const int role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, SPLIT != SPLIT_ALL && sy, p, w, sidx);
   if (SPLIT != SPLIT_ALL && role == ROLE_SYRK) {

@@ -914,7 +914,8 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
     const int nqt = (int)((m + T - 1) / T);
     const int Cm = nqt * T;
     rc = launch(c, PC_PREDK, 8.0 * Np * Cm, [&] {
-      hipLaunchKernelGGL(gpf::k_cross_cov, dim3(Cm / BT, (unsigned)(Np / BT)), dim3(NTHR), 0, c->stream, (int)c->N,
+      hipLaunchKernelGGL(gpf::k_cross_cov, dim3((unsigned)((Cm + gpf::CC_C - 1) / gpf::CC_C), (unsigned)(Np / gpf::CC_R)), dim3(NTHR),
+                         gpf::cross_cov_lds(c->d), c->stream, (int)c->N,
                          (int)m, (int)Np, Cm, c->d, c->d_x, (int)c->N, d_xf, (int)Cp, c->d_ls, d_ks, (int64_t)Cp);
     });
     if (rc) break;
@@ -939,6 +940,12 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
   }
   hipStreamSynchronize(c->stream);
   if (c->prof) harvest(c);
+  // keep the query-chunk buffers for the next call only while they are modest (a huge batch_size
+  // can size them up to half of free HBM, which must not stay pinned for the context's life and
+  // starve the next factorisation's or hull's allocations); GPF_PREDICT_KEEP_MB sets the bound
+  double keep_mb = 2048.0;
+  if (const char* e = getenv("GPF_PREDICT_KEEP_MB")) keep_mb = atof(e);
+  if ((double)c->p_np * (double)c->p_cols * 8.0 > keep_mb * 1048576.0) free_pred(c);
   return rc;
 }
 
@@ -958,8 +965,8 @@ int gpf_kernel(gpf_ctx* c, const double* x1, int64_t N1, const double* x2, int64
   GPF_HIP(c, hipMemcpyAsync(dx2, x2, (size_t)N2 * d * 8, hipMemcpyHostToDevice, c->stream));
   GPF_HIP(c, hipMemcpyAsync(dl, l, (size_t)d * 8, hipMemcpyHostToDevice, c->stream));
   int rc = launch(c, PC_BUILD, 8.0 * N1 * N2, [&] {
-    hipLaunchKernelGGL(gpf::k_cross_cov, dim3((unsigned)((N2 + BT - 1) / BT), (unsigned)((N1 + BT - 1) / BT)),
-                       dim3(NTHR), 0, c->stream, (int)N1, (int)N2, (int)N1, (int)N2, d, dx1, (int)N1, dx2, (int)N2,
+    hipLaunchKernelGGL(gpf::k_cross_cov, dim3((unsigned)((N2 + gpf::CC_C - 1) / gpf::CC_C), (unsigned)((N1 + gpf::CC_R - 1) / gpf::CC_R)),
+                       dim3(NTHR), gpf::cross_cov_lds(d), c->stream, (int)N1, (int)N2, (int)N1, (int)N2, d, dx1, (int)N1, dx2, (int)N2,
                        dl, dout, (int64_t)N2);
   });
   if (rc == GPF_OK) {

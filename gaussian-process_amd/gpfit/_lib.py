@@ -59,6 +59,7 @@ SIGNATURES = {
     "gpf_comm_rank": (ctypes.c_int, [_vp]),
     "gpf_comm_size": (ctypes.c_int, [_vp]),
     "gpf_comm_last_error": (ctypes.c_char_p, [_vp]),
+    "gpf_comm_stats": (ctypes.c_int, [_vp, _dp, ctypes.POINTER(ctypes.c_longlong)]),
     "gpf_comm_allreduce": (ctypes.c_int, [_vp, _dp, ctypes.c_int64, ctypes.c_int]),
     "gpf_comm_exchange_scores": (ctypes.c_int, [_vp, ctypes.c_int, _dp, ctypes.c_int, ctypes.c_int, _dp, _ip]),
     "gpf_eval_batch_sharded": (ctypes.c_int, [_vp, _vp, _dp, ctypes.c_int, _dp, _ip]),
@@ -383,6 +384,15 @@ class Comm:
 
     def barrier(self):
         self.allreduce(np.zeros(1))
+
+    def stats(self):
+        """(ms, count): cumulative wall time this rank spent in the score exchange
+        (gpf_comm_exchange_scores: the all-reduce, including the wait for the slowest rank)."""
+        ms = ctypes.c_double(0.0)
+        n = ctypes.c_longlong(0)
+        if self.lib.gpf_comm_stats(self.handle, ctypes.byref(ms), ctypes.byref(n)) != GPF_OK:
+            raise GPFitError("gpf_comm_stats failed")
+        return ms.value, n.value
 
     def rows(self, P):
         """This rank's contiguous rows [rP/G, (r+1)P/G) of a P-particle swarm."""

@@ -109,15 +109,25 @@ class ShardedScorer:
         if self.ctx is not None:
             return self.ctx.eval_batch_sharded(self.comm, positions)
         from ._lib import GPF_HIP_ERROR, GPF_NOT_PD, GPF_OK
-        rc, local, failure = GPF_OK, None, None
+        rc, local, failure, bad = GPF_OK, None, None, -1
         try:
             local = np.asarray(self.backend(positions[lo:hi]), dtype=np.float64) if hi > lo else np.zeros(0)
         except np.linalg.LinAlgError:
-            rc = GPF_NOT_PD  # (the injected evaluator does not say which row; the first is reported)
+            rc = GPF_NOT_PD
+            # the injected evaluator does not say which row failed: score the rows one at a time
+            # (this path only runs on error), so the exchange reports the smallest failing row of
+            # the whole swarm, the particle the reference's in-order map raises on
+            bad = 0
+            for i in range(hi - lo):
+                try:
+                    self.backend(positions[lo + i:lo + i + 1])
+                except np.linalg.LinAlgError:
+                    bad = i
+                    break
         except Exception as exc:  # noqa: BLE001 - re-raised below, after the other ranks are told
             rc, failure = GPF_HIP_ERROR, exc
         try:
-            return self.comm.exchange_scores(P, local, rc, 0)
+            return self.comm.exchange_scores(P, local, rc, bad)
         except Exception:
             if failure is not None:
                 raise failure

@@ -22,7 +22,8 @@
  *   - host buffers are caller-owned; data set by gpf_set_data stays resident
  *     on the device until the next gpf_set_data / gpf_close;
  *   - a context drives ONE device and is not thread-safe (one host thread per
- *     context; one process per GPU, torch.distributed over RCCL above it).
+ *     context); one process per GPU, the swarm exchange between them is in this
+ *     library (gpf_comm_*: RCCL over xGMI, or a host transport).
  *
  * Return codes: GPF_OK, GPF_NOT_PD (Cholesky pivot <= 0 or NaN: the Python side
  * raises numpy.linalg.LinAlgError("Matrix is not positive definite") exactly
@@ -139,6 +140,9 @@ void gpf_comm_close(gpf_comm* comm);
 int gpf_comm_rank(const gpf_comm* comm);
 int gpf_comm_size(const gpf_comm* comm);
 const char* gpf_comm_last_error(const gpf_comm* comm);
+/* Cumulative wall time spent inside gpf_comm_exchange_scores on this rank (the all-reduce,
+ * including the wait for the slowest rank) and the number of exchanges. */
+int gpf_comm_stats(const gpf_comm* comm, double* exchange_ms, long long* exchanges);
 
 /* In-place all-reduce of n host doubles (GPF_OP_SUM or GPF_OP_MAX) across the ranks: the
  * seed broadcast of the PSO driver, the bench's barrier and max-over-ranks timing. */

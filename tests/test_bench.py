@@ -29,6 +29,9 @@ def test_gpus_flag_starts_that_many_ranks(n):
     out = json.loads(lines[0])
     assert out["n_gpus"] == n and out["ranks_joined"] == n and out["scores_ok"]
     assert out["swarm"] == 32 * n  # config D's 32 particles per GPU
+    # the scaling line describes its exchange: transport, RCCL or not, its cost per step
+    assert out["rccl"] is False and out["exchange"] == {"transport": "host"}
+    assert out["exchange_ms_per_step"] >= 0.0
 
 
 def test_world_size_mismatch_is_an_error():
@@ -50,7 +53,8 @@ def test_multi_rank_bench_on_one_gpu():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["swarm"] == 64 and out["value"] > 0
     assert out["config"]["swarm_per_gpu"] == 32
-    assert out["exchange"] == {"transport": "host"}
+    assert out["exchange"] == {"transport": "host"} and out["rccl"] is False
+    assert 0.0 <= out["exchange_ms_per_step_min_rank"] <= out["exchange_ms_per_step"]
 
 
 @pytest.mark.gpu
@@ -67,5 +71,7 @@ def test_multi_rank_bench_rccl_agreement_on_one_gpu():
     assert out["n_gpus"] == 2 and out["value"] > 0
     ex = out["exchange"]
     assert ex["transport"] in ("rccl", "host")
+    assert out["rccl"] == (ex["transport"] == "rccl") and out["exchange_ms_per_step"] >= 0.0
     if ex["transport"] == "host":
         assert ex["rccl_error"]
+        assert "RCCL unavailable" in r.stderr  # one stderr line says the fallback triggered

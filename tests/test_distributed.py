@@ -127,6 +127,40 @@ def test_exchange_protocol(world):
         assert out["sum"] == [world, world * (world - 1) / 2]
 
 
+def _injected_notpd_worker(rank, world, port, q):
+    """ShardedScorer with an injected evaluator that raises LinAlgError (like numpy's cholesky)
+    for particles 5 and 8 of a 10-particle swarm: every rank must report particle 5."""
+    _env(rank, world, port)
+    import gpfit
+    from gpfit.swarm import ShardedScorer
+    comm = gpfit.Comm.from_env()
+    pos = np.arange(10.0)[:, None] * np.ones((1, 2))
+
+    def backend(rows):
+        if np.any(np.isin(rows[:, 0], (5.0, 8.0))):
+            raise np.linalg.LinAlgError("Matrix is not positive definite")
+        return rows[:, 0] * 2.0
+
+    sc = ShardedScorer(backend, comm=comm)
+    ok = sc(pos[[0, 1, 2, 3, 4, 6, 7, 9, 9, 9]]).tolist()
+    try:
+        sc(pos)
+        bad = None
+    except np.linalg.LinAlgError as e:
+        bad = e.bad_index
+    comm.close()
+    q.put((rank, ok, bad))
+
+
+def test_injected_evaluator_reports_the_failing_row():
+    """with an injected evaluator the exchange used to report the failing rank's first
+    row; the scorer now finds the failing row, so bad_index is the swarm's smallest failing row."""
+    res = _spawn(_injected_notpd_worker, 3, timeout=120)
+    for rank, ok, bad in res:
+        assert ok == [0.0, 2.0, 4.0, 6.0, 8.0, 12.0, 14.0, 18.0, 18.0, 18.0]
+        assert bad == 5, rank
+
+
 def _gpu_worker(rank, world, port, path, k, q):
     """One rank; every rank scores its shard with gpf_eval_batch_sharded on GPU 0 (the host
     transport: RCCL needs one GPU per rank, the driver's 8-GPU run covers it)."""

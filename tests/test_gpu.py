@@ -274,12 +274,16 @@ def test_chunked_batches_equal_single_batch(f3, monkeypatch):
     np.testing.assert_array_equal(full, chunked)
 
 
-def test_predict_buffer_reuse_across_calls():
+@pytest.mark.parametrize("keep_mb", [None, "0"])
+def test_predict_buffer_reuse_across_calls(monkeypatch, keep_mb):
     """gpf_predict keeps its query-chunk buffers in the context between calls (grow-only): a
     call after a larger one runs with a smaller leading dimension inside the bigger buffers, a
     call after set_data with another N reallocates. Every result equals that of a fresh context
-    bit for bit."""
+    bit for bit. With GPF_PREDICT_KEEP_MB=0 (buffers larger than the bound are freed at the end
+    of each call, so a huge batch cannot pin HBM) the results are the same."""
     import gpfit
+    if keep_mb is not None:
+        monkeypatch.setenv("GPF_PREDICT_KEEP_MB", keep_mb)
     rng = np.random.default_rng(17)
     datasets = []
     for N, d in ((300, 2), (700, 3)):
