@@ -383,11 +383,14 @@ struct DiagSmem {
 // Lt/Ut: top-left of the block in the particle's L / U buffers (row stride ld);
 // yseg: the block's 128 RHS entries (replaced by z); s2o/szo: 128 partial outputs.
 // ----------------------------------------------------------------------------
+// pub (the early diagonal factor, WT = true): the per-particle flag to set to pub_val once U_JJ
+// and z_J — all a tile of the launch reads — are stored (write-through) and drained; the column
+// partials of the block (read only after the launch) are formed after the flag ("early publish").
 template <bool WT = false>
 __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __restrict__ Ut, size_t ld,
                                           double* __restrict__ yseg, double* __restrict__ s2o,
                                           double* __restrict__ szo, int* __restrict__ info, const DiagSmem& sm,
-                                          bool pad2) {
+                                          bool pad2, int* pub = nullptr, int pub_val = 0) {
   const int tid = threadIdx.x;
   const Quad<64> qd;
   double* const t0 = sm.t0;
@@ -429,6 +432,11 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
       gst<WT>(&yseg[tid], (tid < H) ? sm.z[tid] : 0.0);
     }
     if (bad && tid == 0 && *info == 0) *info = 1;
+    if (pub) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(pub, pub_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     return;
   }
 
@@ -486,6 +494,12 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
   DIAG_STAMP(7);
   // (f) forward substitution: z2 = U22 (y2 - L21 z1) (y2 already reduced in (c))
   rows_dot64(sm.z + H, t1, LDH, sm.y + H, sm.scratch, false);
+  if (pub) {  // early publish: U_JJ (stored write-through above) and z_J are complete
+    if (tid < T) gst<WT>(&yseg[tid], sm.z[tid]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's U_JJ and z_J stores drained
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(pub, pub_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   DIAG_STAMP(8);
   // (g) partials: columns 0..63 get the U21 rows, columns 64..127 the U22 rows
   cols_partial64(sm.ps2, sm.psz, t0, LDH, sm.z + H, sm.scratch);
@@ -493,7 +507,7 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
   if (tid < T) {
     s2o[tid] = sm.ps2[tid];
     szo[tid] = sm.psz[tid];
-    gst<WT>(&yseg[tid], sm.z[tid]);
+    if (!pub) gst<WT>(&yseg[tid], sm.z[tid]);
   }
   if (bad && tid == 0 && *info == 0) *info = 1;
   DIAG_STAMP(9);
@@ -1020,6 +1034,24 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
 #endif
   int p, w, sidx;
   const int role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, SPLIT != SPLIT_ALL && sy, p, w, sidx);
+#ifdef GPF_CHECK
+  // diagnostic build (-DGPF_CHECK): every index the workgroup derives its addresses from, checked
+  // against the launch's extents before any access (an out-of-range role prints and does nothing)
+  {
+    bool ok = p >= 0 && p < P && J >= 0 && J < nt && Npad == nt * T && S >= 1;
+    if (role == ROLE_SYRK) ok = ok && w == -1 && J >= 1 && J <= nt - 2 && yflag != nullptr;
+    else if (role == ROLE_DIAG) ok = ok && w == -1 && ED && dflag != nullptr;
+    else if (role != ROLE_IDLE) ok = ok && w >= 0 && w < nt - 1 && sidx >= 0 && sidx < S &&
+                                     (role != ROLE_PIECE || (part != nullptr && cnt != nullptr && S > 1)) &&
+                                     (w >= nt - 1 - J || J + 1 + w < nt) && (w < nt - 1 - J || w - (nt - 1 - J) < J);
+    if (!ok) {
+      if (tid == 0)
+        printf("k_step check: J=%d block %d role %d p=%d w=%d sidx=%d (P=%d nt=%d S=%d)\n", J, (int)blockIdx.x, role,
+               p, w, sidx, P, nt, S);
+      return;
+    }
+  }
+#endif
   if (SPLIT != SPLIT_ALL && role == ROLE_SYRK) {
     syrk_item(J, p, Npad, Lb, yflag, lds);
   } else if (ED && role == ROLE_DIAG) {
@@ -1031,11 +1063,9 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
 #if GPF_DIAG_PRIO
     __builtin_amdgcn_s_setprio(3);  // the launch's tiles wait for this block
 #endif
+    // publishes block J (dflag[p] = J) as soon as U_JJ and z_J are stored, before its partials
     factor128<true>(Lb + off, Ub + off, ld, yb + (size_t)p * Npad + J * T, s2p + poff, szp + poff, info + p,
-                    carve_diag(lds, lds + DIAG_BASE), J * T + H >= N);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(dflag + p, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    carve_diag(lds, lds + DIAG_BASE), J * T + H >= N, dflag + p, J);
   } else {
     step_item<SPLIT, ED>(role, J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, sidx, part, cnt, &sflag,
                          dflag, yflag, defer, spins, lds);

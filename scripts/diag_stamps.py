@@ -4,13 +4,12 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ["GPFIT_LIB"] = os.path.join(ROOT, "gaussian-process_amd", os.environ.get("STAMPS_LIB", "libgpfit_stamps.so"))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "gaussian-process_amd")]
-import torch  # noqa
 import gpfit
 from oracle import ref_cpu
 ctx = gpfit.Context(0)
 names = ["factor64 #1", "store L11/U11, z1, partials", "L21 = A21 U11^T", "syrk, y2, T", "factor64 #2",
          "store L22/U22", "U21 = -U22 T", "z2", "partials + out"]
-for N, P in [(128, 1), (128, 64), (4096, 64)]:
+for N, P in [(int(a), int(b)) for a, b in (c.split("x") for c in os.environ.get("CFGS", "128x1,1024x32,4096x1").split(","))]:
     rng = np.random.default_rng(0)
     x = rng.uniform(size=(3, N)); y = np.sin(6 * x[0]); e = np.full(N, 0.1)
     lo, hi = ref_cpu.search_bounds(x); s, ex = ref_cpu.sigma_grid()
