@@ -84,14 +84,33 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// 1/sqrt(p) for the pivots of the diagonal factor: v_rsq_f64 and two Newton steps
-// (y += y (1/2 - p/2 y^2)), a ~9-op dependent chain instead of the ~25 of a
-// correctly rounded sqrt followed by a division; within a few ulp of 1/sqrt(p).
+// Barrier for LDS-only hand-offs between the waves of the diagonal factor: every wave's LDS
+// operations retired, then s_barrier (the asm's memory clobber keeps the compiler from moving
+// memory operations across it). Unlike __syncthreads() (a workgroup-scope release fence) it does
+// not wait for the wave's outstanding global stores, so the L/U tile stores of the factor drain
+// behind its LDS phases instead of stalling every barrier. GPF_LSYNC=0: __syncthreads().
+#ifndef GPF_LSYNC
+#define GPF_LSYNC 1
+#endif
+__device__ __forceinline__ void lsync() {
+#if GPF_LSYNC
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+  __syncthreads();
+#endif
+}
+
+// 1/sqrt(p) for the pivots of the diagonal factor: v_rsq_f64 and GPF_RSQ_NEWTON Newton steps
+// (y += y (1/2 - p/2 y^2)), a short dependent chain instead of the ~25 ops of a correctly
+// rounded sqrt followed by a division; within a few ulp of 1/sqrt(p).
+#ifndef GPF_RSQ_NEWTON
+#define GPF_RSQ_NEWTON 2
+#endif
 __device__ __forceinline__ double rsqrt_nr(double p) {
   double y = __builtin_amdgcn_rsq(p);
   const double h = 0.5 * p;
 #pragma unroll
-  for (int it = 0; it < 2; ++it) {
+  for (int it = 0; it < GPF_RSQ_NEWTON; ++it) {
     const double t = fma(-(h * y), y, 0.5);
     y = fma(y, t, y);
   }
@@ -190,7 +209,7 @@ __device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx,
   }
   bool bad = false;
   double v[PW], w[PW];  // panel wave: the current panel (L columns by row lane, X rows by column lane)
-  __syncthreads();
+  lsync();
   if (wave == 0) {
     const int l = lane;
     const d2 p01 = *reinterpret_cast<const d2*>(strip + l * PW);
@@ -204,7 +223,7 @@ __device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx,
   for (int k = 0; k < 64 / PW; ++k) {
     const int cb = k * PW, ce = cb + PW, pc = cb / 16;
     if (k == 4) DIAG_STAMP(10);
-    __syncthreads();
+    lsync();
     if (k == 4) DIAG_STAMP(11);
     const double* pk = pout + (k & 1) * 64 * PW;
     if (wave == 0) {
@@ -236,6 +255,8 @@ __device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx,
         if (k == 4) DIAG_STAMP(13);
       }
     } else {
+      if (k == 4) DIAG_STAMP_T(20, 64);  // update wave 1 after the barrier
+      if (k == 4) DIAG_STAMP_T(24, 448);  // update wave 7 after the barrier
       // rank-4 updates with one MFMA per owned live block (A operand staged negated):
       //   A(bi,bj), bj >= pc:          C -= L[rows][cb..] L[cols][cb..]^T
       //   X(bi,bj), bi >= pc >= bj:    C -= L[rows > cb+3][cb..] X[cb..][cols <= cb+3]
@@ -289,9 +310,11 @@ __device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx,
           }
         }
       }
+      if (k == 4) DIAG_STAMP_T(21, 64);
+      if (k == 4) DIAG_STAMP_T(25, 448);
     }
   }
-  __syncthreads();
+  lsync();
   // outputs: X blocks from their owners, zeros above the diagonal of X (wave 0) and of L
 #pragma unroll
   for (int j = 0; j < NS; ++j) {
@@ -335,12 +358,12 @@ __device__ __forceinline__ void rows_dot64(double* out, const double* s1, int l1
   double acc = 0.0;
   for (int c = q * 8; c < q * 8 + 8; ++c) acc = fma(s1[r * l1 + c], v1[c], acc);
   scratch[q * 64 + r] = acc;
-  __syncthreads();
+  lsync();
   if (tid < 64) {
     const double s = sum8(scratch, tid);
     out[tid] = accumulate ? out[tid] - s : s;
   }
-  __syncthreads();
+  lsync();
 }
 
 // Column partials of a 64x64 LDS tile s (rows r, cols c): s2[c] += sum_r s^2,
@@ -356,13 +379,13 @@ __device__ __forceinline__ void cols_partial64(double* s2, double* sz, const dou
     az = fma(v, z[r], az);
   }
   scratch[q * 64 + c] = a2;
-  __syncthreads();
+  lsync();
   if (tid < 64) s2[tid] = s2[tid] + sum8(scratch, tid);
-  __syncthreads();
+  lsync();
   scratch[q * 64 + c] = az;
-  __syncthreads();
+  lsync();
   if (tid < 64) sz[tid] = sz[tid] + sum8(scratch, tid);
-  __syncthreads();
+  lsync();
 }
 
 struct DiagSmem {
@@ -404,9 +427,9 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
     sm.ps2[tid] = 0.0;
     sm.psz[tid] = 0.0;
   }
-  __syncthreads();
+  lsync();
   bool bad = factor64(t0, LDH, t1, LDH, sm.scratch);
-  __syncthreads();
+  lsync();
   DIAG_STAMP(1);
   lds_to_tile64(Lt, ld, t0, LDH, true);
   zero_tile64(Lt + H, ld);
@@ -441,18 +464,22 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
   }
 
   DIAG_STAMP(2);
-  // (b) L21 = A21 U11^T
+  // (b) L21 = A21 U11^T; A22 is read into registers now, so its load runs behind (b) and (c)
+  double* U21 = Ut + (size_t)H * ld;
+  const double* A22 = Lt + (size_t)H * ld + H;
+  Acc<64> a22;
+  a22.load(qd, A22, ld);
   tile64_to_lds(t0, LDH, Lt + (size_t)H * ld, ld);
-  __syncthreads();
+  lsync();
   Acc<64> acc;
   acc.zero();
   gemm_lds64<false, TRI_B_KLEC>(acc, t0, LDH, t1, LDH, qd);  // U11^T is upper triangular
-  __syncthreads();
+  lsync();
   acc.foreach(qd, [&](int r, int c, double v) {
       t0[r * LDH + c] = v;
       Lt[(size_t)(H + r) * ld + c] = v;
     });
-  __syncthreads();
+  lsync();
 
   DIAG_STAMP(3);
   // (c) A22 -= L21 L21^T ; y2 -= L21 z1 ; T = L21 U11 (to the U21 slot as scratch)
@@ -462,34 +489,51 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
   Acc<64> tt;
   tt.zero();
   gemm_lds64<true, TRI_B_KGEC>(tt, t0, LDH, t1, LDH, qd);  // U11 is lower triangular
-  __syncthreads();
-  double* U21 = Ut + (size_t)H * ld;
-  const double* A22 = Lt + (size_t)H * ld + H;
+  lsync();
   tt.foreach(qd, [&](int r, int c, double v) { gst<WT>(&U21[(size_t)r * ld + c], v); });
-  acc.foreach(qd, [&](int r, int c, double v) { t0[r * LDH + c] = A22[(size_t)r * ld + c] - v; });
-  __syncthreads();
+#pragma unroll
+  for (int mi = 0; mi < Acc<64>::MBR; ++mi)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc.v[mi][0][e] = a22.v[mi][0][e] - acc.v[mi][0][e];
+  acc.foreach(qd, [&](int r, int c, double v) { t0[r * LDH + c] = v; });
+  lsync();
 
   DIAG_STAMP(4);
   // (d) L22, U22
   bad = factor64(t0, LDH, t1, LDH, sm.scratch) | bad;
-  __syncthreads();
+  lsync();
   DIAG_STAMP(5);
+  // T (stored to the U21 slot in (c), long drained: the factor ran since) read back into
+  // registers first, so the loads run behind the stores of L22 and U22
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  d2 tv[2048 / DNTH];
+#pragma unroll
+  for (int u = 0; u < 2048 / DNTH; ++u) {
+    const int q = tid + DNTH * u, row = q >> 5, c2 = q & 31;
+    tv[u] = *reinterpret_cast<const d2*>(U21 + (size_t)row * ld + 2 * c2);
+  }
   lds_to_tile64(Lt + (size_t)H * ld + H, ld, t0, LDH, true);
   lds_to_tile64<WT>(Ut + (size_t)H * ld + H, ld, t1, LDH, false);
-  __syncthreads();
+  lsync();
 
   DIAG_STAMP(6);
   // (e) U21 = -U22 T
-  tile64_to_lds(t0, LDH, U21, ld);
-  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 2048 / DNTH; ++u) {
+    const int q = tid + DNTH * u, row = q >> 5, c2 = q & 31;
+    t0[row * LDH + 2 * c2] = tv[u].x;
+    t0[row * LDH + 2 * c2 + 1] = tv[u].y;
+  }
+  lsync();
   acc.zero();
   gemm_lds64<true, TRI_A_KLER>(acc, t1, LDH, t0, LDH, qd);  // U22 is lower triangular
-  __syncthreads();
+  lsync();
   acc.foreach(qd, [&](int r, int c, double v) {
       t0[r * LDH + c] = -v;
       gst<WT>(&U21[(size_t)r * ld + c], -v);
     });
-  __syncthreads();
+  lsync();
 
   DIAG_STAMP(7);
   // (f) forward substitution: z2 = U22 (y2 - L21 z1) (y2 already reduced in (c))

@@ -24,6 +24,7 @@ for N, P in [(int(a), int(b)) for a, b in (c.split("x") for c in os.environ.get(
     p = np.array(buf[10:14], dtype=np.float64)
     if p.any(): print(f"    iteration k=4 (last factor64, wave 0): barrier {p[1]-p[0]:.0f}, strip read+update {p[2]-p[1]:.0f}, "
           f"factor panel {p[3]-p[2]:.0f}")
-    u = np.array(buf[20:23], dtype=np.float64)
-    if u.any(): print(f"    iteration k=4 wave 7: loads+mfma {u[1]-u[0]:.0f}, finish+strips {u[2]-u[1]:.0f}; "
-                      f"wave 7 start vs wave 0 after-barrier {u[0]-p[1]:.0f}")
+    u = np.array(buf[20:26], dtype=np.float64)
+    if u.any():
+        print(f"    iteration k=4 update wave 1: work {u[1]-u[0]:.0f} (starts {u[0]-p[1]:+.0f} vs wave 0 after the barrier); "
+              f"wave 7: work {u[5]-u[4]:.0f} (starts {u[4]-p[1]:+.0f})")
