@@ -79,6 +79,19 @@ def pmc_traffic(N, d, swarm):
     return best
 
 
+def secondary_pmc():
+    """rocprofv3 PMC summary of the secondary kernels from the latest committed
+    profiles/<round>/secondary_pmc.json (scripts/gpu_r3_secondary.sh + scripts/pmc_secondary.py,
+    the bench's own secondary calls), or None."""
+    best = None
+    for f in sorted((ROOT / "profiles").glob("*/secondary_pmc.json")):
+        try:
+            best = (json.loads(f.read_text()), str(f.relative_to(ROOT)))
+        except (OSError, ValueError):
+            continue
+    return best
+
+
 def synthetic(N, d, seed, hetero=False):
     """x ~ U[0,1)^d, y = sum_k sin(2 pi x_k) + 0.1 N(0,1), e = 0.1."""
     rng = np.random.default_rng(seed)
@@ -187,6 +200,8 @@ def predict_line(ctx, x, y, e, N, d, args):
            if prof["predict_ms"] > 0 else None,
            "k_cross_cov_GBps": prof["predict_cov_bytes"] / (prof["predict_cov_ms"] * 1e-3) / 1e9
            if prof["predict_cov_ms"] > 0 else None,
+           "k_cross_cov_hbm_frac": prof["predict_cov_bytes"] / (prof["predict_cov_ms"] * 1e-3) / 8e12
+           if prof["predict_cov_ms"] > 0 else None,
            "note": "wall time (median of 3 calls) includes the single-particle factorisation and host<->device copies"}
     if not args.no_cpu and args.cpu_predict_points > 0:
         from oracle import ref_cpu  # CPU baseline leg only
@@ -250,7 +265,17 @@ def psurf_line(ctx, args):
            "rows_per_s_kernel": M / (kms * 1e-3) if kms > 0 else None, "rows_per_s_wall": M / dt,
            "kernel_GBps": prof["psurf_bytes"] / (kms * 1e-3) / 1e9 if kms > 0 else None,
            "hbm_peak_GBps": 8000.0,
-           "note": "wall includes host<->device copies of the tails and of y, p (PCIe)"}
+           "note": "wall includes host<->device copies of the tails and of y, p (PCIe); kernel = row setup + "
+                   "grid/probability kernel"}
+    pmc = secondary_pmc()
+    if pmc and pmc[0].get("k_prob_surf", {}).get("valu_busy_pct"):
+        # VALU roofline: the kernels issue erf/erfc and division sequences, not HBM traffic; frac
+        # = the fraction of cycles the vector ALUs were issuing (rocprofv3 PMC of the same call)
+        k = pmc[0]["k_prob_surf"]
+        out["roofline"] = {"bound": "valu", "frac": k["valu_busy_pct"] / 100.0,
+                           "achieved_fp64_TFLOPs": k.get("fp64_tflops"), "valu_insts_per_simd": k.get("valu_insts_per_simd"),
+                           "kernel_ns": k.get("avg_ns"), "source": pmc[1],
+                           "note": "frac = SQ_ACTIVE_INST_VALU x 4 / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8 XCDs)"}
     if not args.no_cpu:
         from oracle import ref_cpu  # CPU baseline leg only
         m = 2000

@@ -95,23 +95,29 @@ __global__ __launch_bounds__(NTHR) void k_build_cov(int N, int Npad, int d, cons
 
 // Rectangular cross-covariance kernel_func(x1, x2, l) (no noise) into
 // out[i*ldo + j] for i < R, j < C; entries with i >= N1 or j >= N2 are 0.
-// One workgroup per 64 x 256 output block: the scaled coordinates and squared norms of its 64
-// rows and 256 columns are staged once in LDS (dynamic: d x 320 + 320 doubles), then every lane
-// writes 64 outputs, a wave covering 64 consecutive columns of one row (512 contiguous bytes;
-// 4 waves = one 2 KiB row segment). A write-bound kernel (8 B per output) once the exponential
-// per output is spread over enough resident waves: the LDS is sized by d, not DMAX.
-// grid: (ceil(C/256), ceil(R/64)), dynamic LDS cross_cov_lds(d) bytes
-constexpr int CC_R = 64, CC_C = 256;
+// One workgroup per CC_R x 256 output block: the scaled coordinates and squared norms of its
+// rows and 256 columns are staged once in LDS (dynamic: d x (CC_R + 256) + CC_R + 256 doubles),
+// then every lane keeps its column's coordinates in registers and writes CC_R outputs, a wave
+// covering 64 consecutive columns of one row (512 contiguous bytes; 4 waves = one 2 KiB row
+// segment). Write-bound (8 B per output) once the exponential per output is spread over enough
+// resident waves. D: the dimension as a template constant (1..4; 0 = any d <= DMAX at run time).
+// grid: (ceil(C/256), ceil(R/CC_R)), dynamic LDS cross_cov_lds(d) bytes
+#ifndef GPF_CC_R
+#define GPF_CC_R 32
+#endif
+constexpr int CC_R = GPF_CC_R, CC_C = 256;
 __host__ __device__ constexpr size_t cross_cov_lds(int d) { return (size_t)(d + 1) * (CC_R + CC_C) * 8; }
-__global__ __launch_bounds__(NTHR) void k_cross_cov(int N1, int N2, int R, int C, int d,
+template <int D>
+__global__ __launch_bounds__(NTHR) void k_cross_cov(int N1, int N2, int R, int C, int dd,
                                                     const double* __restrict__ x1, int ld1,
                                                     const double* __restrict__ x2, int ld2,
                                                     const double* __restrict__ l, double* __restrict__ out,
                                                     int64_t ldo) {
+  const int d = D > 0 ? D : dd;
   extern __shared__ double cc_lds[];
-  double* ai = cc_lds;                  // [d][64]
+  double* ai = cc_lds;                  // [d][CC_R]
   double* aj = ai + (size_t)d * CC_R;   // [d][256]
-  double* ni = aj + (size_t)d * CC_C;   // [64]
+  double* ni = aj + (size_t)d * CC_C;   // [CC_R]
   double* nj = ni + CC_R;               // [256]
   const int tid = threadIdx.x;
   const int bi = blockIdx.y, bj = blockIdx.x;
@@ -138,8 +144,12 @@ __global__ __launch_bounds__(NTHR) void k_cross_cov(int N1, int N2, int R, int C
   const int c = tid & (CC_C - 1);  // this lane's column (the 4 waves cover 256 consecutive ones)
   const int gj = bj * CC_C + c;
   if (gj >= C) return;
-  const double* bcol = aj + c;  // column coordinates, stride CC_C
+  constexpr int DR = D > 0 ? D : DMAX;
+  double bc[DR];  // the column's scaled coordinates
+#pragma unroll
+  for (int k = 0; k < DR; ++k) bc[k] = (k < d) ? aj[k * CC_C + c] : 0.0;
   const double nc = nj[c];
+  const bool colok = gj < N2;
   double* op = out + gj;
   const int r0 = bi * CC_R;
   const int rmax = min(CC_R, R - r0);
@@ -147,14 +157,34 @@ __global__ __launch_bounds__(NTHR) void k_cross_cov(int N1, int N2, int R, int C
   for (int r = 0; r < rmax; ++r) {
     const int gi = r0 + r;
     double v = 0.0;
-    if (gi < N1 && gj < N2) {
-      double dot = ai[r] * bcol[0];
-      for (int k = 1; k < d; ++k) dot = fma(ai[k * CC_R + r], bcol[k * CC_C], dot);
+    if (gi < N1 && colok) {
+      double dot = ai[r] * bc[0];
+#pragma unroll
+      for (int k = 1; k < DR; ++k)
+        if (k < d) dot = fma(ai[k * CC_R + r], bc[k], dot);
       double r2 = (ni[r] + nc) - 2.0 * dot;
       r2 = r2 > 0.0 ? r2 : 0.0;
       v = exp(-0.5 * r2);
     }
+#if GPF_CC_NT
+    __builtin_nontemporal_store(v, op + (size_t)gi * ldo);
+#else
     op[(size_t)gi * ldo] = v;
+#endif
+  }
+}
+
+// k_cross_cov for dimension d on `stream` (grid and LDS as above)
+inline void launch_cross_cov(hipStream_t stream, int N1, int N2, int R, int C, int d, const double* x1, int ld1,
+                             const double* x2, int ld2, const double* l, double* out, int64_t ldo) {
+  const dim3 grid((unsigned)((C + CC_C - 1) / CC_C), (unsigned)((R + CC_R - 1) / CC_R));
+  const size_t lds = cross_cov_lds(d);
+  switch (d) {
+    case 1: hipLaunchKernelGGL(k_cross_cov<1>, grid, dim3(NTHR), lds, stream, N1, N2, R, C, d, x1, ld1, x2, ld2, l, out, ldo); break;
+    case 2: hipLaunchKernelGGL(k_cross_cov<2>, grid, dim3(NTHR), lds, stream, N1, N2, R, C, d, x1, ld1, x2, ld2, l, out, ldo); break;
+    case 3: hipLaunchKernelGGL(k_cross_cov<3>, grid, dim3(NTHR), lds, stream, N1, N2, R, C, d, x1, ld1, x2, ld2, l, out, ldo); break;
+    case 4: hipLaunchKernelGGL(k_cross_cov<4>, grid, dim3(NTHR), lds, stream, N1, N2, R, C, d, x1, ld1, x2, ld2, l, out, ldo); break;
+    default: hipLaunchKernelGGL(k_cross_cov<0>, grid, dim3(NTHR), lds, stream, N1, N2, R, C, d, x1, ld1, x2, ld2, l, out, ldo); break;
   }
 }
 

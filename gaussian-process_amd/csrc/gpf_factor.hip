@@ -29,7 +29,15 @@ namespace gpf {
 #ifdef GPF_DIAG_STAMPS
 // Diagnostic build only (-DGPF_DIAG_STAMPS): thread 0 of workgroup 0 records s_memtime at
 // phase boundaries of factor128 into a buffer nothing else reads.
-__device__ unsigned long long g_diag_stamps[32];
+// [0, 32): factor128 phases and the k = 4 details; [32, 32 + 16 * 16): per panel k of the last
+// factor64 call, slot 16 k + s: s < 8 wave s arriving at the panel barrier, 8 wave 0 leaving it,
+// 9 wave 0 after its strip update, 10 wave 0 after its panel factor, 11-13 update wave
+// DIAG_UW after its block slot j, 14 wave DIAG_UW leaving the barrier
+#ifndef DIAG_UW
+#define DIAG_UW 4
+#endif
+constexpr int DIAG_NSTAMPS = 32 + 16 * 16;
+__device__ unsigned long long g_diag_stamps[DIAG_NSTAMPS];
 #define DIAG_STAMP(i) DIAG_STAMP_T(i, 0)
 #define DIAG_STAMP_T(i, thr)                                                                       \
   do {                                                                                           \
@@ -223,8 +231,11 @@ __device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx,
   for (int k = 0; k < 64 / PW; ++k) {
     const int cb = k * PW, ce = cb + PW, pc = cb / 16;
     if (k == 4) DIAG_STAMP(10);
+    DIAG_STAMP_T(32 + 16 * k + wave, 64 * wave);
     lsync();
     if (k == 4) DIAG_STAMP(11);
+    DIAG_STAMP_T(32 + 16 * k + 8, 0);
+    DIAG_STAMP_T(32 + 16 * k + 14, 64 * DIAG_UW);
     const double* pk = pout + (k & 1) * 64 * PW;
     if (wave == 0) {
       if (ce < 64) {
@@ -251,8 +262,10 @@ __device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx,
           w[q] = wn[q];
         }
         if (k == 4) DIAG_STAMP(12);
+        DIAG_STAMP_T(32 + 16 * k + 9, 0);
         f64_factor_panel(v, w, l, cn, sA, la, pout + ((k + 1) & 1) * 64 * PW, bad);
         if (k == 4) DIAG_STAMP(13);
+        DIAG_STAMP_T(32 + 16 * k + 10, 0);
       }
     } else {
       if (k == 4) DIAG_STAMP_T(20, 64);  // update wave 1 after the barrier
@@ -309,6 +322,7 @@ __device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx,
             sb[bcol * PW + lk] = xv;
           }
         }
+        DIAG_STAMP_T(32 + 16 * k + 11 + j, 64 * DIAG_UW);
       }
       if (k == 4) DIAG_STAMP_T(21, 64);
       if (k == 4) DIAG_STAMP_T(25, 448);
@@ -649,8 +663,26 @@ enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2, ROLE_DIAG = 3, ROLE_SYRK =
 // touch no diagonal block. Same MFMAs in the same order per element of A_II: bitwise the
 // per-launch look-ahead's values.
 
+// Balanced all-tile split (SPLIT_ALL): tile w of launch J is cut into pieces of about `tgt` 16-deep
+// chunks each (the host picks tgt per launch so that the launch fills the CUs once), so every
+// piece — the critical tile's included — does about the same work, instead of a fixed number of
+// pieces per tile (which gave the deepest tiles the longest pieces: the critical tile's GEMM, not
+// the diagonal factor, ended the launch). At most SPLIT_MAXS pieces (the reduction tree's bound).
+constexpr int SPLIT_MAXS = 32;
+__host__ __device__ __forceinline__ int split_all_chunks(int J, int w, int nt) {
+  const int nL = nt - 1 - J;
+  return (w < nL ? J : J - (w - nL)) * (T / DL_KC);  // L tile: depth 128J; U tile K: 128(J-K)
+}
+__host__ __device__ __forceinline__ int split_all_pieces(int J, int w, int nt, int tgt) {
+  const int ch = split_all_chunks(J, w, nt);
+  const int s = ch <= 0 ? 1 : (ch + tgt - 1) / tgt;
+  return s > SPLIT_MAXS ? SPLIT_MAXS : s;
+}
+
 // Workgroup b of a k_step<SPLIT> launch (grid: [P diagonal workgroups if ed] + [P SYRK workgroups
-// if sy] + P*(nt-1)*S for SPLIT_ALL, P*(nt-1) + P*(S-1) for SPLIT_CRIT, P*(nt-1) otherwise): its
+// if sy] + P * sum_w split_all_pieces(J, w, nt, S) for SPLIT_ALL (tiles in order w = 0, 1, ..:
+// the critical tile first, then the L tiles, then the U tiles deepest first; pieces particle-
+// fastest), P*(nt-1) + P*(S-1) for SPLIT_CRIT, P*(nt-1) otherwise): its
 // particle p, tile w, split index sidx, and whether it factors the diagonal block (ROLE_DIAG,
 // w = -1), reduces the next diagonal block (ROLE_SYRK, w = -1), runs the whole tile, one depth
 // range (piece sidx of S) of it, or nothing. The kernel and the host-side plan check
@@ -676,9 +708,17 @@ __host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt,
     }
     b -= P;
   }
-  if (SPLIT == SPLIT_ALL) {
-    sidx = b / tiles;  // split-major dispatch
-    step_tile(b - sidx * tiles, P, nt - 1, grp, p, w);
+  if (SPLIT == SPLIT_ALL) {  // S: chunks per piece
+    int np = 1;
+    for (w = 0; w < nt - 2; ++w) {
+      np = split_all_pieces(J, w, nt, S);
+      if (b < P * np) break;
+      b -= P * np;
+    }
+    if (w == nt - 2) np = split_all_pieces(J, w, nt, S);
+    p = b % P;
+    sidx = b / P;  // (< np for every dispatched workgroup: gpf_plan_check)
+    return np > 1 ? ROLE_PIECE : ROLE_WHOLE;
   } else if (SPLIT == SPLIT_CRIT && b < P * S) {  // the S pieces of the critical tiles
     p = b % P;
     w = 0;
@@ -689,10 +729,9 @@ __host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt,
   const bool ltile = w < nt - 1 - J;
   if (ltile) {
     // L tiles split their depth-128J GEMM (only with the K tiles fused into k_step)
-    if (GPF_KFUSE && (SPLIT == SPLIT_ALL || (SPLIT == SPLIT_CRIT && w == 0)) && J > 0) return ROLE_PIECE;
+    if (GPF_KFUSE && SPLIT == SPLIT_CRIT && w == 0 && J > 0) return ROLE_PIECE;
     return (SPLIT != SPLIT_NONE && sidx > 0) ? ROLE_IDLE : ROLE_WHOLE;  // nothing to split at J = 0
   }
-  if (SPLIT == SPLIT_ALL) return ROLE_PIECE;
   return (SPLIT == SPLIT_CRIT && sidx > 0) ? ROLE_IDLE : ROLE_WHOLE;  // U tiles never split in CRIT
 }
 
@@ -711,6 +750,9 @@ static_assert(STEP_NTH == DNTH, "the fused diagonal runs on the step workgroup")
 #endif
 #ifndef GPF_WAVE_PRIO
 #define GPF_WAVE_PRIO 0  // build-time A/B knob
+#endif
+#ifndef GPF_CRIT_PRIO
+#define GPF_CRIT_PRIO 0  // wave priority of the critical tile's workgroups (I = J+1; 0 = off)
 #endif
 #ifndef GPF_STEP_WAVES_PER_SIMD
 #define GPF_STEP_WAVES_PER_SIMD 4  // 2 workgroups of 8 waves per CU
@@ -901,7 +943,7 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
                                           double* __restrict__ Ub, double* __restrict__ yb,
                                           double* __restrict__ s2p, double* __restrict__ szp,
                                           int* __restrict__ info, int N, const double* __restrict__ x,
-                                          const double* __restrict__ ls, int d, int S, int sidx,
+                                          const double* __restrict__ ls, int d, int S, int S2, int sidx,
                                           double* __restrict__ part, unsigned* __restrict__ cnt, int* sflag,
                                           const int* __restrict__ dflag, const int* __restrict__ yflag, int defer,
                                           int spins, double* lds) {
@@ -928,9 +970,11 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
     if (SPLIT != SPLIT_NONE && role == ROLE_PIECE) {
       // split-K: partial GEMMs, the last workgroup to arrive finishes the tile; piece 0 seeds
       // its partial with the covariance tile (the unsplit path's accumulator seed)
-      double* pt = part + (size_t)(p * (nt - 1) + w) * S * T * T;
+      // (S2 partial slots per tile; the all-tile split's pieces per tile from the chunk target S)
+      double* pt = part + (size_t)(p * (nt - 1) + w) * S2 * T * T;
+      const int Sx = SPLIT == SPLIT_ALL ? split_all_pieces(J, w, nt, S) : S;
       if (!split_part<false, true, true>(acc, Lp + (size_t)J * T * ld, Npad, Lp + (size_t)I * T * ld, Npad,
-                                         J * T / DL_KC, S, sidx, pt, cnt + (size_t)(p * (nt - 1) + w) * SPLIT_CNT, lds,
+                                         J * T / DL_KC, Sx, sidx, pt, cnt + (size_t)(p * (nt - 1) + w) * SPLIT_CNT, lds,
                                          qd, sflag, [&](Acc<T>& a) { cov_tile_acc(a, qd, x, lp, d, N, J, I, lds); }))
         return;  // (the finisher's accumulators hold D)
     } else {
@@ -992,9 +1036,10 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
     Acc<T> acc;
     // W = L_J,[K,J) U_[K,J),K (U_KK is lower triangular: the wave's first chunks add zeros)
     if (SPLIT == SPLIT_ALL && role == ROLE_PIECE) {  // split-K (the triangular first block runs dense: its upper part holds zeros)
-      double* pt = part + (size_t)(p * (nt - 1) + w) * S * T * T;
+      double* pt = part + (size_t)(p * (nt - 1) + w) * S2 * T * T;
+      const int Sx = split_all_pieces(J, w, nt, S);
       if (!split_part<true, false, false>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
-                                          Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T / DL_KC, S, sidx,
+                                          Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T / DL_KC, Sx, sidx,
                                           pt, cnt + (size_t)(p * (nt - 1) + w) * SPLIT_CNT, lds, qd, sflag,
                                           [](Acc<T>&) {}))
         return;
@@ -1056,7 +1101,7 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
                                                   double* __restrict__ s2p, double* __restrict__ szp,
                                                   int* __restrict__ info, int P, int grp, int N,
                                                   const double* __restrict__ x, const double* __restrict__ ls,
-                                                  int d, int S, double* __restrict__ part,
+                                                  int d, int S, int S2, double* __restrict__ part,
                                                   unsigned* __restrict__ cnt, int* __restrict__ dflag, int ed,
                                                   int* __restrict__ yflag, int defer, int sy, int spins) {
   const int tid = threadIdx.x;
@@ -1082,10 +1127,11 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
   // diagnostic build (-DGPF_CHECK): every index the workgroup derives its addresses from, checked
   // against the launch's extents before any access (an out-of-range role prints and does nothing)
   {
-    bool ok = p >= 0 && p < P && J >= 0 && J < nt && Npad == nt * T && S >= 1;
+    bool ok = p >= 0 && p < P && J >= 0 && J < nt && Npad == nt * T && S >= 1 && S2 >= 1 && S2 <= SPLIT_MAXS;
     if (role == ROLE_SYRK) ok = ok && w == -1 && J >= 1 && J <= nt - 2 && yflag != nullptr;
     else if (role == ROLE_DIAG) ok = ok && w == -1 && ED && dflag != nullptr;
-    else if (role != ROLE_IDLE) ok = ok && w >= 0 && w < nt - 1 && sidx >= 0 && sidx < S &&
+    else if (role != ROLE_IDLE) ok = ok && w >= 0 && w < nt - 1 && sidx >= 0 &&
+                                     sidx < (SPLIT == SPLIT_ALL ? split_all_pieces(J, w, nt, S) : S) && sidx < S2 &&
                                      (role != ROLE_PIECE || (part != nullptr && cnt != nullptr && S > 1)) &&
                                      (w >= nt - 1 - J || J + 1 + w < nt) && (w < nt - 1 - J || w - (nt - 1 - J) < J);
     if (!ok) {
@@ -1095,6 +1141,11 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
       return;
     }
   }
+#endif
+#if GPF_CRIT_PRIO
+  // the critical tile I = J+1 (its pieces too) ahead of co-resident tiles in issue arbitration:
+  // the next launch waits for it, the other tiles only for the launch boundary
+  if ((role == ROLE_WHOLE || role == ROLE_PIECE) && w == 0 && J + 1 < nt) __builtin_amdgcn_s_setprio(GPF_CRIT_PRIO);
 #endif
   if (SPLIT != SPLIT_ALL && role == ROLE_SYRK) {
     syrk_item(J, p, Npad, Lb, yflag, lds);
@@ -1111,7 +1162,7 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
     factor128<true>(Lb + off, Ub + off, ld, yb + (size_t)p * Npad + J * T, s2p + poff, szp + poff, info + p,
                     carve_diag(lds, lds + DIAG_BASE), J * T + H >= N, dflag + p, J);
   } else {
-    step_item<SPLIT, ED>(role, J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, sidx, part, cnt, &sflag,
+    step_item<SPLIT, ED>(role, J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, S2, sidx, part, cnt, &sflag,
                          dflag, yflag, defer, spins, lds);
   }
 #ifdef GPF_WG_TRACE

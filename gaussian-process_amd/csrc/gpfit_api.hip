@@ -92,6 +92,12 @@ struct gpf_ctx {
   double *p_xf = nullptr, *p_ks = nullptr, *p_vsq = nullptr, *p_mu = nullptr, *p_sd = nullptr;
   int64_t p_cols = 0, p_np = 0;
   int p_d = 0, p_nt = 0;
+  // gpf_prob_surface's row-chunk buffers, kept between calls like the prediction's
+  double *s_t = nullptr, *s_cmp = nullptr, *s_y = nullptr, *s_p = nullptr;
+  double4* s_info = nullptr;
+  int* s_ok = nullptr;
+  int64_t s_rows = 0;
+  int s_e = 0;
   int* d_hist = nullptr;
   // pinned host staging for the per-batch transfers (async DMA, capturable in graphs)
   double* h_ls = nullptr;
@@ -189,9 +195,28 @@ static void free_pred(gpf_ctx* c) {
   c->p_d = c->p_nt = 0;
 }
 
+static void free_psurf(gpf_ctx* c) {
+  hipFree(c->s_t); hipFree(c->s_cmp); hipFree(c->s_y); hipFree(c->s_p); hipFree(c->s_info); hipFree(c->s_ok);
+  c->s_t = c->s_cmp = c->s_y = c->s_p = nullptr;
+  c->s_info = nullptr;
+  c->s_ok = nullptr;
+  c->s_rows = 0;
+  c->s_e = 0;
+}
+
+// Device buffers of gpf_predict / gpf_prob_surface are kept for the next call unless larger
+// than GPF_PREDICT_KEEP_MB (default 2048): a one-off large call must not hold HBM that would
+// starve the next factorisation's or hull's allocations
+static double keep_bytes() {
+  double keep_mb = 2048.0;
+  if (const char* e = getenv("GPF_PREDICT_KEEP_MB")) keep_mb = atof(e);
+  return keep_mb * 1048576.0;
+}
+
 static void free_work(gpf_ctx* c) {
   clear_graphs(c);
   free_pred(c);
+  free_psurf(c);
   hipHostFree(c->h_ls); hipHostFree(c->h_loss); hipHostFree(c->h_info);
   c->h_ls = c->h_loss = nullptr;
   c->h_info = nullptr;
@@ -296,6 +321,40 @@ static int split_k(int tiles, int nt) {
   return S;
 }
 
+// Chunk target of launch J under the all-tile split (gpf::split_all_pieces): the launch's GEMM
+// depth (pc particles, every tile) spread over `slots` workgroups of about equal work, one per CU
+// (a slot per particle is kept for the diagonal workgroups — also without the early diagonal
+// factor, so that both schedules sum the same pieces and stay bitwise equal: a piece that shares
+// the diagonal factor's CU slows its dependent chain; two pieces per CU run at half rate each),
+// with pieces of at least
+// GPF_SPLIT_K_MINCH (4) 16-deep chunks. A fixed S pieces per tile (rounds 1-2) gave every tile
+// the same piece count, so the deepest tiles — the critical tile I = J+1 among them — had the
+// longest pieces and, from J ~ 10 on, ended the launch after the diagonal factor.
+// GPF_SPLIT_K_SLOTS overrides the workgroup budget (256).
+static int split_all_target(int pc, int nt, int J) {
+  int slots = 256, minch = 4;
+  if (const char* e = getenv("GPF_SPLIT_K_SLOTS")) slots = std::max(1, atoi(e));
+  if (const char* e = getenv("GPF_SPLIT_K_MINCH")) minch = std::max(1, atoi(e));
+  const int budget = std::max(1, slots - pc);
+  long long tot = 0;
+  for (int w = 0; w < nt - 1; ++w) tot += gpf::split_all_chunks(J, w, nt);
+  const int cap = std::max(1, J * T / gpf::DL_KC);  // every tile in one piece from here on
+  auto wgs = [&](int tgt) {
+    long long n = 0;
+    for (int w = 0; w < nt - 1; ++w) n += gpf::split_all_pieces(J, w, nt, tgt);
+    return pc * n;
+  };
+  // smallest target >= the even share whose pieces fit the budget (the count falls with tgt)
+  int lo = (int)std::min<long long>(cap, std::max<long long>(minch, (pc * tot + budget - 1) / budget)), hi = cap;
+  while (lo < hi) {
+    const int mid = (lo + hi) / 2;
+    if (wgs(mid) <= budget) hi = mid;
+    else lo = mid + 1;
+  }
+  const int tgt = lo;
+  return std::min(tgt, cap);
+}
+
 // Early diagonal factor (gpf::k_step<SPLIT, 1>, gpf_factor.hip) for factorisations whose launches
 // leave workgroup slots idle: there the launch time is the critical tile's chain, and moving the
 // diagonal factor of block J to the start of launch J, beside the GEMMs, takes it off that chain
@@ -387,6 +446,17 @@ static void split_sizes(int pc, int nt, int& S, int& Smax) {
   const int gmax = (pc + ng - 1) / ng;
   S = split_k(gmax * (nt - 1), nt);
   Smax = S;
+  if (S > 1) {  // the all-tile split: slots for the most pieces any tile gets
+    Smax = 1;
+    for (int g = 0; g < ng; ++g) {  // (the target depends on the group's particle count)
+      const int gc = (int)((long long)pc * (g + 1) / ng) - (int)((long long)pc * g / ng);
+      for (int J = 1; J < nt; ++J) {
+        const int tgt = split_all_target(gc, nt, J);
+        for (int w = 0; w < nt - 1; ++w) Smax = std::max(Smax, gpf::split_all_pieces(J, w, nt, tgt));
+      }
+    }
+    Smax = std::max(Smax, 2);
+  }
   for (int J = 1; S == 1 && J < nt; ++J) Smax = std::max(Smax, split_crit(pc, nt, J, step_group(gmax), S));
 }
 
@@ -400,7 +470,8 @@ static int split_plan(gpf_ctx* c, int pc, int& S, int& Smax) {
 // tile, and where its split-K partial slots and arrival counters start (element offsets into
 // d_part / d_cnt). run_factor launches exactly this list; gpf_plan_check verifies it on the host.
 struct StepLaunch {
-  int J, g, p0, gc, split, S, grp, ed;  // ed: the launch starts with gc diagonal workgroups
+  int J, g, p0, gc, split, S, S2, grp, ed;  // S: pieces per split tile (SPLIT_ALL: chunks per piece); S2: partial
+                                            // slots per tile; ed: the launch starts with gc diagonal workgroups
   int defer, sy;                        // deferred diagonal update; sy: gc SYRK workgroups follow
   unsigned grid;
   size_t part_off, cnt_off;
@@ -420,12 +491,15 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
       l.gc = (int)((long long)pc * (g + 1) / ng) - l.p0;
       l.grp = step_group(l.gc);
       const int Sc = split_crit(pc, nt, J, l.grp, S);
-      l.S = S > 1 ? S : Sc;  // pieces per split tile in this launch
+      l.S = S > 1 ? split_all_target(l.gc, nt, J) : Sc;
+      l.S2 = S > 1 ? Smax : l.S;
       l.split = S > 1 ? gpf::SPLIT_ALL : Sc > 1 ? gpf::SPLIT_CRIT : gpf::SPLIT_NONE;
       l.ed = ed ? 1 : 0;
       l.defer = (S == 1 && defer_syrk()) ? 1 : 0;  // the all-tile split keeps the per-tile look-ahead
       l.sy = (l.defer && J >= 1 && J <= nt - 2) ? 1 : 0;
-      l.grid = (S > 1 ? l.gc * (nt - 1) * S : l.gc * (nt - 1) + l.gc * (Sc - 1)) + (l.ed ? l.gc : 0) + (l.sy ? l.gc : 0);
+      int nall = 0;
+      for (int w = 0; S > 1 && w < nt - 1; ++w) nall += gpf::split_all_pieces(J, w, nt, l.S);
+      l.grid = (S > 1 ? l.gc * nall : l.gc * (nt - 1) + l.gc * (Sc - 1)) + (l.ed ? l.gc : 0) + (l.sy ? l.gc : 0);
       // one set of partial slots per group: groups run concurrently
       l.part_off = (size_t)l.p0 * (nt - 1) * Smax * T * T;
       l.cnt_off = (size_t)l.p0 * (nt - 1) * gpf::SPLIT_CNT;
@@ -521,7 +595,7 @@ static int run_factor(gpf_ctx* c, int pc) {
       hipLaunchKernelGGL(kern, dim3(l.grid), dim3(gpf::STEP_NTH), 0, st, l.J, nt, Np, c->d_L + (size_t)p0 * ld * ld,
                          c->d_U + (size_t)p0 * ld * ld, c->d_yb + (size_t)p0 * ld, c->d_s2p + (size_t)p0 * nt * ld,
                          c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc, l.grp, N, c->d_x,
-                         c->d_ls + (size_t)p0 * c->d, c->d, l.S, partg, cntg, c->d_flag + p0, l.ed,
+                         c->d_ls + (size_t)p0 * c->d, c->d, l.S, l.S2, partg, cntg, c->d_flag + p0, l.ed,
                          c->d_cflag + p0, l.defer, l.sy, spins);
     });
     if (rc) return rc;
@@ -914,9 +988,8 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
     const int nqt = (int)((m + T - 1) / T);
     const int Cm = nqt * T;
     rc = launch(c, PC_PREDK, 8.0 * Np * Cm, [&] {
-      hipLaunchKernelGGL(gpf::k_cross_cov, dim3((unsigned)((Cm + gpf::CC_C - 1) / gpf::CC_C), (unsigned)(Np / gpf::CC_R)), dim3(NTHR),
-                         gpf::cross_cov_lds(c->d), c->stream, (int)c->N,
-                         (int)m, (int)Np, Cm, c->d, c->d_x, (int)c->N, d_xf, (int)Cp, c->d_ls, d_ks, (int64_t)Cp);
+      gpf::launch_cross_cov(c->stream, (int)c->N, (int)m, (int)Np, Cm, c->d, c->d_x, (int)c->N, d_xf, (int)Cp, c->d_ls, d_ks,
+                            (int64_t)Cp);
     });
     if (rc) break;
     // V = U K_s: row tile t of U has (t+1) column tiles, the last one triangular
@@ -941,11 +1014,8 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
   hipStreamSynchronize(c->stream);
   if (c->prof) harvest(c);
   // keep the query-chunk buffers for the next call only while they are modest (a huge batch_size
-  // can size them up to half of free HBM, which must not stay pinned for the context's life and
-  // starve the next factorisation's or hull's allocations); GPF_PREDICT_KEEP_MB sets the bound
-  double keep_mb = 2048.0;
-  if (const char* e = getenv("GPF_PREDICT_KEEP_MB")) keep_mb = atof(e);
-  if ((double)c->p_np * (double)c->p_cols * 8.0 > keep_mb * 1048576.0) free_pred(c);
+  // can size them up to half of free HBM; see keep_bytes)
+  if ((double)c->p_np * (double)c->p_cols * 8.0 > keep_bytes()) free_pred(c);
   return rc;
 }
 
@@ -965,9 +1035,7 @@ int gpf_kernel(gpf_ctx* c, const double* x1, int64_t N1, const double* x2, int64
   GPF_HIP(c, hipMemcpyAsync(dx2, x2, (size_t)N2 * d * 8, hipMemcpyHostToDevice, c->stream));
   GPF_HIP(c, hipMemcpyAsync(dl, l, (size_t)d * 8, hipMemcpyHostToDevice, c->stream));
   int rc = launch(c, PC_BUILD, 8.0 * N1 * N2, [&] {
-    hipLaunchKernelGGL(gpf::k_cross_cov, dim3((unsigned)((N2 + gpf::CC_C - 1) / gpf::CC_C), (unsigned)((N1 + gpf::CC_R - 1) / gpf::CC_R)),
-                       dim3(NTHR), gpf::cross_cov_lds(d), c->stream, (int)N1, (int)N2, (int)N1, (int)N2, d, dx1, (int)N1, dx2, (int)N2,
-                       dl, dout, (int64_t)N2);
+    gpf::launch_cross_cov(c->stream, (int)N1, (int)N2, (int)N1, (int)N2, d, dx1, (int)N1, dx2, (int)N2, dl, dout, (int64_t)N2);
   });
   if (rc == GPF_OK) {
     if (hipMemcpyAsync(out, dout, (size_t)N1 * N2 * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
@@ -1032,11 +1100,15 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
   for (const StepLaunch& l : plan) {
     if (l.gc <= 0 || l.p0 < 0 || l.p0 + l.gc > pc || l.g < 0 || l.g >= ng)
       return plan_fail(msg, msg_len, "J=%d: bad group range p0=%d gc=%d g=%d", l.J, l.p0, l.gc, l.g);
-    if (l.S < 1 || l.S > Smax || (l.split != gpf::SPLIT_NONE) != (l.S > 1))
-      return plan_fail(msg, msg_len, "J=%d g=%d: split kind %d with S=%d", l.J, l.g, l.split, l.S);
+    if (l.S < 1 || (l.split == gpf::SPLIT_CRIT && (l.S < 2 || l.S > Smax || l.S2 != l.S)) ||
+        (l.split == gpf::SPLIT_NONE && (l.S != 1 || l.S2 != 1)) || (l.split == gpf::SPLIT_ALL && l.S2 != Smax))
+      return plan_fail(msg, msg_len, "J=%d g=%d: split kind %d with S=%d S2=%d", l.J, l.g, l.split, l.S, l.S2);
     const int tiles = l.gc * ntl;
+    auto pieces_of = [&](int w) { return l.split == gpf::SPLIT_ALL ? gpf::split_all_pieces(l.J, w, nt, l.S) : l.S; };
+    for (int w = 0; w < ntl; ++w)
+      if (pieces_of(w) > l.S2) return plan_fail(msg, msg_len, "J=%d tile %d: %d pieces but %d slots", l.J, w, pieces_of(w), l.S2);
     whole.assign((size_t)tiles, 0);
-    piece.assign((size_t)tiles * l.S, 0);
+    piece.assign((size_t)tiles * l.S2, 0);
     diag.assign((size_t)l.gc, 0);
     syrk.assign((size_t)l.gc, 0);
     if (l.sy && (!l.defer || l.J < 1 || l.J > nt - 2 || l.split == gpf::SPLIT_ALL))
@@ -1061,17 +1133,19 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
         ++wgs;
         continue;
       }
-      if (p < 0 || p >= l.gc || w < 0 || w >= ntl || sidx < 0 || sidx >= l.S)
+      if (p < 0 || p >= l.gc || w < 0 || w >= ntl || sidx < 0 || sidx >= pieces_of(w))
         return plan_fail(msg, msg_len, "J=%d block %u decodes out of range (p=%d w=%d)", l.J, b, p, w);
       const int t = p * ntl + w;
       if (role == gpf::ROLE_WHOLE) {
         ++whole[t];
       } else if (role == gpf::ROLE_PIECE) {
-        if (l.S < 2) return plan_fail(msg, msg_len, "J=%d block %u is a piece of an unsplit launch (S=%d)", l.J, b, l.S);
-        ++piece[(size_t)t * l.S + sidx];
-        const size_t off = l.part_off + ((size_t)t * l.S + sidx) * T * T, ci = l.cnt_off + (size_t)t * gpf::SPLIT_CNT;
-        if (off + (size_t)T * T > part_cap || ci + gpf::SPLIT_CNT > cnt_cap || l.S > 32)
-          return plan_fail(msg, msg_len, "J=%d tile %d piece %d outside the split buffers (S=%d)", l.J, t, sidx, l.S);
+        if (pieces_of(w) < 2) return plan_fail(msg, msg_len, "J=%d block %u is a piece of an unsplit tile", l.J, b);
+        ++piece[(size_t)t * l.S2 + sidx];
+        // slots as k_step addresses them: S2 per tile
+        const size_t off = l.part_off + ((size_t)t * l.S2 + sidx) * T * T, ci = l.cnt_off + (size_t)t * gpf::SPLIT_CNT;
+        if (off + (size_t)T * T > part_cap || ci + gpf::SPLIT_CNT > cnt_cap || l.S2 > gpf::SPLIT_MAXS)
+          return plan_fail(msg, msg_len, "J=%d tile %d piece %d outside the split buffers (S=%d S2=%d)", l.J, t, sidx, l.S,
+                           l.S2);
         plo[l.g] = std::min(plo[l.g], off);
         phi[l.g] = std::max(phi[l.g], off + (size_t)T * T);
         clo[l.g] = std::min(clo[l.g], ci);
@@ -1080,10 +1154,10 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
       ++wgs;
     }
     // the split-K reduction tree (gpf::split_part): every pair of node ranges has its own counter
-    for (int lv = 0; l.S > 1 && (1 << lv) < l.S; ++lv)
-      for (int cn = 0; (cn << lv) < l.S; cn += 2)
-        if (((cn + 1) << lv) < l.S && lv * 16 + (cn >> 1) >= gpf::SPLIT_CNT)
-          return plan_fail(msg, msg_len, "J=%d: split factor %d needs more than %d tree counters", l.J, l.S,
+    for (int lv = 0; l.split != gpf::SPLIT_NONE && (1 << lv) < l.S2; ++lv)
+      for (int cn = 0; (cn << lv) < l.S2; cn += 2)
+        if (((cn + 1) << lv) < l.S2 && lv * 16 + (cn >> 1) >= gpf::SPLIT_CNT)
+          return plan_fail(msg, msg_len, "J=%d: split factor %d needs more than %d tree counters", l.J, l.S2,
                            gpf::SPLIT_CNT);
     for (int q = 0; q < l.gc; ++q) {
       if (diag[q] != l.ed) return plan_fail(msg, msg_len, "J=%d particle %d: %d diagonal workgroups", l.J, q, diag[q]);
@@ -1093,12 +1167,12 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     }
     for (int t = 0; t < tiles; ++t) {
       int np = 0;
-      for (int s = 0; s < l.S; ++s) {
-        if (piece[(size_t)t * l.S + s] > 1) return plan_fail(msg, msg_len, "J=%d tile %d: piece %d run %d times", l.J, t, s, piece[(size_t)t * l.S + s]);
-        np += piece[(size_t)t * l.S + s];
+      for (int s = 0; s < l.S2; ++s) {
+        if (piece[(size_t)t * l.S2 + s] > 1) return plan_fail(msg, msg_len, "J=%d tile %d: piece %d run %d times", l.J, t, s, piece[(size_t)t * l.S2 + s]);
+        np += piece[(size_t)t * l.S2 + s];
       }
       if (whole[t] == 1 && np == 0) ++whole_tiles;
-      else if (whole[t] == 0 && np == l.S) ++split_tiles;  // S arrivals on a zeroed counter: one finisher
+      else if (whole[t] == 0 && np == pieces_of(t % ntl)) ++split_tiles;  // S arrivals on a zeroed counter: one finisher
       else return plan_fail(msg, msg_len, "J=%d tile %d: %d whole runs and %d pieces", l.J, t, whole[t], np);
     }
   }
@@ -1224,12 +1298,21 @@ int gpf_prob_surface(gpf_ctx* c, const double* tails, int64_t M, int E, double* 
   if (M == 0) return GPF_OK;
   hipSetDevice(c->device);
   const int64_t chunk = std::min<int64_t>(M, 1 << 20);
-  double *dt = nullptr, *dy = nullptr, *dp = nullptr;
-  int* dok = nullptr;
-  GPF_HIP(c, hipMalloc(&dt, (size_t)chunk * std::max(E, 1) * 8));
-  GPF_HIP(c, hipMalloc(&dy, (size_t)chunk * gpf::PS_POINTS * 8));
-  GPF_HIP(c, hipMalloc(&dp, (size_t)chunk * gpf::PS_POINTS * 8));
-  GPF_HIP(c, hipMalloc(&dok, (size_t)chunk * 4));
+  const int Ea = std::max(E, 1);
+  if (c->s_rows < chunk || c->s_e < Ea) {  // grow-only (rows and tail width)
+    GPF_HIP(c, hipStreamSynchronize(c->stream));
+    free_psurf(c);
+    GPF_HIP(c, hipMalloc(&c->s_t, (size_t)chunk * Ea * 8));
+    GPF_HIP(c, hipMalloc(&c->s_cmp, (size_t)chunk * Ea * 8));
+    GPF_HIP(c, hipMalloc(&c->s_info, (size_t)chunk * sizeof(double4)));
+    GPF_HIP(c, hipMalloc(&c->s_y, (size_t)chunk * gpf::PS_POINTS * 8));
+    GPF_HIP(c, hipMalloc(&c->s_p, (size_t)chunk * gpf::PS_POINTS * 8));
+    GPF_HIP(c, hipMalloc(&c->s_ok, (size_t)chunk * 4));
+    c->s_rows = chunk;
+    c->s_e = Ea;
+  }
+  double *dt = c->s_t, *dy = c->s_y, *dp = c->s_p;
+  int* dok = c->s_ok;
   int rc = GPF_OK;
   for (int64_t s = 0; s < M && rc == GPF_OK; s += chunk) {
     const int64_t m = std::min<int64_t>(chunk, M - s);
@@ -1240,7 +1323,9 @@ int gpf_prob_surface(gpf_ctx* c, const double* tails, int64_t M, int E, double* 
     // algorithmic bytes: the tails read, y and p written, the row flags
     const double bytes = (double)m * (E * 8.0 + 2.0 * gpf::PS_POINTS * 8.0 + 4.0);
     rc = launch(c, PC_PSURF, bytes, [&] {
-      hipLaunchKernelGGL(gpf::k_prob_surf, dim3((unsigned)m), dim3(gpf::PS_NTH), 0, c->stream, dt, m, E, dy, dp, dok);
+      hipLaunchKernelGGL(gpf::k_prob_prep, dim3(blocks_for(m)), dim3(NTHR), 0, c->stream, dt, m, E, c->s_cmp, c->s_info);
+      hipLaunchKernelGGL(gpf::k_prob_surf, dim3(blocks_for(m * gpf::PS_POINTS)), dim3(NTHR), 0, c->stream, c->s_cmp,
+                         c->s_info, m, E, dy, dp, dok);
     });
     if (rc) break;
     if (hipMemcpyAsync(y + s * gpf::PS_POINTS, dy, (size_t)m * gpf::PS_POINTS * 8, hipMemcpyDeviceToHost, c->stream) !=
@@ -1254,7 +1339,8 @@ int gpf_prob_surface(gpf_ctx* c, const double* tails, int64_t M, int E, double* 
     }
   }
   if (rc == GPF_HIP_ERROR && c->err.empty()) c->err = "gpf_prob_surface: HIP error";
-  hipFree(dt); hipFree(dy); hipFree(dp); hipFree(dok);
+  hipStreamSynchronize(c->stream);
+  if ((double)c->s_rows * (2.0 * c->s_e + 2.0 * gpf::PS_POINTS + 4.5) * 8.0 > keep_bytes()) free_psurf(c);
   return rc;
 }
 
@@ -1399,7 +1485,7 @@ int gpf_debug_wg_phase(unsigned long long* out, int nj, int nwg) {
 int gpf_debug_diag_stamps(unsigned long long* out, int n) {
   if (!out || n <= 0) return GPF_BAD_ARG;
   hipDeviceSynchronize();
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gpf::g_diag_stamps), sizeof(unsigned long long) * std::min(n, 32)) !=
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gpf::g_diag_stamps), sizeof(unsigned long long) * std::min(n, gpf::DIAG_NSTAMPS)) !=
       hipSuccess)
     return GPF_HIP_ERROR;
   return GPF_OK;

@@ -202,11 +202,11 @@ const char* gpf_build_info(void);
  * on a zeroed counter elect exactly one finisher), that pieces stay inside the split-K buffers,
  * and that concurrent particle groups never share partial slots or counters.
  * With the early diagonal factor it also checks that every launch starts with exactly one
- * diagonal workgroup per particle, ahead of all tiles, and with the quadrant finish of the
- * critical tile that every launch but the last ends with exactly four quadrant workgroups per
- * particle, behind all tiles.
+ * diagonal workgroup per particle, ahead of all tiles; with the deferred diagonal update
+ * (GPF_DEFER_SYRK, default on) that launches 1 .. nt-2 without the all-tile split carry exactly
+ * one SYRK workgroup per particle right behind the diagonal workgroups, and no other launch any.
  * stats (nullable, 9 entries): launches, workgroups, whole tiles, split tiles, S (all-tile
- * split factor), largest split factor, particle groups, diagonal workgroups, quadrant
+ * split factor), largest split factor, particle groups, diagonal workgroups, SYRK
  * workgroups. Returns GPF_OK, or
  * GPF_BAD_ARG with a description of the first violation in msg. */
 int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len);

@@ -29,6 +29,33 @@ rng = np.random.default_rng(1)
 x = rng.uniform(size=(d, N))
 y = np.sin(2 * np.pi * x).sum(0) + 0.1 * rng.standard_normal(N)
 e = np.full(N, 0.1)
+
+
+def split_all_chunks(J, w, nt):  # mirrors gpf::split_all_chunks / split_all_pieces / split_all_target
+    nL = nt - 1 - J
+    return (J if w < nL else J - (w - nL)) * 8
+
+
+def split_all_pieces(J, w, nt, tgt):
+    c = split_all_chunks(J, w, nt)
+    return min(32, 1 if c <= 0 else -(-c // tgt))
+
+
+def split_all_target(pc, nt, J):
+    budget = max(1, int(os.environ.get("GPF_SPLIT_K_SLOTS", 256)) - pc)
+    minch = int(os.environ.get("GPF_SPLIT_K_MINCH", 4))
+    tot = sum(split_all_chunks(J, w, nt) for w in range(nt - 1))
+    cap = max(1, J * 8)
+    lo, hi = min(cap, max(minch, -(-pc * tot // budget))), cap
+    while lo < hi:
+        m = (lo + hi) // 2
+        if pc * sum(split_all_pieces(J, w, nt, m) for w in range(nt - 1)) <= budget:
+            hi = m
+        else:
+            lo = m + 1
+    return lo
+
+
 ctx = gpfit.Context(0)
 ctx.set_data(x, y, e)
 if mode == "predict":
@@ -42,6 +69,7 @@ else:
     for _ in range(2):
         ctx.eval_batch(rng.uniform(0.05, 0.6, size=(P, d)))
 ctx.synchronize()
+plan = gpfit.plan_check(P, nt)
 W = 4096
 tr = np.zeros((nt, W, 3), dtype=np.uint64)
 ph = np.zeros((nt, W, 4), dtype=np.uint64)
@@ -61,15 +89,19 @@ for J in range(nt - 1):
     live &= st >= t0
     span = (en[live].max() - t0) * 1e-2
     tot += span
-    # tile w = 0 of particle 0: block ids with (p, w) = (0, 0) in particle-fastest order, plus pieces
-    ed = P if P * (nt - 1) <= 512 else 0  # early diagonal workgroups first (early_diag)
-    if mode == "predict":  # split-all: piece s of tile w at b = ed + s * (nt - 1) + w
-        ids = [b for b in range(ed, W) if live[b] and (b - ed) % (nt - 1) == 0]
-    else:  # critical-tile split (csrc/gpfit_api.hip split_crit): pieces of particle 0 at b = ed + s * P
-        S = 1 if (J == 0 or J >= nt - 1 or nt < 4) else min(4, max(1, J * T // 16 // 16))
-        while S > 1 and P * (nt - 1) + P * (S - 1) + ed > 512:
+    # tile w = 0 of particle 0: block ids with (p, w) = (0, 0) in particle-fastest order, plus pieces;
+    # the launch starts with P diagonal workgroups (early diagonal factor), then, in launches
+    # 1 .. nt-2 without the all-tile split, P SYRK workgroups (deferred diagonal update)
+    ed = P if plan["diag_workgroups"] > 0 else 0
+    if mode == "predict":  # balanced all-tile split: tile w = 0's pieces right after the diagonal workgroup
+        np0 = split_all_pieces(J, 0, nt, split_all_target(P, nt, J))
+        ids = [b for b in range(ed, ed + np0 * P, P) if live[b]]
+    else:  # critical-tile split (csrc/gpfit_api.hip split_crit, off by default): pieces at b = off + s * P
+        off = ed + (P if (plan["syrk_workgroups"] > 0 and 1 <= J <= nt - 2) else 0)
+        S = 1 if (J == 0 or J >= nt - 1 or nt < 4) else min(int(os.environ.get("GPF_SPLIT_CRIT", 1)), max(1, J * T // 16 // 16))
+        while S > 1 and P * (nt - 1) + P * (S - 1) + off > 512:
             S -= 1
-        ids = [ed + s * P for s in range(S) if live[ed + s * P]]
+        ids = [off + s * P for s in range(S) if live[off + s * P]]
     last = int(np.argmax(np.where(live, en, 0)))
     dg = f" diag end {(en[0] - t0) * 1e-2:6.1f}" if ed else ""
     if not ids:

@@ -16,8 +16,9 @@ for N, P in [(int(a), int(b)) for a, b in (c.split("x") for c in os.environ.get(
     ctx.set_data(x, y, e); ctx.set_grid(s, ex, lo, hi)
     for _ in range(3):
         ctx.eval_batch(rng.uniform(0.1, 0.5, size=(P, 3)))
-    buf = (ctypes.c_ulonglong * 32)()
-    assert ctx.lib.gpf_debug_diag_stamps(buf, 32) == 0
+    NS = 32 + 16 * 16
+    buf = (ctypes.c_ulonglong * NS)()
+    assert ctx.lib.gpf_debug_diag_stamps(buf, NS) == 0
     st = np.array(buf[:10], dtype=np.float64)
     d = np.diff(st)
     print(f"N={N} P={P}: total {st[9]-st[0]:.0f} cycles; " + ", ".join(f"{n} {v:.0f}" for n, v in zip(names, d)))
@@ -28,3 +29,20 @@ for N, P in [(int(a), int(b)) for a, b in (c.split("x") for c in os.environ.get(
     if u.any():
         print(f"    iteration k=4 update wave 1: work {u[1]-u[0]:.0f} (starts {u[0]-p[1]:+.0f} vs wave 0 after the barrier); "
               f"wave 7: work {u[5]-u[4]:.0f} (starts {u[4]-p[1]:+.0f})")
+    # per panel of the last factor64 call (build with the per-panel stamps)
+    pk = np.array(buf[32:32 + 256], dtype=np.float64).reshape(16, 16)
+    if pk[:, 8].any():
+        print("    k | w0 work (apply, factor) | update waves: last arrival (wave), spread | barrier release after last arrival")
+        for k in range(1, 16):
+            t0 = pk[k - 1, 8]  # wave 0 left the barrier of panel k-1
+            arr = pk[k, :8] - t0
+            last = int(np.argmax(arr[1:])) + 1
+            print(f"   {k:2d} | {arr[0]:6.0f} ({pk[k - 1, 9] - t0:5.0f}, {pk[k - 1, 10] - pk[k - 1, 9]:5.0f}) | "
+                  f"{arr[last]:6.0f} (w{last}), {arr[1:].min():6.0f}..{arr[1:].max():6.0f} | {pk[k, 8] - pk[k, :8].max():6.0f}")
+    uw = int(os.environ.get("DIAG_UW", 4))
+    if pk[:, 14].any():
+        print(f"    update wave {uw} per panel k (cycles after wave 0 leaves barrier k): leaves, after slot 0/1/2, arrives at k+1")
+        for k in range(15):
+            t0 = pk[k, 8]
+            print(f"   {k:2d} | {pk[k, 14] - t0:6.0f} | {pk[k, 11] - t0:6.0f} {pk[k, 12] - t0:6.0f} {pk[k, 13] - t0:6.0f} | "
+                  f"{pk[k + 1, uw] - t0:6.0f}")

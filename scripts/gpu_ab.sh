@@ -1,6 +1,7 @@
 #!/bin/bash
-# Interleaved A/B of library variants (VARIANTS, each gaussian-process_amd/libgpfit_<v>.so) on
-# configs CFGS, REPS rounds, one box (boxes of the pool differ by a few %).
+# Interleaved A/B of library variants (VARIANTS, each gaussian-process_amd/libgpfit_<v>.so, or
+# <v>@VAR=val[,VAR=val]: that library under those environment knobs) on configs CFGS, REPS
+# rounds, one box (boxes of the pool differ by a few %).
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${TAG:-ab}; mkdir -p $O
 declare -A CFG=( [B]="--n 1024 --d 2 --swarm-per-gpu 32" [C]="--n 4096 --d 3 --swarm-per-gpu 64"
@@ -8,15 +9,19 @@ declare -A CFG=( [B]="--n 1024 --d 2 --swarm-per-gpu 32" [C]="--n 4096 --d 3 --s
                  [P]="--n 4096 --d 3 --swarm-per-gpu 1" )
 for r in $(seq ${REPS:-2}); do
   for c in ${CFGS:-C}; do
-    for v in $VARIANTS; do
-      tag=${v}_${c}_$r
+    for spec in $VARIANTS; do
+      v=${spec%%@*}
+      envs=""
+      [ "$spec" != "$v" ] && envs=${spec#*@}
+      envs=${envs//,/ }
+      tag=${spec//[^A-Za-z0-9_]/_}_${c}_$r
       if [ "$c" = PRED ]; then  # the prediction line: GP at 10k query points, N=4096 (median of 3 calls)
-        GPFIT_LIB=$PWD/gaussian-process_amd/libgpfit_$v.so timeout -k 10 300 python bench.py --steps 1 --warmup 1 --no-cpu --pso-steps 0 --no-hull --psurf-rows 0 > $O/$tag.log 2>&1 || exit $?
-        python -c "import json; d=json.loads(open('$O/$tag.log').read().strip().splitlines()[-1])['predict']; print('$v $c #$r', round(d['ms'],3), 'ms  factor', round(d['factor_ms'],3), 'ms')"
+        env $envs GPFIT_LIB=$PWD/gaussian-process_amd/libgpfit_$v.so timeout -k 10 300 python bench.py --steps 1 --warmup 1 --no-cpu --pso-steps 0 --no-hull --psurf-rows 0 > $O/$tag.log 2>&1 || exit $?
+        python -c "import json; d=json.loads(open('$O/$tag.log').read().strip().splitlines()[-1])['predict']; print('$spec $c #$r', round(d['ms'],3), 'ms  factor', round(d['factor_ms'],3), 'ms')"
         continue
       fi
-      GPFIT_LIB=$PWD/gaussian-process_amd/libgpfit_$v.so timeout -k 10 300 python bench.py ${CFG[$c]} --steps ${STEPS:-8} --warmup 2 --no-cpu --pso-steps 0 --predict-points 0 --no-hull --psurf-rows 0 > $O/$tag.log 2>&1 || exit $?
-      python -c "import json; d=json.loads(open('$O/$tag.log').read().strip().splitlines()[-1]); r=d['roofline']; print('$v $c #$r', round(d['value'],1), 'evals/s  ', round(r['achieved'],2), 'TF')"
+      env $envs GPFIT_LIB=$PWD/gaussian-process_amd/libgpfit_$v.so timeout -k 10 300 python bench.py ${CFG[$c]} --steps ${STEPS:-8} --warmup 2 --no-cpu --pso-steps 0 --predict-points 0 --no-hull --psurf-rows 0 > $O/$tag.log 2>&1 || exit $?
+      python -c "import json; d=json.loads(open('$O/$tag.log').read().strip().splitlines()[-1]); r=d['roofline']; print('$spec $c #$r', round(d['value'],1), 'evals/s  ', round(r['achieved'],2), 'TF')"
     done
   done
 done

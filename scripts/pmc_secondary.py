@@ -1,6 +1,7 @@
 """Summarise rocprofv3 PMC passes for the secondary kernels (k_prob_surf, k_cross_cov, k_predict_vsq):
-per-dispatch averages of every collected counter, plus the kernel-trace duration of the same
-dispatches. Usage: python scripts/pmc_secondary.py <out.json> <pass_dir> [<pass_dir> ...]"""
+the counters of each kernel's LONGEST dispatch (the bench's measured call; the warm-up calls
+are smaller), with that dispatch's duration from the same pass.
+Usage: python scripts/pmc_secondary.py <out.json> <pass_dir> [<pass_dir> ...]"""
 import csv
 import glob
 import json
@@ -8,29 +9,24 @@ import sys
 
 KERNELS = ("k_prob_surf", "k_cross_cov", "k_predict_vsq")
 out, dirs = sys.argv[1], sys.argv[2:]
-res = {k: {"counters": {}, "dispatches": 0, "avg_ns": None} for k in KERNELS}
+res = {k: {"counters": {}, "grid": None, "avg_ns": None} for k in KERNELS}
 for d in dirs:
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
-        per = {}
+        per = {}  # (kernel, dispatch) -> [duration, grid, {counter: value}]
         for row in csv.DictReader(open(f)):
             name = next((k for k in KERNELS if k in row.get("Kernel_Name", "")), None)
             if name is None:
                 continue
-            key = (name, row["Counter_Name"])
-            disp = per.setdefault(key, {})
-            disp[row["Dispatch_Id"]] = disp.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
-        for (name, cn), disp in per.items():
-            res[name]["counters"][cn] = sum(disp.values()) / len(disp)
-            res[name]["dispatches"] = max(res[name]["dispatches"], len(disp))
-    for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
-        dur = {k: [] for k in KERNELS}
-        for row in csv.DictReader(open(f)):
-            name = next((k for k in KERNELS if k in row.get("Kernel_Name", "")), None)
-            if name:
-                dur[name].append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
-        for k, v in dur.items():
-            if v and res[k]["avg_ns"] is None:
-                res[k]["avg_ns"] = sum(v) / len(v)
+            e = per.setdefault((name, row["Dispatch_Id"]), [int(row["End_Timestamp"]) - int(row["Start_Timestamp"]),
+                                                            int(row["Grid_Size"]), {}])
+            e[2][row["Counter_Name"]] = e[2].get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+        for k in KERNELS:
+            mine = [v for (n, _), v in per.items() if n == k]
+            if mine:
+                dur, grid, cn = max(mine, key=lambda v: v[0])
+                res[k]["counters"].update(cn)
+                res[k]["grid"] = grid
+                res[k]["avg_ns"] = dur if res[k]["avg_ns"] is None else min(res[k]["avg_ns"], dur)
 ps = res["k_prob_surf"]
 c = ps["counters"]
 if "SQ_INSTS_VALU_FLOPS_FP64" in c and ps["avg_ns"]:
@@ -40,7 +36,12 @@ if "SQ_INSTS_VALU_FLOPS_FP64" in c and ps["avg_ns"]:
 if "SQ_ACTIVE_INST_VALU" in c and "GRBM_GUI_ACTIVE" in c:
     # SQ counters are summed over the 8 XCDs' SEs; GRBM_GUI_ACTIVE over the 8 XCDs (quad-cycles /
     # cycles: see MI355X_MICROARCH.md "s_memtime tick vs SQ PMC units"); VALUBusy as in rocprof's
-    # derived counter: 100 * SQ_ACTIVE_INST_VALU * 4 / CU_NUM / GRBM_GUI_ACTIVE (per XCD)
-    ps["valu_busy_pct"] = 100.0 * c["SQ_ACTIVE_INST_VALU"] * 4 / 256 / (c["GRBM_GUI_ACTIVE"] / 8)
+    # derived counter: 100 * SQ_ACTIVE_INST_VALU * 4 / SIMD_NUM / GRBM_GUI_ACTIVE (per XCD); 1024 SIMDs
+    ps["valu_busy_pct"] = 100.0 * c["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / (c["GRBM_GUI_ACTIVE"] / 8)
+    ps["valu_insts_per_simd"] = c["SQ_INSTS_VALU"] / 1024
+cc = res["k_cross_cov"]["counters"]
+if "WRITE_SIZE" in cc and res["k_cross_cov"]["avg_ns"]:
+    res["k_cross_cov"]["write_bytes"] = cc["WRITE_SIZE"] * 1024  # WRITE_SIZE is in KiB
+    res["k_cross_cov"]["write_TBps"] = cc["WRITE_SIZE"] * 1024 / res["k_cross_cov"]["avg_ns"] / 1e3
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1)[:2500])

@@ -150,6 +150,50 @@ def test_prob_surface_on_gpu_edge_rows():
     np.testing.assert_allclose(p[ok], ps, rtol=1e-12, atol=1e-15)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("keep_mb", ["2048", "0"])
+def test_prob_surface_buffer_reuse(monkeypatch, keep_mb):
+    """The row-chunk buffers kept between calls (grow-only; freed after the call above
+    GPF_PREDICT_KEEP_MB): a small call, a larger one with a wider tail, then the small one again
+    all equal fresh-context results bit for bit, and the oracle to 1e-12."""
+    import gpfit
+    from oracle import ref_cpu
+    monkeypatch.setenv("GPF_PREDICT_KEEP_MB", keep_mb)
+    rng = np.random.default_rng(7)
+
+    def frame(m, E):
+        t = np.empty((m, E))
+        t[:, 0::2] = rng.normal(size=(m, E // 2))
+        t[:, 1::2] = rng.uniform(0.05, 0.5, size=(m, E // 2))
+        t[rng.uniform(size=m) < 0.2, E - 2:] = np.inf
+        t[rng.uniform(size=m) < 0.05, 1] = np.nan  # odd count: skipped
+        return t
+
+    small, big = frame(300, 4), frame(5000, 8)
+    ctx = gpfit.Context(0)
+    try:
+        runs = [ctx.prob_surface(small), ctx.prob_surface(big), ctx.prob_surface(small)]
+    finally:
+        ctx.close()
+    fresh = []
+    for t in (small, big):
+        c2 = gpfit.Context(0)
+        try:
+            fresh.append(c2.prob_surface(t))
+        finally:
+            c2.close()
+    for got, ref in zip(runs, [fresh[0], fresh[1], fresh[0]]):
+        np.testing.assert_array_equal(got[2], ref[2])  # (skipped rows' y, p are not written)
+        np.testing.assert_array_equal(got[0][got[2]], ref[0][ref[2]])
+        np.testing.assert_array_equal(got[1][got[2]], ref[1][ref[2]])
+    y, p, ok = runs[1]
+    rows, ys, ps = ref_cpu.prob_surface(np.concatenate([np.zeros((len(big), 2)), big], axis=1), 2)
+    assert 0 < len(rows) < len(big)
+    assert list(np.nonzero(ok)[0]) == list(rows)
+    np.testing.assert_array_equal(y[ok], ys)
+    np.testing.assert_allclose(p[ok], ps, rtol=1e-12, atol=1e-15)
+
+
 def test_read_in_matches_reference_loader(f2, tmp_path, monkeypatch):
     import read_in
     shutil.copytree(INPUTS, tmp_path / "in")

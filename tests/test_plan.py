@@ -29,6 +29,8 @@ ENVS = [
     {"GPF_EARLY_DIAG": "1", "GPF_SPLIT_CRIT": "8", "GPF_SPLIT_CRIT_MIN": "2", "GPF_GROUPS": "3"},
     {"GPF_DEFER_SYRK": "0"}, {"GPF_DEFER_SYRK": "0", "GPF_EARLY_DIAG": "1"},
     {"GPF_DEFER_SYRK": "0", "GPF_EARLY_DIAG": "1", "GPF_SPLIT_CRIT": "8", "GPF_SPLIT_CRIT_MIN": "2", "GPF_GROUPS": "2"},
+    {"GPF_SPLIT_K_SLOTS": "512"}, {"GPF_SPLIT_K_SLOTS": "64", "GPF_SPLIT_K_MINCH": "1"},
+    {"GPF_SPLIT_K": "3", "GPF_SPLIT_K_SLOTS": "1000", "GPF_SPLIT_K_MINCH": "1", "GPF_GROUPS": "2"},
 ]
 
 
@@ -36,7 +38,7 @@ ENVS = [
 def env(monkeypatch):
     def apply(kv):
         for k in ("GPF_GROUPS", "GPF_SPLIT_K", "GPF_SPLIT_CRIT", "GPF_SPLIT_CRIT_MIN", "GPF_STEP_GROUP", "GPF_EARLY_DIAG",
-                  "GPF_DEFER_SYRK"):
+                  "GPF_DEFER_SYRK", "GPF_SPLIT_K_SLOTS", "GPF_SPLIT_K_MINCH"):
             monkeypatch.delenv(k, raising=False)
         for k, v in kv.items():
             monkeypatch.setenv(k, v)
@@ -84,7 +86,10 @@ def test_default_plans_of_the_baseline_configs(env):
     assert bs["S"] == 1 and bs["Smax"] > 1 and bs["split_tiles"] > 0
     env({})
     one = gpfit.plan_check(1, 32)           # prediction: single particle, all tiles split
-    assert one["S"] == 8 and one["whole_tiles"] == 31  # J = 0 has nothing to split; 8 pieces (8J chunks)
+    assert one["S"] > 1 and one["whole_tiles"] >= 31  # J = 0 has nothing to split
+    # balanced pieces: every launch fits one workgroup per CU (255 + the diagonal workgroup),
+    # and the critical tile of the deep launches gets the most pieces
+    assert one["workgroups"] <= 32 * 256 and one["Smax"] > 8
     # early diagonal factor where launches leave slots idle (B, the prediction), the fused factor
     # where they are slot-bound (C, D's and E's shares)
     assert e["diag_workgroups"] == 0
