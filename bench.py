@@ -427,9 +427,11 @@ def main():
     for _ in range(args.warmup):
         score(batch())
 
-    if not args.no_profile:
-        ctx.set_profiling(True)
-    ctx.reset_profile()
+    # `value`: K steps with no HIP events in the stream (recording an event pair around every
+    # launch costs the latency-bound configs real time: config B 31.8k vs 29.0k evals/s, C +0.8%;
+    # profiles/r3/ab_profiling_overhead.txt); the roofline and the per-kernel breakdown come from
+    # a second timed pass of the same K steps with an event pair around every launch
+    ctx.set_profiling(False)
     fence()
     x0 = comm.stats()[0] if comm is not None else 0.0
     t0 = time.perf_counter()
@@ -440,12 +442,25 @@ def main():
     fence()
     dt = time.perf_counter() - t0
     xch = (comm.stats()[0] - x0) / args.steps if comm is not None else None  # exchange ms per step, this rank
+    dt_prof = None
+    ctx.reset_profile()
+    if not args.no_profile:
+        ctx.set_profiling(True)
+        ctx.reset_profile()
+        fence()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            score(batch())
+        fence()
+        dt_prof = time.perf_counter() - t1
     prof = ctx.profile()
     ctx.set_profiling(False)
     if comm is not None:
         dt = float(comm.allreduce([dt], op="max")[0])  # max over ranks
         xch_max = float(comm.allreduce([xch], op="max")[0])
         xch_min = -float(comm.allreduce([-xch], op="max")[0])
+        if dt_prof is not None:
+            dt_prof = float(comm.allreduce([dt_prof], op="max")[0])
     evals = P * args.steps                # swarm x iterations, all of them full evaluations
     value = evals / dt
 
@@ -497,7 +512,10 @@ def main():
             # group's particles (the PMC pass ran the same schedule)
             "traffic_per": (f"k_step launch of one of {traffic['groups']} particle groups"
                             if traffic and traffic["groups"] > 1 else "k_step launch") if traffic else None,
-            "timing": timing, "particle_groups": groups,
+            "timing": timing + "; measured over a second timed pass of the same steps with an event pair "
+                               "around every launch (the `value` pass records no events)",
+            "ms_per_step_profiled_pass": dt_prof / args.steps * 1e3 if dt_prof else None,
+            "particle_groups": groups,
             "gemm_core_tflops": core,
             "frac_of_gemm_core": (achieved / core) if (achieved and core) else None,
             "launches": prof["panel_launches"], "avg_launch_ms": prof["panel_ms"] / max(prof["panel_launches"], 1),

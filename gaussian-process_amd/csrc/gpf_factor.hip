@@ -270,10 +270,10 @@ __device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx,
     } else {
       if (k == 4) DIAG_STAMP_T(20, 64);  // update wave 1 after the barrier
       if (k == 4) DIAG_STAMP_T(24, 448);  // update wave 7 after the barrier
-      // rank-4 updates with one MFMA per owned live block (A operand staged negated):
-      //   A(bi,bj), bj >= pc:          C -= L[rows][cb..] L[cols][cb..]^T
-      //   X(bi,bj), bi >= pc >= bj:    C -= L[rows > cb+3][cb..] X[cb..][cols <= cb+3]
-      // entries of A left of / above the panel are dead (never read again).
+      // rank-4 updates with one MFMA per owned live block (A operand staged negated); entries of
+      // A left of / above the panel are dead (never read again). (Issuing every slot's loads and
+      // MFMAs together measured slower, with or without the MFMA negate modifier; timing builds
+      // that drop parts of this work: profiles/r3/factor64_update_experiments.txt.)
       const int c2 = cb + 2 * PW;
       double* sb = strip + (k & 1) * 64 * PW;
 #pragma unroll
@@ -285,7 +285,7 @@ __device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx,
         f64_block(id, isx, bi, bj);
         const int arow = 16 * bi + lr, bcol = 16 * bj + lr;
         if (!isx) {
-          if (bj >= pc) {
+          if (bj >= pc) {  // A(bi,bj), bj >= pc: C -= L[rows][cb..] L[cols][cb..]^T
             const double av = -pk[arow * PW + lk];
             const double bv = pk[bcol * PW + lk];
             acc[j] = mfma(av, bv, acc[j]);
@@ -302,7 +302,7 @@ __device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx,
             }
           }
         } else {
-          if (bi >= pc && bj <= pc) {
+          if (bi >= pc && bj <= pc) {  // X(bi,bj), bi >= pc >= bj: C -= L[rows > cb+3][cb..] X[cb..][cols <= cb+3]
             const double av = (arow > cb + PW - 1) ? -pk[arow * PW + lk] : 0.0;
             const double bv = (bcol <= cb + PW - 1) ? pk[bcol * PW + lk] : 0.0;
             acc[j] = mfma(av, bv, acc[j]);
@@ -829,28 +829,33 @@ __device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, con
 // Split-K for launches with few tiles (a single particle: the prediction path, or small
 // swarms): the streamed GEMM of a tile is cut into S depth ranges, one workgroup ("piece")
 // each, and the S partial products are summed by a binary tree of hand-offs: at level l the
-// pieces pair up by node (c = s >> l, sibling c ^ 1); each stores its node sum to the node's
-// slot, takes a ticket on the pair's counter, and the second to arrive adds the sibling's slot
-// and carries the pair up; the last one standing holds the whole sum in its accumulators and
-// finishes the tile. Per chain that is log2(S) partial reads instead of S (the prediction's
-// 16-way split: 4 instead of 16, each a latency-bound 128 KiB read). IEEE addition commutes, so
-// a node's sum does not depend on which sibling arrived last: results are deterministic.
+// pieces pair up by node (c = s >> l, sibling c ^ 1); each takes a ticket on the pair's counter;
+// the first to arrive stores its node sum to the node's slot, raises the pair's ready flag and
+// leaves; the second waits for that flag (the first is running: it took its ticket), adds the
+// sibling's slot and carries the pair up; the last one standing holds the whole sum in its
+// accumulators and finishes the tile. Per level the chain (the second arriver) pays a ticket and
+// a 128 KiB read, not also a store and its drain (round 3: the tree sits on the prediction's
+// critical path once the pieces are balanced). IEEE addition commutes, so a node's sum does not
+// depend on which sibling arrived last: results are deterministic.
 // Hand-off (the memory-model argument): node sums are stored write-through (agent-scope relaxed
 // atomic stores, `sc1`: the line goes to memory, no L2 write-back fence, which on gfx950 would
 // write back every dirty line of the XCD's L2 — ~10-100 us here), every wave drains them
-// (s_waitcnt vmcnt(0)) before the barrier that precedes the ticket, and the second arriver does
-// an agent-scope acquire (L1/L2 invalidate) before reading the sibling's slot, which may have
-// been written from another XCD. The counter is reset by the second arriver for the next launch.
+// (s_waitcnt vmcnt(0)) before the barrier that precedes the ready flag, and the second arriver
+// does an agent-scope acquire (L1/L2 invalidate) after seeing the flag, before reading the
+// sibling's slot, which may have been written from another XCD. The second arriver resets the
+// pair's ticket and flag for the next launch. The wait is bounded like wait_diag (`spins`; on
+// timeout info gets bit 2 and the piece gives up, so the host reports the error).
 // seed(acc) (SEEDED: piece 0 only) starts piece 0's accumulator instead of zero: the L tiles seed
 // it with their covariance tile A_IJ, so the finisher does not compute it after the pieces, on
 // the critical path.
 // ----------------------------------------------------------------------------
-constexpr int SPLIT_CNT = 80;  // arrival counters per split tile: node (level l < 5, pair k < 16) at l * 16 + k
+constexpr int SPLIT_TREE = 80;              // tickets per split tile: pair (level l < 5, pair k < 16) at l * 16 + k
+constexpr int SPLIT_CNT = 2 * SPLIT_TREE;   // + the pairs' ready flags at SPLIT_TREE + l * 16 + k
 
 template <bool NN, bool NEG, bool SEEDED = false, typename Seed>
 __device__ bool split_part(Acc<T>& acc, const double* Ap, int lda, const double* Bp, int ldb, int nch, int S,
                            int s, double* __restrict__ pt, unsigned* __restrict__ ct, double* smem,
-                           const Quad<T>& qd, int* flag, Seed seed) {
+                           const Quad<T>& qd, int* flag, int* info, int spins, Seed seed) {
   const int c0 = s * nch / S, c1 = (s + 1) * nch / S;
   if (SEEDED && s == 0)
     seed(acc);
@@ -863,22 +868,38 @@ __device__ bool split_part(Acc<T>& acc, const double* Ap, int lda, const double*
   for (int l = 0; (1 << l) < S; ++l) {
     const int c = s >> l, sib = c ^ 1;
     if ((sib << l) >= S) continue;  // no sibling range at this level: go up alone
-    acc.store_wt(qd, pt + (size_t)(c << l) * T * T, T);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its part of the node sum
+    unsigned* tk = ct + l * 16 + (c >> 1);
+    unsigned* rdy = ct + SPLIT_TREE + l * 16 + (c >> 1);
+    __syncthreads();  // (the previous level's reads of *flag are done)
+    if (threadIdx.x == 0) *flag = (int)__hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
+    if (*flag == 0) {  // first: publish the node sum, then the sibling carries the pair on
+      acc.store_wt(qd, pt + (size_t)(c << l) * T * T, T);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its part of the node sum
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_store(rdy, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __syncthreads();  // (every wave has read *flag)
     if (threadIdx.x == 0) {
-      unsigned* cn = ct + l * 16 + (c >> 1);
-      const unsigned old = __hip_atomic_fetch_add(cn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int second = old == 1u;
-      if (second) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(cn, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int n = 0, late = 0;
+      while (__hip_atomic_load(rdy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        if (n++ >= spins) {
+          __hip_atomic_fetch_or(info, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          late = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
       }
-      *flag = second;
+      if (!late) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __hip_atomic_store(rdy, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      *flag = late;
     }
     __syncthreads();
-    if (!*flag) return false;  // the sibling carries the pair on
+    if (*flag) return false;  // timed out: the host reports it
     const double* p0 =
         launder(pt + (size_t)(sib << l) * T * T + (size_t)(qd.rb + (qd.lane >> 4)) * T + qd.cb + (qd.lane & 15));
 #pragma unroll
@@ -975,7 +996,8 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
       const int Sx = SPLIT == SPLIT_ALL ? split_all_pieces(J, w, nt, S) : S;
       if (!split_part<false, true, true>(acc, Lp + (size_t)J * T * ld, Npad, Lp + (size_t)I * T * ld, Npad,
                                          J * T / DL_KC, Sx, sidx, pt, cnt + (size_t)(p * (nt - 1) + w) * SPLIT_CNT, lds,
-                                         qd, sflag, [&](Acc<T>& a) { cov_tile_acc(a, qd, x, lp, d, N, J, I, lds); }))
+                                         qd, sflag, info + p, spins,
+                                         [&](Acc<T>& a) { cov_tile_acc(a, qd, x, lp, d, N, J, I, lds); }))
         return;  // (the finisher's accumulators hold D)
     } else {
       cov_tile_acc(acc, qd, x, lp, d, N, J, I, lds);
@@ -1040,8 +1062,8 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
       const int Sx = split_all_pieces(J, w, nt, S);
       if (!split_part<true, false, false>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
                                           Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T / DL_KC, Sx, sidx,
-                                          pt, cnt + (size_t)(p * (nt - 1) + w) * SPLIT_CNT, lds, qd, sflag,
-                                          [](Acc<T>&) {}))
+                                          pt, cnt + (size_t)(p * (nt - 1) + w) * SPLIT_CNT, lds, qd, sflag, info + p,
+                                          spins, [](Acc<T>&) {}))
         return;
     } else {
       acc.zero();

@@ -1156,9 +1156,9 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     // the split-K reduction tree (gpf::split_part): every pair of node ranges has its own counter
     for (int lv = 0; l.split != gpf::SPLIT_NONE && (1 << lv) < l.S2; ++lv)
       for (int cn = 0; (cn << lv) < l.S2; cn += 2)
-        if (((cn + 1) << lv) < l.S2 && lv * 16 + (cn >> 1) >= gpf::SPLIT_CNT)
+        if (((cn + 1) << lv) < l.S2 && lv * 16 + (cn >> 1) >= gpf::SPLIT_TREE)
           return plan_fail(msg, msg_len, "J=%d: split factor %d needs more than %d tree counters", l.J, l.S2,
-                           gpf::SPLIT_CNT);
+                           gpf::SPLIT_TREE);
     for (int q = 0; q < l.gc; ++q) {
       if (diag[q] != l.ed) return plan_fail(msg, msg_len, "J=%d particle %d: %d diagonal workgroups", l.J, q, diag[q]);
       diag_wgs += diag[q];

@@ -15,7 +15,10 @@ for N, P in [(int(a), int(b)) for a, b in (c.split("x") for c in os.environ.get(
     lo, hi = ref_cpu.search_bounds(x); s, ex = ref_cpu.sigma_grid()
     ctx.set_data(x, y, e); ctx.set_grid(s, ex, lo, hi)
     for _ in range(3):
-        ctx.eval_batch(rng.uniform(0.1, 0.5, size=(P, 3)))
+        try:
+            ctx.eval_batch(rng.uniform(0.1, 0.5, size=(P, 3)))
+        except Exception as err:  # timing-experiment builds compute garbage
+            print(f"    (eval_batch: {type(err).__name__})")
     NS = 32 + 16 * 16
     buf = (ctypes.c_ulonglong * NS)()
     assert ctx.lib.gpf_debug_diag_stamps(buf, NS) == 0
