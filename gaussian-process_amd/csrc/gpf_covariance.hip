@@ -105,6 +105,9 @@ __global__ __launch_bounds__(NTHR) void k_build_cov(int N, int Npad, int d, cons
 #ifndef GPF_CC_R
 #define GPF_CC_R 32
 #endif
+#ifndef GPF_CC_NT
+#define GPF_CC_NT 1  // non-temporal stores (A/B, profiles/r3/ab_cross_cov.txt: 4.7 -> 4.9 TB/s)
+#endif
 constexpr int CC_R = GPF_CC_R, CC_C = 256;
 __host__ __device__ constexpr size_t cross_cov_lds(int d) { return (size_t)(d + 1) * (CC_R + CC_C) * 8; }
 template <int D>
