@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 O=gpurun_out/${TAG:-ev}; mkdir -p $O
 GPF_FORCE_BUILD=1 timeout -k 10 300 python -c "import __graft_entry__ as g; g.build()" > $O/build.log 2>&1 || exit 3
 tail -1 $O/build.log
-timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $O/bench_C.log 2>&1 || exit $?
+timeout -k 10 600 python bench.py > $O/bench_C.log 2>&1 || exit $?
 tail -1 $O/bench_C.log | cut -c1-300
 BQ="--no-cpu --predict-points 0 --no-hull --psurf-rows 0"
 timeout -k 10 300 python bench.py --n 1024 --d 2 --swarm-per-gpu 32 --steps 40 --warmup 4 $BQ > $O/bench_B.log 2>&1 || exit $?
