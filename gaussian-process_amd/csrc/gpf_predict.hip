@@ -16,7 +16,9 @@ __global__ __launch_bounds__(Geo<T>::NTH, 4) void k_predict_vsq(int Npad, const 
                                                          const double* __restrict__ Ks, int ldks,
                                                          double* __restrict__ vsq) {
   __shared__ __attribute__((aligned(16))) double smem[DL_STAGE];
-  const int q = blockIdx.x, t = blockIdx.y;
+  // deepest row tiles first (t = nt-1 streams (t+1) x 128 deep): the dispatch order is x fastest,
+  // so the longest workgroups start in the first rounds instead of forming the launch's tail
+  const int q = blockIdx.x, t = (int)gridDim.y - 1 - (int)blockIdx.y;
   const Quad<T> qd;
   Acc<T> acc;
   acc.zero();
