@@ -248,6 +248,16 @@ __device__ __forceinline__ void dl_load_s(const void* base, uint32_t off, double
 #endif
 __device__ __forceinline__ int dl_sw(int r) { return GPF_DL_SW ? ((r >> 1) & 7) : (r & 7); }
 
+// A wave-uniform pointer forced into SGPRs (v_readfirstlane of each half): the saddr transfers
+// need their base there, and the divergence analysis cannot always prove a base uniform (e.g.
+// behind a branch on a value read from LDS), in which case the "s" operand would get a VGPR pair.
+template <typename P>
+__device__ __forceinline__ P* uniform_ptr(P* p) {
+  const unsigned long long v = (unsigned long long)(uintptr_t)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (P*)(uintptr_t)(((unsigned long long)hi << 32) | lo);
+}
+
 // Per-lane LDS byte offsets of an MFMA A-operand read from a [r][k] panel in the dl_sw layout
 // (rows r0 + (lane & 15), r0 a multiple of 16; depth 4 s + (lane >> 4) of a 16-deep chunk), for
 // the k-steps s = 0..3 of a chunk. Row-block and chunk displacements are added as immediates.
@@ -293,8 +303,9 @@ struct DenseRun {
 
   template <int BUF>
   __device__ __forceinline__ void issue(const double* Ap, const double* Bp, int ldb, int c, double* smem) const {
-    const char* Ac = (const char*)(Ap + c * DL_KC);
-    const char* Bc = NN ? (const char*)(Bp + (size_t)c * DL_KC * ldb) : (const char*)(Bp + c * DL_KC);
+    // (uniform_ptr: a no-op where the chunk base is already scalar, as in every dense loop)
+    const char* Ac = uniform_ptr((const char*)(Ap + c * DL_KC));
+    const char* Bc = uniform_ptr(NN ? (const char*)(Bp + (size_t)c * DL_KC * ldb) : (const char*)(Bp + c * DL_KC));
     double* sbuf = smem + BUF * DL_BUF;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -368,13 +379,13 @@ struct DenseRun {
 // allocation of the dense loop); exactly the MFMAs tri_live admits are issued, so results are
 // bitwise those of per-block skipping. Every wave still passes one barrier per chunk.
 template <bool NN, bool NEG = false, int TRI = TRI_NONE>
-__device__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
+__device__ __forceinline__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
                                int ldb, int K, double* smem, const Quad<128>& qd) {
   const int nch = K / DL_KC;
   if (nch <= 0) return;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const double* Ar = Ap;  // scalar bases
-  const double* Br = Bp;
+  const double* Ar = uniform_ptr(Ap);  // scalar bases
+  const double* Br = uniform_ptr(Bp);
   const DenseRun<NN, NEG> dr(qd, lda, ldb, wave);
   dr.template issue<0>(Ar, Br, ldb, 0, smem);
   // Drain every outstanding vector-memory op here (the chunk-0 transfers, which the first chunk
@@ -427,6 +438,7 @@ __device__ __forceinline__ void syrk_rows(double* __restrict__ C, size_t ldc, co
   if (nch > 0) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const DenseRun<false, true> dr(qd, lda, lda, wave);
+    A = uniform_ptr(A);
     dr.template issue<0>(A, A, lda, 0, smem);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the seed loads retired outside the loop (gemm_stream_dl)
     dr.template run<M0>(acc, A, A, lda, 0, nch, nch, smem);

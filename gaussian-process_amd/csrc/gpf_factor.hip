@@ -185,7 +185,198 @@ __device__ __forceinline__ void f64_block(int id, bool& isx, int& bi, int& bj) {
   bj = t - bi * (bi + 1) / 2;
 }
 
+// ----------------------------------------------------------------------------
+// Blocked 64x64 factor (GPF_F64_BLOCKED = 1, default): 16-wide block columns, right-looking.
+// The 4-wide panels above pass 17 barriers and put the 4x4 pivot chain, the strip hand-off and
+// the update waves' serialised operand loads on every 4 columns (~3.4k cycles per panel,
+// profiles/r3/factor64_panel_stamps.txt). Here one wave factors a whole 16-column block column
+// (all rows below the diagonal at once, lane = row, registers only), and everything else is
+// 16x16x16 MFMA products between LDS blocks on the other waves, two barriers per block column:
+//   P1(k): wave 0 factors block column k (rows 16k..63) -> L_{.,k};   other waves, off the
+//          chain: the trailing updates of columns >= k+1 by block column k-1, X_{k-1,k-1} =
+//          L_{k-1,k-1}^-1 (one lane per column, forward substitution) and the inverse's products
+//   P2(k): the chain: A_{i,k+1} -= L_ik L_{k+1,k}^T (i > k, one wave per block); inverse products
+// then three short phases finish the last block row of X = L^-1:
+//   X_ij = -X_ii sum_{t=j}^{i-1} L_it X_tj   (block back-substitution, accumulated in X's blocks)
+// Deterministic (a fixed assignment of blocks to waves); not bitwise the 4-wide panels' result.
+// Waves w and w+4 share a SIMD: while wave 0 factors a block column, wave 4 stays idle and the
+// longest side job (the 16x16 inversion) runs on wave 6.
+// ----------------------------------------------------------------------------
+#ifndef GPF_F64_BLOCKED
+#define GPF_F64_BLOCKED 1
+#endif
+
+// D (+)= (NEG ? -1 : 1) A B for 16x16 blocks in LDS: A row-major [r][k] at pa; B as [k][c] at pb
+// (BT = false) or given transposed, Bt[c][k] at pb (BT = true); D row-major at pc (ACC: D is
+// also the addend). One wave.
+template <bool BT, bool NEG, bool ACC>
+__device__ __forceinline__ void mm16(double* pc, int ldc, const double* pa, int lda, const double* pb, int ldb) {
+  const int lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
+  double a[4], b[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    a[s] = pa[lr * lda + 4 * s + lk];
+    b[s] = BT ? pb[lr * ldb + 4 * s + lk] : pb[(4 * s + lk) * ldb + lr];
+  }
+  d4 acc;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) acc[e] = ACC ? pc[(lk + 4 * e) * ldc + lr] : 0.0;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = NEG ? mfma_neg_a(a[s], b[s], acc) : mfma(a[s], b[s], acc);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) pc[(lk + 4 * e) * ldc + lr] = acc[e];
+}
+
+// Block column k (rows 16k..63, columns 16k..16k+15, fully updated by the earlier columns) on one
+// wave: lane r holds row 16k + r. Column by column: pivot from lane q (readlane), 1/sqrt by
+// v_rsq + Newton, scale the column, rank-1 update of the lane's row (one fma per entry) with the
+// column's other diagonal-block entries (readlanes, a few per scheduling region: the scheduler
+// would otherwise hoist a column's readlanes together and spill the scalar registers; an LDS
+// column buffer instead measured more vector spills inside k_step). Writes L (zeros above the
+// diagonal of block (k,k)) and the pivots' reciprocal square roots dinv[16k + q]. Returns whether
+// a pivot was not > 0.
+__device__ __forceinline__ bool f64b_column(double* sA, int la, int k, double* dinv) {
+  const int r = threadIdx.x & 63;
+  const int R = 16 * k + r;
+  const bool live = R < 64;
+  double* row = sA + (live ? R : 0) * la + 16 * k;
+  double a[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) a[c] = (live && (r >= 16 || c <= r)) ? row[c] : 0.0;
+  bool bad = false;
+  double myinv = 0.0;  // lane q: the reciprocal square root of pivot q
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const double p = readlane_f64(a[q], q);
+    bad = bad | !(p > 0.0);
+    const double inv = rsqrt_nr(p);
+    const double l = (r > q) ? a[q] * inv : ((r == q) ? p * inv : 0.0);
+    a[q] = l;
+    myinv = (r == q) ? inv : myinv;
+#pragma unroll
+    for (int s = q + 1; s < 16; ++s) {
+      a[s] = fma(-l, readlane_f64(l, s), a[s]);
+      if (((s - q) & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (r < 16) dinv[16 * k + r] = myinv;
+  if (live) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) row[c] = (r < 16 && c > r) ? 0.0 : a[c];
+  }
+  return bad;
+}
+
+// X_kk = L_kk^-1 of a 16x16 lower-triangular block (zeros above its diagonal in LDS): lane c
+// (c < 16) forward-substitutes column c, x_i = -(sum_{j<i} L_ij x_j) * dinv_i, x_c = dinv_c (the
+// [A | I] elimination's X_qq); the L entries are uniform LDS reads. One wave; writes zeros above
+// the diagonal of X_kk.
+__device__ __forceinline__ void f64b_inv(const double* sL, int la, double* sXo, int lx, const double* dv) {
+  const int lane = threadIdx.x & 63, c = lane & 15;
+  double x[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    double dot = 0.0;
+#pragma unroll
+    for (int j = 0; j < i; ++j) dot = fma(sL[i * la + j], x[j], dot);
+    x[i] = (i < c) ? 0.0 : ((i == c) ? dv[i] : -dot * dv[i]);
+    __builtin_amdgcn_sched_barrier(0);  // a row of uniform L reads per region (register budget)
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sXo[i * lx + c] = x[i];
+  }
+}
+
+__device__ __forceinline__ bool factor64_blocked(double* sA, int la, double* sX, int lx, double* buf) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  double* dinv = buf;  // [64]
+  auto Ab = [&](int i, int j) { return sA + 16 * i * la + 16 * j; };
+  auto Xb = [&](int i, int j) { return sX + 16 * i * lx + 16 * j; };
+  bool bad = false;
+  DIAG_STAMP_T(31, 0);
+  // P1(0) / P2(0)
+  if (wave == 0) {
+    bad = f64b_column(sA, la, 0, dinv);
+    DIAG_STAMP_T(41, 0);
+  }
+  lsync();
+  DIAG_STAMP_T(32, 0);  // (diagnostic build) thread 0 leaves barrier 0
+  if (wave >= 1 && wave <= 3) mm16<true, true, true>(Ab(wave, 1), la, Ab(wave, 0), la, Ab(1, 0), la);  // A_i1 -= L_i0 L_10^T
+  lsync();
+  DIAG_STAMP_T(33, 0);  // (diagnostic build) thread 0 leaves barrier 1
+  // P1(1): column 1 | X_00, A_22 / A_32 / A_33 -= (column 0 terms)
+  if (wave == 0) {
+    bad = f64b_column(sA, la, 1, dinv) | bad;
+    DIAG_STAMP_T(42, 0);
+  }
+  else if (wave == 1) mm16<true, true, true>(Ab(2, 2), la, Ab(2, 0), la, Ab(2, 0), la);
+  else if (wave == 2) mm16<true, true, true>(Ab(3, 2), la, Ab(3, 0), la, Ab(2, 0), la);
+  else if (wave == 3) mm16<true, true, true>(Ab(3, 3), la, Ab(3, 0), la, Ab(3, 0), la);
+  else if (wave == 6) f64b_inv(Ab(0, 0), la, Xb(0, 0), lx, dinv);
+  lsync();
+  DIAG_STAMP_T(34, 0);  // (diagnostic build) thread 0 leaves barrier 2
+  // P2(1): A_i2 -= L_i1 L_21^T | Xcur_i0 = L_i0 X_00
+  if (wave == 1 || wave == 2) mm16<true, true, true>(Ab(wave + 1, 2), la, Ab(wave + 1, 1), la, Ab(2, 1), la);
+  else if (wave >= 4 && wave <= 6) mm16<false, false, false>(Xb(wave - 3, 0), lx, Ab(wave - 3, 0), la, Xb(0, 0), lx);
+  lsync();
+  DIAG_STAMP_T(35, 0);  // (diagnostic build) thread 0 leaves barrier 3
+  // P1(2): column 2 | X_11, A_33 -= L_31 L_31^T
+  if (wave == 0) {
+    bad = f64b_column(sA, la, 2, dinv) | bad;
+    DIAG_STAMP_T(43, 0);
+  }
+  else if (wave == 3) mm16<true, true, true>(Ab(3, 3), la, Ab(3, 1), la, Ab(3, 1), la);
+  else if (wave == 6) f64b_inv(Ab(1, 1), la, Xb(1, 1), lx, dinv + 16);
+  lsync();
+  DIAG_STAMP_T(36, 0);  // (diagnostic build) thread 0 leaves barrier 4
+  // P2(2): A_33 -= L_32 L_32^T | X_10 = -X_11 Xcur_10, Xcur_21 = L_21 X_11, Xcur_31 = L_31 X_11
+  if (wave == 1) mm16<true, true, true>(Ab(3, 3), la, Ab(3, 2), la, Ab(3, 2), la);
+  else if (wave == 4) mm16<false, true, false>(Xb(1, 0), lx, Xb(1, 1), lx, Xb(1, 0), lx);
+  else if (wave == 5) mm16<false, false, false>(Xb(2, 1), lx, Ab(2, 1), la, Xb(1, 1), lx);
+  else if (wave == 6) mm16<false, false, false>(Xb(3, 1), lx, Ab(3, 1), la, Xb(1, 1), lx);
+  lsync();
+  DIAG_STAMP_T(37, 0);  // (diagnostic build) thread 0 leaves barrier 5
+  // P1(3): column 3 | X_22, Xcur_20 += L_21 X_10, Xcur_30 += L_31 X_10
+  if (wave == 0) {
+    bad = f64b_column(sA, la, 3, dinv) | bad;
+    DIAG_STAMP_T(44, 0);
+  }
+  else if (wave == 6) f64b_inv(Ab(2, 2), la, Xb(2, 2), lx, dinv + 32);
+  else if (wave == 5) mm16<false, false, true>(Xb(2, 0), lx, Ab(2, 1), la, Xb(1, 0), lx);
+  else if (wave == 7) mm16<false, false, true>(Xb(3, 0), lx, Ab(3, 1), la, Xb(1, 0), lx);
+  lsync();
+  DIAG_STAMP_T(38, 0);  // (diagnostic build) thread 0 leaves barrier 6
+  // T1: X_33 | X_20 = -X_22 Xcur_20, X_21 = -X_22 Xcur_21, Xcur_32 = L_32 X_22
+  if (wave == 4) f64b_inv(Ab(3, 3), la, Xb(3, 3), lx, dinv + 48);
+  else if (wave == 5) mm16<false, true, false>(Xb(2, 0), lx, Xb(2, 2), lx, Xb(2, 0), lx);
+  else if (wave == 6) mm16<false, true, false>(Xb(2, 1), lx, Xb(2, 2), lx, Xb(2, 1), lx);
+  else if (wave == 7) mm16<false, false, false>(Xb(3, 2), lx, Ab(3, 2), la, Xb(2, 2), lx);
+  lsync();
+  DIAG_STAMP_T(39, 0);  // (diagnostic build) thread 0 leaves barrier 7
+  // T2: Xcur_30 += L_32 X_20, Xcur_31 += L_32 X_21
+  if (wave == 5 || wave == 6) mm16<false, false, true>(Xb(3, wave - 5), lx, Ab(3, 2), la, Xb(2, wave - 5), lx);
+  lsync();
+  DIAG_STAMP_T(40, 0);  // (diagnostic build) thread 0 leaves barrier 8
+  // T3: X_3j = -X_33 Xcur_3j; zeros above the diagonal blocks of L and X
+  if (wave >= 5) mm16<false, true, false>(Xb(3, wave - 5), lx, Xb(3, 3), lx, Xb(3, wave - 5), lx);
+#pragma unroll
+  for (int u = 0; u < 6 * 256 / DNTH; ++u) {
+    const int i = threadIdx.x + DNTH * u;
+    const int t = i >> 8, e = i & 255;  // upper blocks (0,1) (0,2) (0,3) (1,2) (1,3) (2,3)
+    const int bi = (t < 3) ? 0 : (t < 5) ? 1 : 2;
+    const int bj = (t < 3) ? t + 1 : (t < 5) ? t - 1 : 3;
+    const int rr = 16 * bi + (e >> 4), cc = 16 * bj + (e & 15);
+    sA[rr * la + cc] = 0.0;
+    sX[rr * lx + cc] = 0.0;
+  }
+  return bad;
+}
+
 __device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx, double* buf) {
+#if GPF_F64_BLOCKED
+  return factor64_blocked(sA, la, sX, lx, buf);
+#endif
   constexpr int PW = F64_PW, NS = 3;  // panel width, block slots per update wave
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -853,7 +1044,7 @@ constexpr int SPLIT_TREE = 80;              // tickets per split tile: pair (lev
 constexpr int SPLIT_CNT = 2 * SPLIT_TREE;   // + the pairs' ready flags at SPLIT_TREE + l * 16 + k
 
 template <bool NN, bool NEG, bool SEEDED = false, typename Seed>
-__device__ bool split_part(Acc<T>& acc, const double* Ap, int lda, const double* Bp, int ldb, int nch, int S,
+__device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int lda, const double* Bp, int ldb, int nch, int S,
                            int s, double* __restrict__ pt, unsigned* __restrict__ ct, double* smem,
                            const Quad<T>& qd, int* flag, int* info, int spins, Seed seed) {
   const int c0 = s * nch / S, c1 = (s + 1) * nch / S;

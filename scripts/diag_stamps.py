@@ -32,6 +32,14 @@ for N, P in [(int(a), int(b)) for a, b in (c.split("x") for c in os.environ.get(
     if u.any():
         print(f"    iteration k=4 update wave 1: work {u[1]-u[0]:.0f} (starts {u[0]-p[1]:+.0f} vs wave 0 after the barrier); "
               f"wave 7: work {u[5]-u[4]:.0f} (starts {u[4]-p[1]:+.0f})")
+    # blocked factor64 (the last call): thread 0 leaving each of its 9 barriers (stamps 32..40, start 31),
+    # wave 0's block-column factors ending (41..44)
+    bs = np.array(buf[31:45], dtype=np.float64)
+    if bs[0] and bs[10:14].all():
+        ph = ["P1(0)", "P2(0)", "P1(1)", "P2(1)", "P1(2)", "P2(2)", "P1(3)", "T1", "T2"]
+        print("    blocked factor64 phases (cycles): " + ", ".join(f"{n} {v:.0f}" for n, v in zip(ph, np.diff(bs[:10]))))
+        print("    wave 0 column factors k=0..3 end after phase start: " +
+              ", ".join(f"{bs[10 + k] - bs[2 * k]:.0f}" for k in range(4)))
     # per panel of the last factor64 call (build with the per-panel stamps)
     pk = np.array(buf[32:32 + 256], dtype=np.float64).reshape(16, 16)
     if pk[:, 8].any():
