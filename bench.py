@@ -364,8 +364,9 @@ def plumbing(args, world, rank):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # default: ~3 s of timed GPU work at config C (long enough for a 5 s SMI sampler to see it)
-    ap.add_argument("--steps", type=int, default=60)
+    # default: ~9 s of timed GPU work at config C, twice (the value pass and the profiled pass): the
+    # round-2 default (60 steps, ~3 s) left the driver's ~5 s SMI sampler with no busy sample
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=4096)
     ap.add_argument("--d", type=int, default=3)

@@ -953,7 +953,7 @@ static_assert(STEP_NTH == DNTH, "the fused diagonal runs on the step workgroup")
 // and hardware placement of every k_step workgroup, per block column J.
 constexpr int WG_TRACE_J = 64, WG_TRACE_N = 4096;
 __device__ unsigned long long g_wg_trace[WG_TRACE_J][WG_TRACE_N][3];
-__device__ unsigned long long g_wg_phase[WG_TRACE_J][WG_TRACE_N][4];  // wave-0 phase ends (see step_item)
+__device__ unsigned long long g_wg_phase[WG_TRACE_J][WG_TRACE_N][4];  // wave-0 phase ends (see step_item; [3]: split piece's GEMM before its tree)
 __device__ __forceinline__ unsigned long long realtime() {
   unsigned long long t;
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -1040,13 +1040,23 @@ __device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, con
 // it with their covariance tile A_IJ, so the finisher does not compute it after the pieces, on
 // the critical path.
 // ----------------------------------------------------------------------------
-constexpr int SPLIT_TREE = 80;              // tickets per split tile: pair (level l < 5, pair k < 16) at l * 16 + k
-constexpr int SPLIT_CNT = 2 * SPLIT_TREE;   // + the pairs' ready flags at SPLIT_TREE + l * 16 + k
+// Radix 4 (GPF_SPLIT_RADIX, default): the nodes meet in groups of up to 4 instead of pairs — the
+// first three arrivers store and leave, the last waits for their flags and forms the group's sum
+// in the binary tree's pairwise shape ((n0 + n1) + (n2 + n3)) with its own node taken from the
+// registers (commutativity again), so the sums are bitwise those of the radix-2 tree with half
+// the levels: the hand-offs, not the reads, set a level's cost (~9 us per level on the
+// prediction's critical tile, profiles/r3s2/crit_predict_tree.txt).
+#ifndef GPF_SPLIT_RADIX
+#define GPF_SPLIT_RADIX 2
+#endif
+static_assert(GPF_SPLIT_RADIX == 2 || GPF_SPLIT_RADIX == 4, "split-K tree radix");
+constexpr int SPLIT_TREE = 80;              // tickets per split tile: group k (< 16) of level l (< 5) at l * 16 + k
+constexpr int SPLIT_CNT = SPLIT_TREE + 96;  // + ready flags: radix 2: SPLIT_TREE + l * 16 + pair; radix 4: SPLIT_TREE + l * 32 + node
 
 template <bool NN, bool NEG, bool SEEDED = false, typename Seed>
 __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int lda, const double* Bp, int ldb, int nch, int S,
                            int s, double* __restrict__ pt, unsigned* __restrict__ ct, double* smem,
-                           const Quad<T>& qd, int* flag, int* info, int spins, Seed seed) {
+                           const Quad<T>& qd, int* flag, int* info, int spins, Seed seed, int J) {
   const int c0 = s * nch / S, c1 = (s + 1) * nch / S;
   if (SEEDED && s == 0)
     seed(acc);
@@ -1056,6 +1066,77 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
     gemm_stream_dl<NN, NEG>(acc, Ap + (size_t)c0 * DL_KC, lda,
                             NN ? Bp + (size_t)c0 * DL_KC * ldb : Bp + (size_t)c0 * DL_KC, ldb, (c1 - c0) * DL_KC,
                             smem, qd);
+#ifdef GPF_WG_TRACE
+  {
+    const int tid = threadIdx.x;
+    GPF_PHASE(3);  // (trace build) this piece's GEMM done, before the reduction tree
+  }
+#else
+  (void)J;
+#endif
+#if GPF_SPLIT_RADIX == 4
+  const size_t eo = (size_t)(qd.rb + (qd.lane >> 4)) * T + qd.cb + (qd.lane & 15);  // this lane's first element
+  int span = 1;
+  for (int l = 0; span < S; ++l, span *= 4) {
+    const int nn = (S + span - 1) / span;  // nodes at this level
+    const int c = s / span, g0 = c & ~3, m0 = c - g0;
+    const int gm = nn - g0 < 4 ? nn - g0 : 4;  // nodes in this group
+    if (gm == 1) continue;                     // alone: go up
+    unsigned* tk = ct + l * 16 + (c >> 2);
+    unsigned* rdy = ct + SPLIT_TREE + l * 32 + g0;
+    __syncthreads();  // (the previous level's reads of *flag are done)
+    if (threadIdx.x == 0) *flag = (int)__hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*flag < gm - 1) {  // not the last: publish the node sum and leave
+      acc.store_wt(qd, pt + (size_t)c * span * T * T, T);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its part of the node sum
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_store(rdy + m0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __syncthreads();  // (every wave has read *flag)
+    if (threadIdx.x == 0) {  // the others took their tickets first: they are running
+      int n = 0, late = 0;
+      for (int m = 0; m < gm && !late; ++m) {
+        if (m == m0) continue;
+        while (__hip_atomic_load(rdy + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+          if (n++ >= spins) {
+            __hip_atomic_fetch_or(info, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            late = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      if (!late) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        for (int m = 0; m < gm; ++m)
+          if (m != m0) __hip_atomic_store(rdy + m, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      *flag = late;
+    }
+    __syncthreads();
+    if (*flag) return false;  // timed out: the host reports it
+    // ((n0 + n1) + (n2 + n3)), own node m0 from the registers; pairs without a partner pass through
+    const double* pn = launder(pt + (size_t)g0 * span * T * T + eo);
+    const size_t ns = (size_t)span * T * T;  // slot distance between neighbouring nodes
+#pragma unroll
+    for (int mi = 0; mi < Acc<T>::MBR; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < Acc<T>::MBC; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const size_t e = (size_t)(mi * 16 + 4 * r) * T + ni * 16;
+          const double own = acc.v[mi][ni][r];
+          const double pa = m0 < 2 ? own + pn[(1 - m0) * ns + e] : pn[e] + pn[ns + e];
+          double v = pa;
+          if (gm == 3) v = pa + (m0 == 2 ? own : pn[2 * ns + e]);
+          if (gm == 4) v = pa + (m0 >= 2 ? own + pn[(5 - m0) * ns + e] : pn[2 * ns + e] + pn[3 * ns + e]);
+          acc.v[mi][ni][r] = v;
+        }
+  }
+#else
   for (int l = 0; (1 << l) < S; ++l) {
     const int c = s >> l, sib = c ^ 1;
     if ((sib << l) >= S) continue;  // no sibling range at this level: go up alone
@@ -1100,6 +1181,7 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc.v[mi][ni][r] = acc.v[mi][ni][r] + p0[(mi * 16 + 4 * r) * T + ni * 16];
   }
+#endif
   return true;
 }
 
@@ -1188,7 +1270,7 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
       if (!split_part<false, true, true>(acc, Lp + (size_t)J * T * ld, Npad, Lp + (size_t)I * T * ld, Npad,
                                          J * T / DL_KC, Sx, sidx, pt, cnt + (size_t)(p * (nt - 1) + w) * SPLIT_CNT, lds,
                                          qd, sflag, info + p, spins,
-                                         [&](Acc<T>& a) { cov_tile_acc(a, qd, x, lp, d, N, J, I, lds); }))
+                                         [&](Acc<T>& a) { cov_tile_acc(a, qd, x, lp, d, N, J, I, lds); }, J))
         return;  // (the finisher's accumulators hold D)
     } else {
       cov_tile_acc(acc, qd, x, lp, d, N, J, I, lds);
@@ -1233,7 +1315,6 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
       syrk_tile<false>(Aii, ld, Aij, Npad, T, lds, qd);
     }
     GPF_PHASE(2);
-    GPF_PHASE(3);
     if (!ED && I == J + 1) {  // fused diagonal factor of block J+1 (A_II, y_I fully reduced)
       __syncthreads();
       const size_t poff = ((size_t)p * nt + I) * Npad + (size_t)I * T;
@@ -1254,7 +1335,7 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
       if (!split_part<true, false, false>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
                                           Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T / DL_KC, Sx, sidx,
                                           pt, cnt + (size_t)(p * (nt - 1) + w) * SPLIT_CNT, lds, qd, sflag, info + p,
-                                          spins, [](Acc<T>&) {}))
+                                          spins, [](Acc<T>&) {}, J))
         return;
     } else {
       acc.zero();

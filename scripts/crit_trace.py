@@ -77,7 +77,7 @@ u64p = ctypes.POINTER(ctypes.c_ulonglong)
 assert probe.gpf_debug_wg_trace(tr.ctypes.data_as(u64p), nt, W) == 0
 assert probe.gpf_debug_wg_phase(ph.ctypes.data_as(u64p), nt, W) == 0
 tot = 0.0
-print("J   span   | w0: pieces start..gemm-end (max)  finisher: trmm   syrk    dot    end   (us from launch start)")
+print("J   span   | w0: pieces start..gemm-end (max)  gemm-only (max, finisher)  finisher: trmm   syrk    end   (us from launch start)")
 for J in range(nt - 1):
     st, en = tr[J, :, 0].astype(np.int64), tr[J, :, 1].astype(np.int64)
     live = (st > 0) & (en >= st)
@@ -111,8 +111,10 @@ for J in range(nt - 1):
     fin = max(ids, key=lambda b: en[b])
     g_end = max(p0[b, 0] for b in ids if p0[b, 0] >= t0) if any(p0[b, 0] >= t0 for b in ids) else 0
     rel = lambda v: (v - t0) * 1e-2 if v >= t0 else float("nan")  # noqa: E731
+    g_only = max(p0[b, 3] for b in ids)
     print(f"{J:2d} {span:7.1f}   | {len(ids):2d} pieces {rel(min(st[b] for b in ids)):6.1f}..{rel(g_end):6.1f}"
-          f"   {rel(p0[fin, 1]):6.1f} {rel(p0[fin, 2]):6.1f} {rel(p0[fin, 3]):6.1f} {rel(en[fin]):6.1f}"
+          f"   {rel(g_only):6.1f} {rel(p0[fin, 3]):6.1f}"
+          f"   {rel(p0[fin, 1]):6.1f} {rel(p0[fin, 2]):6.1f} {rel(en[fin]):6.1f}"
           f"  |{dg}  last wg {last} ends {(en[last] - t0) * 1e-2:6.1f}")
 print(f"sum of launch spans {tot:.1f} us")
 ctx.close()
