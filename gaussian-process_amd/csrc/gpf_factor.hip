@@ -270,7 +270,8 @@ __device__ __forceinline__ bool f64b_column(double* sA, int la, int k, double* d
 // X_kk = L_kk^-1 of a 16x16 lower-triangular block (zeros above its diagonal in LDS): lane c
 // (c < 16) forward-substitutes column c, x_i = -(sum_{j<i} L_ij x_j) * dinv_i, x_c = dinv_c (the
 // [A | I] elimination's X_qq); the L entries are uniform LDS reads. One wave; writes zeros above
-// the diagonal of X_kk.
+// the diagonal of X_kk. (A column-oriented variant, every later row taking x_j's term at once,
+// spilled inside k_step.)
 __device__ __forceinline__ void f64b_inv(const double* sL, int la, double* sXo, int lx, const double* dv) {
   const int lane = threadIdx.x & 63, c = lane & 15;
   double x[16];
@@ -1040,18 +1041,12 @@ __device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, con
 // it with their covariance tile A_IJ, so the finisher does not compute it after the pieces, on
 // the critical path.
 // ----------------------------------------------------------------------------
-// Radix 4 (GPF_SPLIT_RADIX, default): the nodes meet in groups of up to 4 instead of pairs — the
-// first three arrivers store and leave, the last waits for their flags and forms the group's sum
-// in the binary tree's pairwise shape ((n0 + n1) + (n2 + n3)) with its own node taken from the
-// registers (commutativity again), so the sums are bitwise those of the radix-2 tree with half
-// the levels: the hand-offs, not the reads, set a level's cost (~9 us per level on the
-// prediction's critical tile, profiles/r3s2/crit_predict_tree.txt).
-#ifndef GPF_SPLIT_RADIX
-#define GPF_SPLIT_RADIX 2
-#endif
-static_assert(GPF_SPLIT_RADIX == 2 || GPF_SPLIT_RADIX == 4, "split-K tree radix");
-constexpr int SPLIT_TREE = 80;              // tickets per split tile: group k (< 16) of level l (< 5) at l * 16 + k
-constexpr int SPLIT_CNT = SPLIT_TREE + 96;  // + ready flags: radix 2: SPLIT_TREE + l * 16 + pair; radix 4: SPLIT_TREE + l * 32 + node
+// (A radix-4 tree — groups of up to 4 nodes, the last arriver forming ((n0 + n1) + (n2 + n3)),
+// bitwise these sums with half the levels — measured slower: factor 3.45 -> 3.73 ms, the
+// carrier's three 128 KiB reads per level cost more than the saved hand-offs;
+// profiles/r3s2/ab_split_tree_radix.txt.)
+constexpr int SPLIT_TREE = 80;              // tickets per split tile: pair (level l < 5, pair k < 16) at l * 16 + k
+constexpr int SPLIT_CNT = 2 * SPLIT_TREE;   // + the pairs' ready flags at SPLIT_TREE + l * 16 + k
 
 template <bool NN, bool NEG, bool SEEDED = false, typename Seed>
 __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int lda, const double* Bp, int ldb, int nch, int S,
@@ -1074,69 +1069,6 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
 #else
   (void)J;
 #endif
-#if GPF_SPLIT_RADIX == 4
-  const size_t eo = (size_t)(qd.rb + (qd.lane >> 4)) * T + qd.cb + (qd.lane & 15);  // this lane's first element
-  int span = 1;
-  for (int l = 0; span < S; ++l, span *= 4) {
-    const int nn = (S + span - 1) / span;  // nodes at this level
-    const int c = s / span, g0 = c & ~3, m0 = c - g0;
-    const int gm = nn - g0 < 4 ? nn - g0 : 4;  // nodes in this group
-    if (gm == 1) continue;                     // alone: go up
-    unsigned* tk = ct + l * 16 + (c >> 2);
-    unsigned* rdy = ct + SPLIT_TREE + l * 32 + g0;
-    __syncthreads();  // (the previous level's reads of *flag are done)
-    if (threadIdx.x == 0) *flag = (int)__hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (*flag < gm - 1) {  // not the last: publish the node sum and leave
-      acc.store_wt(qd, pt + (size_t)c * span * T * T, T);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its part of the node sum
-      __syncthreads();
-      if (threadIdx.x == 0) __hip_atomic_store(rdy + m0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-    __syncthreads();  // (every wave has read *flag)
-    if (threadIdx.x == 0) {  // the others took their tickets first: they are running
-      int n = 0, late = 0;
-      for (int m = 0; m < gm && !late; ++m) {
-        if (m == m0) continue;
-        while (__hip_atomic_load(rdy + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-          if (n++ >= spins) {
-            __hip_atomic_fetch_or(info, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            late = 1;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-        }
-      }
-      if (!late) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        for (int m = 0; m < gm; ++m)
-          if (m != m0) __hip_atomic_store(rdy + m, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      *flag = late;
-    }
-    __syncthreads();
-    if (*flag) return false;  // timed out: the host reports it
-    // ((n0 + n1) + (n2 + n3)), own node m0 from the registers; pairs without a partner pass through
-    const double* pn = launder(pt + (size_t)g0 * span * T * T + eo);
-    const size_t ns = (size_t)span * T * T;  // slot distance between neighbouring nodes
-#pragma unroll
-    for (int mi = 0; mi < Acc<T>::MBR; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < Acc<T>::MBC; ++ni)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const size_t e = (size_t)(mi * 16 + 4 * r) * T + ni * 16;
-          const double own = acc.v[mi][ni][r];
-          const double pa = m0 < 2 ? own + pn[(1 - m0) * ns + e] : pn[e] + pn[ns + e];
-          double v = pa;
-          if (gm == 3) v = pa + (m0 == 2 ? own : pn[2 * ns + e]);
-          if (gm == 4) v = pa + (m0 >= 2 ? own + pn[(5 - m0) * ns + e] : pn[2 * ns + e] + pn[3 * ns + e]);
-          acc.v[mi][ni][r] = v;
-        }
-  }
-#else
   for (int l = 0; (1 << l) < S; ++l) {
     const int c = s >> l, sib = c ^ 1;
     if ((sib << l) >= S) continue;  // no sibling range at this level: go up alone
@@ -1181,7 +1113,6 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc.v[mi][ni][r] = acc.v[mi][ni][r] + p0[(mi * 16 + 4 * r) * T + ni * 16];
   }
-#endif
   return true;
 }
 

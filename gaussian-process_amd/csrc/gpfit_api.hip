@@ -1153,19 +1153,12 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
       }
       ++wgs;
     }
-    // the split-K reduction tree (gpf::split_part): every group of node ranges has its own ticket
-    // and its members their ready flags, inside the tile's SPLIT_CNT counters
-    for (int lv = 0, span = 1; l.split != gpf::SPLIT_NONE && span < l.S2; ++lv, span *= GPF_SPLIT_RADIX) {
-      const int nn = (l.S2 + span - 1) / span;
-      for (int cn = 0; cn < nn; cn += GPF_SPLIT_RADIX) {
-        if (nn - cn < 2) continue;  // a lone node goes up without a hand-off
-        const int flag_hi = GPF_SPLIT_RADIX == 4 ? gpf::SPLIT_TREE + lv * 32 + std::min(nn, cn + 4) - 1
-                                                 : gpf::SPLIT_TREE + lv * 16 + cn / 2;
-        if (lv * 16 + cn / GPF_SPLIT_RADIX >= gpf::SPLIT_TREE || flag_hi >= gpf::SPLIT_CNT)
+    // the split-K reduction tree (gpf::split_part): every pair of node ranges has its own counter
+    for (int lv = 0; l.split != gpf::SPLIT_NONE && (1 << lv) < l.S2; ++lv)
+      for (int cn = 0; (cn << lv) < l.S2; cn += 2)
+        if (((cn + 1) << lv) < l.S2 && lv * 16 + (cn >> 1) >= gpf::SPLIT_TREE)
           return plan_fail(msg, msg_len, "J=%d: split factor %d needs more than %d tree counters", l.J, l.S2,
-                           gpf::SPLIT_CNT);
-      }
-    }
+                           gpf::SPLIT_TREE);
     for (int q = 0; q < l.gc; ++q) {
       if (diag[q] != l.ed) return plan_fail(msg, msg_len, "J=%d particle %d: %d diagonal workgroups", l.J, q, diag[q]);
       diag_wgs += diag[q];
