@@ -832,7 +832,7 @@ __host__ __device__ __forceinline__ void step_tile(int b, int P, int ntl, int gr
 }
 
 enum { SPLIT_NONE = 0, SPLIT_ALL = 1, SPLIT_CRIT = 2 };
-enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2, ROLE_DIAG = 3, ROLE_SYRK = 4 };
+enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2, ROLE_DIAG = 3, ROLE_SYRK = 4, ROLE_LA = 5 };
 
 // Early diagonal factor (k_step<SPLIT, ED = 1>; the host chooses it for launches that leave
 // workgroup slots idle): launch J starts with P extra workgroups that factor diagonal
@@ -880,8 +880,8 @@ __host__ __device__ __forceinline__ int split_all_pieces(int J, int w, int nt, i
 // range (piece sidx of S) of it, or nothing. The kernel and the host-side plan check
 // (gpf_plan_check) both decode through this function.
 template <int SPLIT>
-__host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt, int grp, int S, int ed, int sy, int& p,
-                                                    int& w, int& sidx) {
+__host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt, int grp, int S, int ed, int sy, int la,
+                                                    int& p, int& w, int& sidx) {
   const int tiles = P * (nt - 1);
   sidx = 0;
   if (ed) {
@@ -897,6 +897,14 @@ __host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt,
       p = b;
       w = -1;
       return ROLE_SYRK;
+    }
+    b -= P;
+  }
+  if (la) {
+    if (b < P) {
+      p = b;
+      w = -1;
+      return ROLE_LA;
     }
     b -= P;
   }
@@ -1155,6 +1163,26 @@ __device__ __forceinline__ void syrk_item(int J, int p, int Npad, double* __rest
   if (threadIdx.x == 0) __hip_atomic_store(yflag + p, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Look-ahead workgroup of launch J (ROLE_LA; launches with the early diagonal factor and no split,
+// 1 <= J <= nt-3): the next launch's critical tile (I = J+2 of block column J+1) over the columns
+// < J — its covariance seed and a depth-128J GEMM, everything except block column J, which this
+// launch is computing — to lab (plain stores, read after the launch boundary). Launch J+1's
+// critical tile then runs a single 128-deep block after loading it instead of the whole
+// depth-128(J+1) GEMM, so its chain is the diagonal factor, not its GEMM (config B: the chain of
+// J >= 4 was that GEMM, profiles/r3s2/crit_B_*.txt). Bitwise the same accumulation.
+__device__ __forceinline__ void la_item(int J, int p, int Npad, const double* __restrict__ Lb, int N,
+                                        const double* __restrict__ x, const double* __restrict__ ls, int d,
+                                        double* __restrict__ lab, double* lds) {
+  const size_t ld = (size_t)Npad;
+  const double* Lp = Lb + (size_t)p * ld * ld;
+  const Quad<T> qd;
+  Acc<T> acc;
+  cov_tile_acc(acc, qd, x, ls + (size_t)p * d, d, N, J + 1, J + 2, lds);
+  gemm_stream_dl<false, true>(acc, Lp + (size_t)(J + 1) * T * ld, Npad, Lp + (size_t)(J + 2) * T * ld, Npad, J * T, lds,
+                              qd);
+  acc.store(qd, lab + (size_t)p * T * T, T);
+}
+
 // Tile w of block column J of particle p (the unit of work of k_step); role from step_decode.
 //   L tile (I = J+1+w):  D = A_IJ^T - L_J,<J L_I,<J^T  (the transposed panel C^T, so that each
 //                        wave holds all 128 k of the triangular multiply for its 16 rows of C)
@@ -1171,7 +1199,7 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
                                           const double* __restrict__ ls, int d, int S, int S2, int sidx,
                                           double* __restrict__ part, unsigned* __restrict__ cnt, int* sflag,
                                           const int* __restrict__ dflag, const int* __restrict__ yflag, int defer,
-                                          int spins, double* lds) {
+                                          int spins, int la, const double* __restrict__ lab, double* lds) {
   const int tid = threadIdx.x;
   const int nL = nt - 1 - J;
   const size_t ld = (size_t)Npad;
@@ -1203,6 +1231,12 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
                                          qd, sflag, info + p, spins,
                                          [&](Acc<T>& a) { cov_tile_acc(a, qd, x, lp, d, N, J, I, lds); }, J))
         return;  // (the finisher's accumulators hold D)
+    } else if (SPLIT == SPLIT_NONE && ED && (la & 2) && I == J + 1) {
+      // look-ahead seed: launch J-1's LA workgroup left this tile's GEMM over the columns < J-1
+      // (cov seed included); only block column J-1 remains — the same MFMAs in the same order
+      acc.load(qd, lab + (size_t)p * T * T, T);
+      gemm_stream_dl<false, true>(acc, Lp + (size_t)J * T * ld + (size_t)(J - 1) * T, Npad,
+                                  Lp + (size_t)I * T * ld + (size_t)(J - 1) * T, Npad, T, lds, qd);
     } else {
       cov_tile_acc(acc, qd, x, lp, d, N, J, I, lds);
       if (J > 0)
@@ -1328,7 +1362,8 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
                                                   const double* __restrict__ x, const double* __restrict__ ls,
                                                   int d, int S, int S2, double* __restrict__ part,
                                                   unsigned* __restrict__ cnt, int* __restrict__ dflag, int ed,
-                                                  int* __restrict__ yflag, int defer, int sy, int spins) {
+                                                  int* __restrict__ yflag, int defer, int sy, int spins, int la,
+                                                  double* __restrict__ lab) {
   const int tid = threadIdx.x;
 #ifdef GPF_WG_TRACE
   if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) {
@@ -1347,13 +1382,15 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
   if (__builtin_amdgcn_readfirstlane(tid >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
   int p, w, sidx;
-  const int role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, SPLIT != SPLIT_ALL && sy, p, w, sidx);
+  const int role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, SPLIT != SPLIT_ALL && sy,
+                                      SPLIT == SPLIT_NONE && ED && (la & 1), p, w, sidx);
 #ifdef GPF_CHECK
   // diagnostic build (-DGPF_CHECK): every index the workgroup derives its addresses from, checked
   // against the launch's extents before any access (an out-of-range role prints and does nothing)
   {
     bool ok = p >= 0 && p < P && J >= 0 && J < nt && Npad == nt * T && S >= 1 && S2 >= 1 && S2 <= SPLIT_MAXS;
     if (role == ROLE_SYRK) ok = ok && w == -1 && J >= 1 && J <= nt - 2 && yflag != nullptr;
+    else if (role == ROLE_LA) ok = ok && w == -1 && J >= 1 && J + 2 < nt && lab != nullptr;
     else if (role == ROLE_DIAG) ok = ok && w == -1 && ED && dflag != nullptr;
     else if (role != ROLE_IDLE) ok = ok && w >= 0 && w < nt - 1 && sidx >= 0 &&
                                      sidx < (SPLIT == SPLIT_ALL ? split_all_pieces(J, w, nt, S) : S) && sidx < S2 &&
@@ -1374,6 +1411,8 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
 #endif
   if (SPLIT != SPLIT_ALL && role == ROLE_SYRK) {
     syrk_item(J, p, Npad, Lb, yflag, lds);
+  } else if (SPLIT == SPLIT_NONE && ED && role == ROLE_LA) {
+    la_item(J, p, Npad, Lb, N, x, ls, d, lab, lds);
   } else if (ED && role == ROLE_DIAG) {
     // diagonal block J of particle p (fully reduced by the previous launches' look-ahead): factor,
     // then publish to this launch's tiles (write-through stores drained, then the flag)
@@ -1388,7 +1427,7 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
                     carve_diag(lds, lds + DIAG_BASE), J * T + H >= N, dflag + p, J);
   } else {
     step_item<SPLIT, ED>(role, J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, S2, sidx, part, cnt, &sflag,
-                         dflag, yflag, defer, spins, lds);
+                         dflag, yflag, defer, spins, la, lab, lds);
   }
 #ifdef GPF_WG_TRACE
   __syncthreads();

@@ -80,6 +80,8 @@ struct gpf_ctx {
   double* d_part = nullptr;    // split-K partial products (run_factor, few tiles per launch)
   unsigned* d_cnt = nullptr;   // split-K arrival counters, one per (particle, tile), kept zero
   size_t part_cap = 0, cnt_cap = 0;
+  double* d_la = nullptr;      // look-ahead partials of the next critical tiles (gpf::la_item), one tile per particle
+  size_t la_cap = 0;
   double* d_szp = nullptr;
   double* d_ls = nullptr;
   double* d_mu = nullptr;
@@ -231,6 +233,9 @@ static void free_work(gpf_ctx* c) {
   c->d_part = nullptr;
   c->d_cnt = nullptr;
   c->part_cap = c->cnt_cap = 0;
+  hipFree(c->d_la);
+  c->d_la = nullptr;
+  c->la_cap = 0;
   c->d_L = c->d_U = c->d_yb = c->d_s2p = c->d_szp = c->d_ls = c->d_mu = c->d_sd = c->d_loss = nullptr;
   c->d_info = nullptr;
   c->d_hist = nullptr;
@@ -377,6 +382,18 @@ static bool defer_syrk() {
   return on;
 }
 
+// Look-ahead of the critical tile (gpf::la_item) for launches with the early diagonal factor and
+// no split: launch J (1 <= J <= nt-3) also runs the next critical tile's GEMM over the columns
+// < J, and launch J+1's critical tile finishes it with one 128-deep block. There the launch's
+// chain was that tile's depth-128J GEMM once it outgrew the diagonal factor (config B from J = 4).
+// Slot-bound launches (config C, the fused factor) gain nothing from moving work between launches.
+// GPF_LOOKAHEAD = 0/1 overrides.
+static bool look_ahead(int pc, int nt) {
+  bool on = false;  // (opt-in until measured on the GPU)
+  if (const char* s = getenv("GPF_LOOKAHEAD")) on = atoi(s) != 0;
+  return on && nt >= 4;
+}
+
 // Bound of the early-diagonal hand-off spin (gpf::wait_diag, polls of ~1 us): ~2 s by default;
 // GPF_WAIT_SPINS lowers it to exercise the timeout report (tests/test_gpu.py).
 static int wait_spins() {
@@ -473,6 +490,7 @@ struct StepLaunch {
   int J, g, p0, gc, split, S, S2, grp, ed;  // S: pieces per split tile (SPLIT_ALL: chunks per piece); S2: partial
                                             // slots per tile; ed: the launch starts with gc diagonal workgroups
   int defer, sy;                        // deferred diagonal update; sy: gc SYRK workgroups follow
+  int la;  // look-ahead: bit 0: gc LA workgroups follow (gpf::la_item); bit 1: the critical tiles seed from launch J-1's
   unsigned grid;
   size_t part_off, cnt_off;
 };
@@ -497,9 +515,15 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
       l.ed = ed ? 1 : 0;
       l.defer = (S == 1 && defer_syrk()) ? 1 : 0;  // the all-tile split keeps the per-tile look-ahead
       l.sy = (l.defer && J >= 1 && J <= nt - 2) ? 1 : 0;
+      // look-ahead: launch J-1 of this group must have run unsplit too (its LA workgroups)
+      const bool la_ok = look_ahead(pc, nt) && l.ed && l.split == gpf::SPLIT_NONE;
+      const bool prev_none = J >= 1 && (S > 1 ? false : split_crit(pc, nt, J - 1, l.grp, S) <= 1);
+      const bool next_none = S > 1 ? false : split_crit(pc, nt, J + 1, l.grp, S) <= 1;
+      l.la = ((la_ok && next_none && J >= 1 && J <= nt - 3) ? 1 : 0) | ((la_ok && prev_none && J >= 2 && J <= nt - 2) ? 2 : 0);
       int nall = 0;
       for (int w = 0; S > 1 && w < nt - 1; ++w) nall += gpf::split_all_pieces(J, w, nt, l.S);
-      l.grid = (S > 1 ? l.gc * nall : l.gc * (nt - 1) + l.gc * (Sc - 1)) + (l.ed ? l.gc : 0) + (l.sy ? l.gc : 0);
+      l.grid = (S > 1 ? l.gc * nall : l.gc * (nt - 1) + l.gc * (Sc - 1)) + (l.ed ? l.gc : 0) + (l.sy ? l.gc : 0) +
+               ((l.la & 1) ? l.gc : 0);
       // one set of partial slots per group: groups run concurrently
       l.part_off = (size_t)l.p0 * (nt - 1) * Smax * T * T;
       l.cnt_off = (size_t)l.p0 * (nt - 1) * gpf::SPLIT_CNT;
@@ -582,6 +606,16 @@ static int run_factor(gpf_ctx* c, int pc) {
   // block-column launches (split-K for launches with few tiles, planned above)
   std::vector<StepLaunch> plan;
   step_plan(pc, nt, S, Smax, plan);
+  bool any_la = false;
+  for (const StepLaunch& l : plan) any_la = any_la || l.la != 0;
+  if (any_la && (size_t)pc * T * T * 8 > c->la_cap) {  // (never under a graph capture: nt >= 4 only)
+    clear_graphs(c);
+    hipFree(c->d_la);
+    c->d_la = nullptr;
+    c->la_cap = 0;
+    GPF_HIP(c, hipMalloc(&c->d_la, (size_t)pc * T * T * 8));
+    c->la_cap = (size_t)pc * T * T * 8;
+  }
   for (const StepLaunch& l : plan) {
     const double fl = step_flops(l.J);
     const int p0 = l.p0, gc = l.gc;
@@ -596,7 +630,7 @@ static int run_factor(gpf_ctx* c, int pc) {
                          c->d_U + (size_t)p0 * ld * ld, c->d_yb + (size_t)p0 * ld, c->d_s2p + (size_t)p0 * nt * ld,
                          c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc, l.grp, N, c->d_x,
                          c->d_ls + (size_t)p0 * c->d, c->d, l.S, l.S2, partg, cntg, c->d_flag + p0, l.ed,
-                         c->d_cflag + p0, l.defer, l.sy, spins);
+                         c->d_cflag + p0, l.defer, l.sy, spins, l.la, l.la ? c->d_la + (size_t)p0 * T * T : nullptr);
     });
     if (rc) return rc;
     total += fl * gc;
@@ -1095,6 +1129,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
   long long wgs = 0, whole_tiles = 0, split_tiles = 0;
   std::vector<int> whole, piece, diag, syrk;
   long long diag_wgs = 0, syrk_wgs = 0;
+  std::vector<int> la_prev(MAX_GROUPS, 0);
   if ((int)plan.size() != (nt > 1 ? nt * ng : 0)) return plan_fail(msg, msg_len, "plan has %d launches, want %d",
                                                               (int)plan.size(), nt * ng);
   for (const StepLaunch& l : plan) {
@@ -1115,15 +1150,31 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
       return plan_fail(msg, msg_len, "J=%d: SYRK workgroups without a diagonal block to reduce", l.J);
     if (l.defer && l.split == gpf::SPLIT_ALL)
       return plan_fail(msg, msg_len, "J=%d: deferred diagonal update under the all-tile split", l.J);
+    // look-ahead: LA workgroups only where a next critical tile exists, no split, early diagonal
+    // factor; a seeded launch follows a launch of the same group that ran them
+    if (l.la && (l.split != gpf::SPLIT_NONE || !l.ed || ((l.la & 1) && (l.J < 1 || l.J > nt - 3)) ||
+                 ((l.la & 2) && (l.J < 2 || l.J > nt - 2 || !(la_prev[l.g] & 1)))))
+      return plan_fail(msg, msg_len, "J=%d g=%d: look-ahead bits %d out of place", l.J, l.g, l.la);
+    if ((la_prev[l.g] & 1) && !(l.la & 2))
+      return plan_fail(msg, msg_len, "J=%d g=%d: look-ahead partials of launch J-1 left unused", l.J, l.g);
+    la_prev[l.g] = l.la;
+    std::vector<int> lawg((size_t)l.gc, 0);
     for (unsigned b = 0; b < l.grid; ++b) {
       int p = -1, w = -1, sidx = -1;
       const int role =
-          l.split == gpf::SPLIT_ALL    ? gpf::step_decode<gpf::SPLIT_ALL>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, 0, p, w, sidx)
-          : l.split == gpf::SPLIT_CRIT ? gpf::step_decode<gpf::SPLIT_CRIT>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.sy, p, w, sidx)
-                                       : gpf::step_decode<gpf::SPLIT_NONE>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.sy, p, w, sidx);
+          l.split == gpf::SPLIT_ALL    ? gpf::step_decode<gpf::SPLIT_ALL>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, 0, 0, p, w, sidx)
+          : l.split == gpf::SPLIT_CRIT ? gpf::step_decode<gpf::SPLIT_CRIT>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.sy, 0, p, w, sidx)
+                                       : gpf::step_decode<gpf::SPLIT_NONE>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.sy,
+                                                                           l.la & 1, p, w, sidx);
       if (role == gpf::ROLE_DIAG) {  // one diagonal workgroup per particle, ahead of every tile of the launch
         if (!l.ed || p < 0 || p >= l.gc || (unsigned)p != b || diag[p]++)
           return plan_fail(msg, msg_len, "J=%d block %u: misplaced or duplicate diagonal workgroup (p=%d)", l.J, b, p);
+        ++wgs;
+        continue;
+      }
+      if (role == gpf::ROLE_LA) {  // one per particle, right behind the diagonal and SYRK workgroups
+        if (!(l.la & 1) || p < 0 || p >= l.gc || (unsigned)p + (l.ed ? l.gc : 0) + (l.sy ? l.gc : 0) != b || lawg[p]++)
+          return plan_fail(msg, msg_len, "J=%d block %u: misplaced or duplicate look-ahead workgroup (p=%d)", l.J, b, p);
         ++wgs;
         continue;
       }
@@ -1163,6 +1214,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
       if (diag[q] != l.ed) return plan_fail(msg, msg_len, "J=%d particle %d: %d diagonal workgroups", l.J, q, diag[q]);
       diag_wgs += diag[q];
       if (syrk[q] != l.sy) return plan_fail(msg, msg_len, "J=%d particle %d: %d SYRK workgroups", l.J, q, syrk[q]);
+      if (lawg[q] != (l.la & 1)) return plan_fail(msg, msg_len, "J=%d particle %d: %d look-ahead workgroups", l.J, q, lawg[q]);
       syrk_wgs += syrk[q];
     }
     for (int t = 0; t < tiles; ++t) {
