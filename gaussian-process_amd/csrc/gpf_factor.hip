@@ -1163,13 +1163,25 @@ __device__ __forceinline__ void syrk_item(int J, int p, int Npad, double* __rest
   if (threadIdx.x == 0) __hip_atomic_store(yflag + p, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Look-ahead workgroup of launch J (ROLE_LA; launches with the early diagonal factor and no split,
-// 1 <= J <= nt-3): the next launch's critical tile (I = J+2 of block column J+1) over the columns
+// Look-ahead of launch J (launches with the early diagonal factor and no split, 1 <= J <= nt-3),
+// run by the launch's SYRK workgroup after it has published its block (both GEMMs stream the same
+// row panel L_{J+1,<J}; a workgroup of its own, ROLE_LA, only without the deferred update — an
+// extra workgroup per particle pushed the diagonal factor onto shared CUs): the next launch's critical tile (I = J+2 of block column J+1) over the columns
 // < J — its covariance seed and a depth-128J GEMM, everything except block column J, which this
 // launch is computing — to lab (plain stores, read after the launch boundary). Launch J+1's
 // critical tile then runs a single 128-deep block after loading it instead of the whole
 // depth-128(J+1) GEMM, so its chain is the diagonal factor, not its GEMM (config B: the chain of
 // J >= 4 was that GEMM, profiles/r3s2/crit_B_*.txt). Bitwise the same accumulation.
+// How far the look-ahead of launch J goes: the first la_chunks(J) 16-deep chunks (of the 8J the
+// columns < J hold). The SYRK workgroup that runs it spends ~9/16 of a depth-128J GEMM on its own
+// lower-triangular update first, so it takes ~7/16 of the depth and the critical tile of launch
+// J+1 continues from there: both then end near the launch's other deep L tiles (a look-ahead
+// over the whole depth made that workgroup the launch's last, profiles/r3s2/ab_lookahead_B.txt).
+#ifndef GPF_LA_FRAC16
+#define GPF_LA_FRAC16 7
+#endif
+__host__ __device__ __forceinline__ int la_chunks(int J) { return GPF_LA_FRAC16 * 8 * J / 16; }
+
 __device__ __forceinline__ void la_item(int J, int p, int Npad, const double* __restrict__ Lb, int N,
                                         const double* __restrict__ x, const double* __restrict__ ls, int d,
                                         double* __restrict__ lab, double* lds) {
@@ -1178,8 +1190,8 @@ __device__ __forceinline__ void la_item(int J, int p, int Npad, const double* __
   const Quad<T> qd;
   Acc<T> acc;
   cov_tile_acc(acc, qd, x, ls + (size_t)p * d, d, N, J + 1, J + 2, lds);
-  gemm_stream_dl<false, true>(acc, Lp + (size_t)(J + 1) * T * ld, Npad, Lp + (size_t)(J + 2) * T * ld, Npad, J * T, lds,
-                              qd);
+  gemm_stream_dl<false, true>(acc, Lp + (size_t)(J + 1) * T * ld, Npad, Lp + (size_t)(J + 2) * T * ld, Npad,
+                              la_chunks(J) * DL_KC, lds, qd);
   acc.store(qd, lab + (size_t)p * T * T, T);
 }
 
@@ -1232,11 +1244,12 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
                                          [&](Acc<T>& a) { cov_tile_acc(a, qd, x, lp, d, N, J, I, lds); }, J))
         return;  // (the finisher's accumulators hold D)
     } else if (SPLIT == SPLIT_NONE && ED && (la & 2) && I == J + 1) {
-      // look-ahead seed: launch J-1's LA workgroup left this tile's GEMM over the columns < J-1
-      // (cov seed included); only block column J-1 remains — the same MFMAs in the same order
+      // look-ahead seed: launch J-1 left this tile's GEMM over its first la_chunks(J-1) chunks (cov
+      // seed included); the rest follows — the same MFMAs in the same order
+      const int k0 = la_chunks(J - 1) * DL_KC;  // where launch J-1's look-ahead stopped
       acc.load(qd, lab + (size_t)p * T * T, T);
-      gemm_stream_dl<false, true>(acc, Lp + (size_t)J * T * ld + (size_t)(J - 1) * T, Npad,
-                                  Lp + (size_t)I * T * ld + (size_t)(J - 1) * T, Npad, T, lds, qd);
+      gemm_stream_dl<false, true>(acc, Lp + (size_t)J * T * ld + k0, Npad, Lp + (size_t)I * T * ld + k0, Npad, J * T - k0,
+                                  lds, qd);
     } else {
       cov_tile_acc(acc, qd, x, lp, d, N, J, I, lds);
       if (J > 0)
@@ -1383,7 +1396,7 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
 #endif
   int p, w, sidx;
   const int role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, SPLIT != SPLIT_ALL && sy,
-                                      SPLIT == SPLIT_NONE && ED && (la & 1), p, w, sidx);
+                                      SPLIT == SPLIT_NONE && ED && (la & 1) && !sy, p, w, sidx);
 #ifdef GPF_CHECK
   // diagnostic build (-DGPF_CHECK): every index the workgroup derives its addresses from, checked
   // against the launch's extents before any access (an out-of-range role prints and does nothing)
@@ -1411,6 +1424,10 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
 #endif
   if (SPLIT != SPLIT_ALL && role == ROLE_SYRK) {
     syrk_item(J, p, Npad, Lb, yflag, lds);
+    if (SPLIT == SPLIT_NONE && ED && (la & 1)) {  // the look-ahead rides on the SYRK workgroup (after its flag)
+      __syncthreads();
+      la_item(J, p, Npad, Lb, N, x, ls, d, lab, lds);
+    }
   } else if (SPLIT == SPLIT_NONE && ED && role == ROLE_LA) {
     la_item(J, p, Npad, Lb, N, x, ls, d, lab, lds);
   } else if (ED && role == ROLE_DIAG) {

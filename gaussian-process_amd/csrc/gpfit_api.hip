@@ -383,13 +383,15 @@ static bool defer_syrk() {
 }
 
 // Look-ahead of the critical tile (gpf::la_item) for launches with the early diagonal factor and
-// no split: launch J (1 <= J <= nt-3) also runs the next critical tile's GEMM over the columns
-// < J, and launch J+1's critical tile finishes it with one 128-deep block. There the launch's
-// chain was that tile's depth-128J GEMM once it outgrew the diagonal factor (config B from J = 4).
+// no split: launch J (1 <= J <= nt-3) also runs the first ~7/16 of the next critical tile's GEMM
+// (on its SYRK workgroups), and launch J+1's critical tile continues from there. There the
+// launch's chain was that tile's depth-128J GEMM once it outgrew the diagonal factor (config B
+// from J = 4): same box, B 33.8k -> 36.1k evals/s, launch spans 743 -> 687 us
+// (profiles/r3s2/ab_lookahead_B.txt).
 // Slot-bound launches (config C, the fused factor) gain nothing from moving work between launches.
 // GPF_LOOKAHEAD = 0/1 overrides.
 static bool look_ahead(int pc, int nt) {
-  bool on = false;  // (opt-in until measured on the GPU)
+  bool on = early_diag(pc, nt);
   if (const char* s = getenv("GPF_LOOKAHEAD")) on = atoi(s) != 0;
   return on && nt >= 4;
 }
@@ -523,7 +525,7 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
       int nall = 0;
       for (int w = 0; S > 1 && w < nt - 1; ++w) nall += gpf::split_all_pieces(J, w, nt, l.S);
       l.grid = (S > 1 ? l.gc * nall : l.gc * (nt - 1) + l.gc * (Sc - 1)) + (l.ed ? l.gc : 0) + (l.sy ? l.gc : 0) +
-               ((l.la & 1) ? l.gc : 0);
+               ((l.la & 1) && !l.sy ? l.gc : 0);  // (with SYRK workgroups the look-ahead rides on them)
       // one set of partial slots per group: groups run concurrently
       l.part_off = (size_t)l.p0 * (nt - 1) * Smax * T * T;
       l.cnt_off = (size_t)l.p0 * (nt - 1) * gpf::SPLIT_CNT;
@@ -1165,7 +1167,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
           l.split == gpf::SPLIT_ALL    ? gpf::step_decode<gpf::SPLIT_ALL>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, 0, 0, p, w, sidx)
           : l.split == gpf::SPLIT_CRIT ? gpf::step_decode<gpf::SPLIT_CRIT>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.sy, 0, p, w, sidx)
                                        : gpf::step_decode<gpf::SPLIT_NONE>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.sy,
-                                                                           l.la & 1, p, w, sidx);
+                                                                           (l.la & 1) && !l.sy, p, w, sidx);
       if (role == gpf::ROLE_DIAG) {  // one diagonal workgroup per particle, ahead of every tile of the launch
         if (!l.ed || p < 0 || p >= l.gc || (unsigned)p != b || diag[p]++)
           return plan_fail(msg, msg_len, "J=%d block %u: misplaced or duplicate diagonal workgroup (p=%d)", l.J, b, p);
@@ -1173,7 +1175,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
         continue;
       }
       if (role == gpf::ROLE_LA) {  // one per particle, right behind the diagonal and SYRK workgroups
-        if (!(l.la & 1) || p < 0 || p >= l.gc || (unsigned)p + (l.ed ? l.gc : 0) + (l.sy ? l.gc : 0) != b || lawg[p]++)
+        if (!(l.la & 1) || l.sy || p < 0 || p >= l.gc || (unsigned)p + (l.ed ? l.gc : 0) != b || lawg[p]++)
           return plan_fail(msg, msg_len, "J=%d block %u: misplaced or duplicate look-ahead workgroup (p=%d)", l.J, b, p);
         ++wgs;
         continue;
@@ -1214,7 +1216,8 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
       if (diag[q] != l.ed) return plan_fail(msg, msg_len, "J=%d particle %d: %d diagonal workgroups", l.J, q, diag[q]);
       diag_wgs += diag[q];
       if (syrk[q] != l.sy) return plan_fail(msg, msg_len, "J=%d particle %d: %d SYRK workgroups", l.J, q, syrk[q]);
-      if (lawg[q] != (l.la & 1)) return plan_fail(msg, msg_len, "J=%d particle %d: %d look-ahead workgroups", l.J, q, lawg[q]);
+      if (lawg[q] != ((l.la & 1) && !l.sy ? 1 : 0))
+        return plan_fail(msg, msg_len, "J=%d particle %d: %d look-ahead workgroups", l.J, q, lawg[q]);
       syrk_wgs += syrk[q];
     }
     for (int t = 0; t < tiles; ++t) {

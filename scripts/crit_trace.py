@@ -98,8 +98,8 @@ for J in range(nt - 1):
         ids = [b for b in range(ed, ed + np0 * P, P) if live[b]]
     else:  # critical-tile split (csrc/gpfit_api.hip split_crit, off by default): pieces at b = off + s * P
         off = ed + (P if (plan["syrk_workgroups"] > 0 and 1 <= J <= nt - 2) else 0)
-        if os.environ.get("GPF_LOOKAHEAD", "0") != "0" and ed and 1 <= J <= nt - 3:
-            off += P  # look-ahead workgroups (gpf::la_item) right behind the SYRK workgroups
+        if os.environ.get("GPF_LOOKAHEAD", "0") != "0" and ed and 1 <= J <= nt - 3 and plan["syrk_workgroups"] == 0:
+            off += P  # look-ahead workgroups of their own (gpf::la_item; with SYRK workgroups it rides on them)
         S = 1 if (J == 0 or J >= nt - 1 or nt < 4) else min(int(os.environ.get("GPF_SPLIT_CRIT", 1)), max(1, J * T // 16 // 16))
         while S > 1 and P * (nt - 1) + P * (S - 1) + off > 512:
             S -= 1
