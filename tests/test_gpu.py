@@ -648,6 +648,42 @@ def test_configE_share_two_groups_vs_reference(ctx, monkeypatch):
     _reference_share(ctx, monkeypatch, fx, P, slots)
 
 
+@pytest.mark.parametrize("N,d,P", [(1024, 2, 12), (2048, 3, 32)])
+def test_critical_tile_lookahead_bitwise(ctx, monkeypatch, N, d, P):
+    """The critical-tile look-ahead (gpf::la_item: launch J's SYRK workgroups run the first 7/16 of
+    the next critical tile's GEMM, launch J+1 continues from the stored partial; on by default for
+    early-diagonal launches without split) runs the same MFMAs in the same order as the unsplit
+    tile: scores, mean and sd bitwise equal with it off (GPF_LOOKAHEAD=0), on one particle group
+    (N=1024, 12 particles) and on two concurrent groups (N=2048, 32 particles: 2 x 16, each with
+    its own look-ahead partials), and the two-group schedule bitwise equal to one group."""
+    import gpfit
+    rng = np.random.default_rng(N + P + 7)
+    x = rng.uniform(size=(d, N))
+    y = np.cos(4 * x[0]) + x[-1] + 0.1 * rng.standard_normal(N)
+    e = rng.uniform(0.05, 0.2, size=N)
+    s, ex = ref_cpu.sigma_grid()
+    lo, hi = ref_cpu.search_bounds(x)
+    ctx.set_data(x, y, e)
+    ctx.set_grid(s, ex, lo, hi)
+    Q = rng.uniform(0.1, 0.5, size=(P, d))
+    st = gpfit.plan_check(P, -(-N // 128))
+    assert st["diag_workgroups"] > 0 and st["S"] == 1  # the early-diagonal, unsplit schedule
+    on = ctx.eval_batch(Q, want_mu_sd=True)
+    monkeypatch.setenv("GPF_LOOKAHEAD", "0")
+    off = ctx.eval_batch(Q, want_mu_sd=True)
+    monkeypatch.delenv("GPF_LOOKAHEAD")
+    for a, b in zip(on, off):
+        np.testing.assert_array_equal(a, b)
+    if P >= 16:
+        monkeypatch.setenv("GPF_GROUPS", "1")
+        one = ctx.eval_batch(Q, want_mu_sd=True)
+        monkeypatch.delenv("GPF_GROUPS")
+        for a, b in zip(on, one):
+            np.testing.assert_array_equal(a, b)
+    mo, so = ref_cpu.GP_train_identity(x, y, e, Q[0])
+    assert _rel(on[1][0], mo) < RTOL_MU_SD and _rel(on[2][0], so) < RTOL_MU_SD
+
+
 @pytest.mark.parametrize("N,d,P", [(1000, 2, 12), (2049, 3, 5), (4096, 3, 1)])
 def test_early_diagonal_factor_matches_fused(ctx, monkeypatch, N, d, P):
     """The early diagonal factor (k_step<SPLIT, 1>: block J factored by extra workgroups at the
