@@ -64,27 +64,36 @@ def config_letter(N, d, swarm, hetero):
     return "custom"
 
 
+def _profile_order(f):
+    """Sort key of a committed profile file: round directory (r1 < r3 < r3s2 < r4), then the
+    evidence version of the file name (v5_ < v8_ < v12_), so the last match is the newest tree's."""
+    import re
+    rd = re.match(r"r(\d+)(?:s(\d+))?$", f.parent.name)
+    vm = re.match(r"v(\d+)", f.name)
+    return (int(rd.group(1)) if rd else -1, int(rd.group(2) or 0) if rd else 0, int(vm.group(1)) if vm else -1, f.name)
+
+
 def pmc_traffic(N, d, swarm):
-    """HBM bytes per k_step launch from the committed rocprofv3 PMC passes
-    (scripts/pmc_traffic.py writes profiles/<round>/k_step_traffic.json), or None."""
+    """HBM bytes per k_step launch from the newest committed rocprofv3 PMC passes
+    (scripts/pmc_traffic.py writes profiles/<round>/[vK_]k_step_traffic.json), or None."""
     best = None
-    for f in sorted((ROOT / "profiles").glob("*/k_step_traffic.json")):
+    for f in sorted((ROOT / "profiles").glob("*/*k_step_traffic.json"), key=_profile_order):
         try:
             t = json.loads(f.read_text())
         except (OSError, ValueError):
             continue
         if t.get("N") == N and t.get("d") == d and t.get("swarm") == swarm:
             best = {"bytes_per_launch": t["bytes_per_launch"], "source": str(f.relative_to(ROOT)),
-                    "groups": t.get("particle_groups", 1)}
+                    "groups": t.get("particle_groups", 1), "per": t.get("per")}
     return best
 
 
 def secondary_pmc():
     """rocprofv3 PMC summary of the secondary kernels from the latest committed
-    profiles/<round>/secondary_pmc.json (scripts/gpu_r3_secondary.sh + scripts/pmc_secondary.py,
+    profiles/<round>/secondary_pmc.json (scripts/gpu_secondary.sh + scripts/pmc_secondary.py,
     the bench's own secondary calls), or None."""
     best = None
-    for f in sorted((ROOT / "profiles").glob("*/secondary_pmc.json")):
+    for f in sorted((ROOT / "profiles").glob("*/*secondary_pmc.json"), key=_profile_order):
         try:
             best = (json.loads(f.read_text()), str(f.relative_to(ROOT)))
         except (OSError, ValueError):
@@ -181,8 +190,17 @@ def predict_line(ctx, x, y, e, N, d, args):
     xf = rng.uniform(size=(d, M))
     ls = np.full(d, 0.3)
     ctx.predict(ls, xf)  # warm-up (workspace, code objects)
-    runs = []  # three timed calls; the median by wall time is reported (one call is ~10 ms, so a
-    for _ in range(3):  # single sample is at the mercy of host-side stalls)
+    ctx.set_profiling(False)
+    walls = []  # `ms`: five unprofiled calls (no HIP events in the stream), the median reported
+    for _ in range(5):
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        ctx.predict(ls, xf)
+        ctx.synchronize()
+        walls.append(time.perf_counter() - t0)
+    dt = sorted(walls)[2]
+    runs = []  # the kernel breakdown: three more calls with an event pair around every launch
+    for _ in range(3):
         ctx.reset_profile()
         ctx.set_profiling(True)
         ctx.synchronize()
@@ -191,9 +209,11 @@ def predict_line(ctx, x, y, e, N, d, args):
         ctx.synchronize()
         runs.append((time.perf_counter() - t0, ctx.profile()))
         ctx.set_profiling(False)
-    dt, prof = sorted(runs, key=lambda r: r[0])[1]
+    pdt, prof = sorted(runs, key=lambda r: r[0])[1]
     out = {"N": N, "d": d, "M": M, "ms": dt * 1e3, "points_per_s": M / dt,
-           "ms_runs": [round(r[0] * 1e3, 3) for r in runs],
+           "ms_runs": [round(w * 1e3, 3) for w in walls],
+           "ms_profiled_pass": pdt * 1e3,
+           "factor_flops": (2.0 / 3.0) * (-(-N // 128) * 128) ** 3,
            "factor_ms": prof["factor_wall_ms"],
            "k_predict_vsq_ms": prof["predict_ms"],
            "k_predict_vsq_tflops": prof["predict_flops"] / (prof["predict_ms"] * 1e-3) / 1e12
@@ -202,7 +222,11 @@ def predict_line(ctx, x, y, e, N, d, args):
            if prof["predict_cov_ms"] > 0 else None,
            "k_cross_cov_hbm_frac": prof["predict_cov_bytes"] / (prof["predict_cov_ms"] * 1e-3) / 8e12
            if prof["predict_cov_ms"] > 0 else None,
-           "note": "wall time (median of 3 calls) includes the single-particle factorisation and host<->device copies"}
+           "other_ms_profiled": pdt * 1e3 - prof["factor_wall_ms"] - prof["predict_ms"] - prof["predict_cov_ms"],
+           "note": "ms: wall time of unprofiled calls (median of 5) including the single-particle factorisation "
+                   "and the host<->device copies; the kernel times come from a separate profiled pass"}
+    if out["factor_ms"] > 0:
+        out["factor_tflops"] = out["factor_flops"] / (out["factor_ms"] * 1e-3) / 1e12
     if not args.no_cpu and args.cpu_predict_points > 0:
         from oracle import ref_cpu  # CPU baseline leg only
         m = args.cpu_predict_points
@@ -285,6 +309,49 @@ def psurf_line(ctx, args):
         cdt = time.perf_counter() - t1
         out["cpu_baseline"] = {"rows_per_s": m / cdt, "sample": f"oracle prob_surface (calc_prob_surf.py "
                                f"restated: numpy + scipy.stats.norm) on {m} rows, 1 core", "s": cdt}
+    return out
+
+
+SECONDARY_CONFIGS = (
+    # (letter, N, d, particles, seed, hetero, warmup, steps): the other single-GPU BASELINE configs
+    # (BASELINE.json configs 1, 3 and 4 at one GPU's share, SURVEY.md §8d seeds), timed like the
+    # headline (no HIP events in the stream, interior particles l ~ U[0.05, 0.6]^d)
+    ("B", 1024, 2, 32, 0, False, 5, 200),
+    ("D-share", 4096, 3, 32, 1, False, 2, 40),   # the per-GPU load of every rank of the N>1 runs
+    ("E-share", 16384, 4, 16, 1, True, 1, 3),    # config E's 128 particles over 8 GPUs
+)
+
+
+def secondary_configs(ctx, args, peak):
+    """Secondary lines: B, D's per-GPU share and E's per-GPU share on this GPU (find_len_scales.py:
+    102-104 at each size). frac = evals/s x (2/3) Npad^3 / the FP64 MFMA peak (whole-step rate,
+    everything in the step counted against the factorisation's flops)."""
+    from gpfit.swarm import search_bounds, sigma_grid
+    out = []
+    for name, N, d, P, seed, hetero, warm, steps in SECONDARY_CONFIGS:
+        if args.steps < 20:  # a short debug run keeps the secondary lines short too
+            steps = max(1, min(steps, args.steps))
+        x, y, e = synthetic(N, d, seed, hetero)
+        lo, hi = search_bounds(x)
+        s, ex = sigma_grid()
+        ctx.set_data(x, y, e)
+        ctx.set_grid(s, ex, lo, hi)
+        rng = np.random.default_rng(seed + 2000)
+        for _ in range(warm):
+            ctx.eval_batch(rng.uniform(0.05, 0.6, size=(P, d)))
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            ctx.eval_batch(rng.uniform(0.05, 0.6, size=(P, d)))
+        ctx.synchronize()
+        dt = time.perf_counter() - t0
+        v = P * steps / dt
+        fl = (2.0 / 3.0) * float(-(-N // 128) * 128) ** 3
+        out.append({"config": name, "N": N, "d": d, "particles": P, "hetero_noise": hetero, "seed": seed,
+                    "steps": steps, "warmup": warm, "value": v, "unit": "evals/s", "ms_per_step": dt / steps * 1e3,
+                    "achieved_tflops": v * fl / 1e12, "frac": v * fl / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+                    "frac_of_box_peak": (v * fl / 1e12 / peak) if peak else None,
+                    "flops_per_eval": fl, "formulation": "potrf+trtri (2/3 Npad^3 per eval)"})
     return out
 
 
@@ -384,6 +451,7 @@ def main():
     ap.add_argument("--psurf-rows", type=int, default=100000,
                     help="secondary (SURVEY.md §8f row 4): probability-surface rows, 0 = skip")
     ap.add_argument("--plumbing", action="store_true", help="CPU-only multi-rank plumbing check (no measurement)")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the B / D-share / E-share lines")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -504,6 +572,10 @@ def main():
     # direct-to-LDS, N=4096-sized panels, depth 2048, 960 workgroups)
     core = ctx.gemm_bench(mode=2, npad=4096, particles=64, tiles=15, depth=2048, iters=3) \
         if (rank == 0 and N >= 2048) else None
+    # this box's FP64 matrix ceiling: back-to-back independent v_mfma_f64_16x16x4 chains on every
+    # SIMD (gpf_mfma_peak), at whatever clock the chip holds under that load; boxes of the pool
+    # differ, so fractions against it are checkable per box
+    box_peak = ctx.mfma_peak(blocks=1024, iters=8192) if rank == 0 else None
     traffic = pmc_traffic(N, d, spg)
     roof = {"kernel": "k_step", "bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
@@ -517,6 +589,8 @@ def main():
                                "around every launch (the `value` pass records no events)",
             "ms_per_step_profiled_pass": dt_prof / args.steps * 1e3 if dt_prof else None,
             "particle_groups": groups,
+            "box_fp64_mfma_tflops": box_peak,
+            "frac_of_box_peak": (achieved / box_peak) if (achieved and box_peak) else None,
             "gemm_core_tflops": core,
             "frac_of_gemm_core": (achieved / core) if (achieved and core) else None,
             "launches": prof["panel_launches"], "avg_launch_ms": prof["panel_ms"] / max(prof["panel_launches"], 1),
@@ -524,6 +598,12 @@ def main():
             "formulation": "potrf+trtri (2/3 N^3 per eval)",
             "factor_phase_tflops": (prof["factor_flops"] / (prof["factor_wall_ms"] * 1e-3) / 1e12)
             if prof["factor_wall_ms"] > 0 else None}
+    # each rank's factorisation-phase rate (profiled pass), so a scaling line shows imbalance too
+    ftf = roof["factor_phase_tflops"] or 0.0
+    ftf_max = ftf_min = ftf
+    if comm is not None:
+        ftf_max = float(comm.allreduce([ftf], op="max")[0])
+        ftf_min = -float(comm.allreduce([-ftf], op="max")[0])
     build_gbs = (prof["build_bytes"] / (prof["build_ms"] * 1e-3) / 1e9) if prof["build_ms"] > 0 else None
     breakdown = {k: prof[k] for k in ("panel_ms", "diag_ms", "build_ms", "loss_ms", "factor_wall_ms")}
     breakdown["k_build_cov_GBps"] = build_gbs
@@ -542,6 +622,9 @@ def main():
     hull = None
     if solo and not args.no_hull:
         hull = hull_line(ctx, args)
+    secondary = None
+    if solo and not args.no_secondary:
+        secondary = secondary_configs(ctx, args, box_peak)
     if solo and not args.no_cpu:
         cpu = cpu_baselines(x, y, e, lo, hi, N, d, args.seed)
 
@@ -562,6 +645,7 @@ def main():
                                        if world > 1 else "single GPU"),
                        "hetero_noise": bool(args.hetero),
                        "pso_iters_per_s": args.steps / dt, "particles": "interior l~U[0.05,0.6]^d (full work)"},
+            "configs": secondary,
             "pso_loop": pso,
             "predict": predict,
             "prob_surface": psurf,
@@ -579,6 +663,8 @@ def main():
             "rccl": (exchange["transport"] == "rccl") if exchange else None,
             "exchange_ms_per_step": xch_max if comm is not None else None,
             "exchange_ms_per_step_min_rank": xch_min if comm is not None else None,
+            "factor_tflops_rank_max": ftf_max if comm is not None else None,
+            "factor_tflops_rank_min": ftf_min if comm is not None else None,
         }
         print(json.dumps(line), flush=True)
     if comm is not None:

@@ -220,6 +220,7 @@ int host_allreduce(gpf_comm* c, double* buf, int64_t n, int op) {
 }
 
 int rccl_allreduce(gpf_comm* c, double* buf, int64_t n, int op) {
+  if (!c->nccl) return comm_fail(c, "all-reduce: the RCCL communicator was aborted after an earlier failure");
   if (hipSetDevice(c->device) != hipSuccess) return comm_fail(c, "all-reduce: hipSetDevice failed");
   if ((size_t)n > c->cap) {
     hipFree(c->d_buf);
@@ -244,7 +245,15 @@ int rccl_allreduce(gpf_comm* c, double* buf, int64_t n, int op) {
     if (ncclCommGetAsyncError(c->nccl, &nr) != ncclSuccess) nr = ncclInternalError;
     if (nr == ncclInProgress) std::this_thread::yield();
   }
-  if (nr != ncclSuccess) return comm_fail(c, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+  if (nr != ncclSuccess) {
+    // a collective still in progress at the deadline (or a failed one) stays queued on the
+    // stream: abort the communicator so that no later exchange, and not gpf_comm_close's
+    // ncclCommDestroy, waits on it or mixes its result in; later calls fail fast
+    const std::string why = nr == ncclInProgress ? "timed out" : ncclGetErrorString(nr);
+    ncclCommAbort(c->nccl);
+    c->nccl = nullptr;
+    return comm_fail(c, "ncclAllReduce: " + why + " (communicator aborted)");
+  }
   if (hipMemcpyAsync(c->h_buf, c->d_buf, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess)
     return comm_fail(c, "all-reduce: download failed");

@@ -444,11 +444,14 @@ __device__ __forceinline__ void syrk_rows(double* __restrict__ C, size_t ldc, co
     dr.template run<M0>(acc, A, A, lda, 0, nch, nch, smem);
     __syncthreads();
   }
+  // the stores go through a freshly laundered base: with the seed loads' 64-bit addresses reused
+  // here, the compiler kept up to 32 of them live across the GEMM and spilled them
+  double* p1 = launder(C + (size_t)(qd.lane >> 4) * ldc + qd.cb + (qd.lane & 15));
 #pragma unroll
   for (int mi = M0; mi < 8; ++mi)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      double* q = p0 + (size_t)(mi * 16 + 4 * r) * ldc;
+      double* q = p1 + (size_t)(mi * 16 + 4 * r) * ldc;
       if (WT)
         __hip_atomic_store(reinterpret_cast<unsigned long long*>(q),
                            (unsigned long long)__double_as_longlong(acc.v[mi][0][r]), __ATOMIC_RELAXED,
@@ -576,8 +579,12 @@ __device__ __forceinline__ void gemm_lds64(Acc<64>& acc, const double* sA, int l
   if (TRI == TRI_A_KLER) k1 = qd.rb + 32;           // A(r,k) = 0 for k > r (row block 0 stops at rb + 16)
   const bool live0 = TRI != TRI_C_LOWER || qd.cb < qd.rb + 16;  // lower-only output: row block 0
   const bool live1 = TRI != TRI_C_LOWER || qd.cb < qd.rb + 32;  // ... row block 1
-#pragma unroll 4
-  for (int ks = k0; ks < k1; ks += 4) {
+  // every bound is a multiple of 16: 16-deep blocks of 4 k-steps (an exact unroll by 4; a
+  // `#pragma unroll 4` on the runtime-bounded loop could not be honoured)
+#pragma unroll 1
+  for (int k16 = k0; k16 < k1; k16 += 16)
+#pragma unroll
+  for (int ks = k16; ks < k16 + 16; ks += 4) {
     double a[MBR], b[MBC];
 #pragma unroll
     for (int mi = 0; mi < MBR; ++mi) a[mi] = sA[(qd.rb + mi * 16 + lr) * la + ks + lk];
@@ -595,8 +602,12 @@ __device__ __forceinline__ void gemm_lds64(Acc<64>& acc, const double* sA, int l
 }
 
 // Coalesced 64x64 global tile -> LDS [row][col] with stride ld, 16 B per lane (DNTH threads).
+// (The global tile pointers of these helpers are laundered: factor128 loads and later stores the
+// same 64x64 tiles, and with the addresses shared the compiler kept them live across the factor
+// and spilled them.)
 __device__ __forceinline__ void tile64_to_lds(double* s, int ld, const double* __restrict__ g, size_t gld) {
   const int tid = threadIdx.x;
+  g = launder(g);
 #pragma unroll
   for (int u = 0; u < 2048 / DNTH; ++u) {
     const int q = tid + DNTH * u;
@@ -624,6 +635,7 @@ template <bool WT = false>
 __device__ __forceinline__ void lds_to_tile64(double* __restrict__ g, size_t gld, const double* s, int ld,
                                               bool lower_only) {
   const int tid = threadIdx.x;
+  g = launder(g);
 #pragma unroll
   for (int u = 0; u < 2048 / DNTH; ++u) {
     const int q = tid + DNTH * u;
@@ -644,6 +656,7 @@ __device__ __forceinline__ void lds_to_tile64(double* __restrict__ g, size_t gld
 template <bool WT = false>
 __device__ __forceinline__ void zero_tile64(double* __restrict__ g, size_t gld) {
   const int tid = threadIdx.x;
+  g = launder(g);
 #pragma unroll
   for (int u = 0; u < 2048 / DNTH; ++u) {
     const int q = tid + DNTH * u;

@@ -1114,12 +1114,16 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
     if (*flag) return false;  // timed out: the host reports it
     const double* p0 =
         launder(pt + (size_t)(sib << l) * T * T + (size_t)(qd.rb + (qd.lane >> 4)) * T + qd.cb + (qd.lane & 15));
+    // two row blocks (8 loads) per scheduling region: issued all at once, the sibling's 32 values
+    // plus the 32 accumulators exceeded the 128-register budget and spilled
 #pragma unroll
-    for (int mi = 0; mi < Acc<T>::MBR; ++mi)
+    for (int mi = 0; mi < Acc<T>::MBR; ++mi) {
 #pragma unroll
       for (int ni = 0; ni < Acc<T>::MBC; ++ni)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc.v[mi][ni][r] = acc.v[mi][ni][r] + p0[(mi * 16 + 4 * r) * T + ni * 16];
+      if (mi & 1) __builtin_amdgcn_sched_barrier(0);
+    }
   }
   return true;
 }
@@ -1182,6 +1186,12 @@ __device__ __forceinline__ void syrk_item(int J, int p, int Npad, double* __rest
 #endif
 __host__ __device__ __forceinline__ int la_chunks(int J) { return GPF_LA_FRAC16 * 8 * J / 16; }
 
+// The partial of launch J goes to slot J & 1 of its particle (two slots per particle): the
+// critical tile of launch J + 1 reads slot J & 1 while launch J + 1's own look-ahead writes slot
+// (J + 1) & 1, so a critical tile dispatched late (concurrent groups over-subscribing the slots,
+// another process on the GPU) can never seed from the next tile's partial.
+__host__ __device__ __forceinline__ size_t la_slot(int p, int J) { return (size_t)(2 * p + (J & 1)) * T * T; }
+
 __device__ __forceinline__ void la_item(int J, int p, int Npad, const double* __restrict__ Lb, int N,
                                         const double* __restrict__ x, const double* __restrict__ ls, int d,
                                         double* __restrict__ lab, double* lds) {
@@ -1192,7 +1202,7 @@ __device__ __forceinline__ void la_item(int J, int p, int Npad, const double* __
   cov_tile_acc(acc, qd, x, ls + (size_t)p * d, d, N, J + 1, J + 2, lds);
   gemm_stream_dl<false, true>(acc, Lp + (size_t)(J + 1) * T * ld, Npad, Lp + (size_t)(J + 2) * T * ld, Npad,
                               la_chunks(J) * DL_KC, lds, qd);
-  acc.store(qd, lab + (size_t)p * T * T, T);
+  acc.store(qd, lab + la_slot(p, J), T);
 }
 
 // Tile w of block column J of particle p (the unit of work of k_step); role from step_decode.
@@ -1247,7 +1257,11 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
       // look-ahead seed: launch J-1 left this tile's GEMM over its first la_chunks(J-1) chunks (cov
       // seed included); the rest follows — the same MFMAs in the same order
       const int k0 = la_chunks(J - 1) * DL_KC;  // where launch J-1's look-ahead stopped
-      acc.load(qd, lab + (size_t)p * T * T, T);
+      if (la & 4) {  // test hook (GPF_LA_DELAY_TEST): dispatched "late", after this launch's look-ahead wrote
+        for (int i = 0; i < 96; ++i) __builtin_amdgcn_s_sleep(127);  // ~0.3 ms
+        __syncthreads();
+      }
+      acc.load(qd, lab + la_slot(p, J - 1), T);
       gemm_stream_dl<false, true>(acc, Lp + (size_t)J * T * ld + k0, Npad, Lp + (size_t)I * T * ld + k0, Npad, J * T - k0,
                                   lds, qd);
     } else {

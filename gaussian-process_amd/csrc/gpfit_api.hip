@@ -92,6 +92,7 @@ struct gpf_ctx {
   int* d_cflag = nullptr;  // per particle: last diagonal block reduced by a SYRK workgroup (defer_syrk); reset by k_build_cov
   // gpf_predict's query-chunk buffers, kept between calls (grow-only; freed with the work buffers)
   double *p_xf = nullptr, *p_ks = nullptr, *p_vsq = nullptr, *p_mu = nullptr, *p_sd = nullptr;
+  double *p_hx = nullptr, *p_hout = nullptr;  // pinned staging: query coordinates, (mu, sd)
   int64_t p_cols = 0, p_np = 0;
   int p_d = 0, p_nt = 0;
   // gpf_prob_surface's row-chunk buffers, kept between calls like the prediction's
@@ -192,7 +193,9 @@ static void clear_graphs(gpf_ctx* c) {
 
 static void free_pred(gpf_ctx* c) {
   hipFree(c->p_xf); hipFree(c->p_ks); hipFree(c->p_vsq); hipFree(c->p_mu); hipFree(c->p_sd);
+  hipHostFree(c->p_hx); hipHostFree(c->p_hout);
   c->p_xf = c->p_ks = c->p_vsq = c->p_mu = c->p_sd = nullptr;
+  c->p_hx = c->p_hout = nullptr;
   c->p_cols = c->p_np = 0;
   c->p_d = c->p_nt = 0;
 }
@@ -568,6 +571,11 @@ static int run_factor(gpf_ctx* c, int pc) {
   // took its ticket, leaving a tile unfinished).
   int S = 1, Smax = 1;
   if (int rc = split_plan(c, pc, S, Smax)) return rc;
+  // the split-K tickets and ready flags start at zero in every split factorisation: the
+  // finishing pieces re-zero what they used, but a hand-off that timed out (info bit 2) leaves its
+  // pair's ticket and flag set, and the next tree would elect the wrong finisher;
+  // ~20 KB at N=4096 for one particle, on c->stream ahead of the fork
+  if (Smax > 1) GPF_HIP(c, hipMemsetAsync(c->d_cnt, 0, (size_t)pc * (nt - 1) * gpf::SPLIT_CNT * 4, c->stream));
   hipEvent_t wa = nullptr, wb = nullptr;
   if (c->prof) {
     wa = take_event(c);
@@ -610,20 +618,23 @@ static int run_factor(gpf_ctx* c, int pc) {
   step_plan(pc, nt, S, Smax, plan);
   bool any_la = false;
   for (const StepLaunch& l : plan) any_la = any_la || l.la != 0;
-  if (any_la && (size_t)pc * T * T * 8 > c->la_cap) {  // (never under a graph capture: nt >= 4 only)
+  if (any_la && 2 * (size_t)pc * T * T * 8 > c->la_cap) {  // (never under a graph capture: nt >= 4 only)
     clear_graphs(c);
     hipFree(c->d_la);
     c->d_la = nullptr;
     c->la_cap = 0;
-    GPF_HIP(c, hipMalloc(&c->d_la, (size_t)pc * T * T * 8));
-    c->la_cap = (size_t)pc * T * T * 8;
+    GPF_HIP(c, hipMalloc(&c->d_la, 2 * (size_t)pc * T * T * 8));  // two slots per particle (gpf::la_slot)
+    c->la_cap = 2 * (size_t)pc * T * T * 8;
   }
+  // test hook: the critical tiles that seed from the look-ahead wait ~0.3 ms first (gpf::step_item)
+  const int la_delay = (getenv("GPF_LA_DELAY_TEST") && atoi(getenv("GPF_LA_DELAY_TEST")) != 0) ? 4 : 0;
   for (const StepLaunch& l : plan) {
     const double fl = step_flops(l.J);
     const int p0 = l.p0, gc = l.gc;
     hipStream_t st = (ng > 1) ? c->sub[l.g] : c->stream;
-    double* partg = l.S > 1 ? c->d_part + l.part_off : nullptr;
-    unsigned* cntg = l.S > 1 ? c->d_cnt + l.cnt_off : nullptr;
+    // (every split launch gets its buffers: under SPLIT_ALL, l.S is chunks per piece, not a piece count)
+    double* partg = l.split != gpf::SPLIT_NONE ? c->d_part + l.part_off : nullptr;
+    unsigned* cntg = l.split != gpf::SPLIT_NONE ? c->d_cnt + l.cnt_off : nullptr;
     const auto kern = l.split == gpf::SPLIT_ALL    ? (ed ? gpf::k_step<gpf::SPLIT_ALL, 1> : gpf::k_step<gpf::SPLIT_ALL, 0>)
                       : l.split == gpf::SPLIT_CRIT ? (ed ? gpf::k_step<gpf::SPLIT_CRIT, 1> : gpf::k_step<gpf::SPLIT_CRIT, 0>)
                                                    : (ed ? gpf::k_step<gpf::SPLIT_NONE, 1> : gpf::k_step<gpf::SPLIT_NONE, 0>);
@@ -632,7 +643,8 @@ static int run_factor(gpf_ctx* c, int pc) {
                          c->d_U + (size_t)p0 * ld * ld, c->d_yb + (size_t)p0 * ld, c->d_s2p + (size_t)p0 * nt * ld,
                          c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc, l.grp, N, c->d_x,
                          c->d_ls + (size_t)p0 * c->d, c->d, l.S, l.S2, partg, cntg, c->d_flag + p0, l.ed,
-                         c->d_cflag + p0, l.defer, l.sy, spins, l.la, l.la ? c->d_la + (size_t)p0 * T * T : nullptr);
+                         c->d_cflag + p0, l.defer, l.sy, spins, l.la | ((l.la & 2) ? la_delay : 0),
+                         l.la ? c->d_la + 2 * (size_t)p0 * T * T : nullptr);
     });
     if (rc) return rc;
     total += fl * gc;
@@ -942,11 +954,15 @@ int gpf_eval_batch(gpf_ctx* c, const double* ls, int P, double* loss, double* mu
   return GPF_OK;
 }
 
-// Factorise one particle (slot 0 of the workspace) and produce alpha on device.
-static int factor_single(gpf_ctx* c, const double* ls, double** alpha_out) {
+// Factorise one particle (slot 0 of the workspace) and produce alpha on device, without waiting:
+// the factor's status word is copied to the pinned c->h_info[0] behind it on c->stream, and the
+// caller checks it (factor_status) after its next synchronisation — gpf_predict queues the query
+// kernels right behind the factorisation instead of idling the GPU for a host round trip.
+static int factor_single_async(gpf_ctx* c, const double* ls, double** alpha_out) {
   int rc = ensure_work(c, 1);
   if (rc) return rc;
-  GPF_HIP(c, hipMemcpyAsync(c->d_ls, ls, (size_t)c->d * 8, hipMemcpyHostToDevice, c->stream));
+  std::memcpy(c->h_ls, ls, (size_t)c->d * 8);
+  GPF_HIP(c, hipMemcpyAsync(c->d_ls, c->h_ls, (size_t)c->d * 8, hipMemcpyHostToDevice, c->stream));
   GPF_HIP(c, hipMemsetAsync(c->d_info, 0, 4, c->stream));
   rc = run_factor(c, 1);
   if (rc) return rc;
@@ -956,9 +972,14 @@ static int factor_single(gpf_ctx* c, const double* ls, double** alpha_out) {
                        (int)c->N, (int)c->Npad, c->nt, c->d_szp, c->d_mu);
   });
   if (rc) return rc;
-  int info = 0;
-  GPF_HIP(c, hipMemcpyAsync(&info, c->d_info, 4, hipMemcpyDeviceToHost, c->stream));
-  GPF_HIP(c, hipStreamSynchronize(c->stream));
+  GPF_HIP(c, hipMemcpyAsync(c->h_info, c->d_info, 4, hipMemcpyDeviceToHost, c->stream));
+  *alpha_out = c->d_mu;
+  return GPF_OK;
+}
+
+// The status of the last factor_single_async (valid once c->stream has been synchronised).
+static int factor_status(gpf_ctx* c) {
+  const int info = c->h_info[0];
   if (info & 2) {
     c->err = "k_step: diagonal-block hand-off timed out";
     return GPF_HIP_ERROR;
@@ -967,8 +988,16 @@ static int factor_single(gpf_ctx* c, const double* ls, double** alpha_out) {
     c->err = "Matrix is not positive definite";
     return GPF_NOT_PD;
   }
-  *alpha_out = c->d_mu;
   return GPF_OK;
+}
+
+static int factor_single(gpf_ctx* c, const double* ls, double** alpha_out) {
+  int rc = factor_single_async(c, ls, alpha_out);
+  if (rc) return rc;
+  GPF_HIP(c, hipStreamSynchronize(c->stream));
+  rc = factor_status(c);
+  if (rc) *alpha_out = nullptr;
+  return rc;
 }
 
 int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int64_t batch, double* mu,
@@ -981,22 +1010,27 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
   if (c->K <= 0) {  // predict does not need the objective grid; size the histogram minimally
     c->K = 2;
   }
-  double* alpha = nullptr;
-  int rc = factor_single(c, ls, &alpha);
-  if (rc) return rc;
   // Query chunk: as large as memory allows (the reference's batch_size only bounds its
-  // own host memory, GP_func.py:28-30; results do not depend on it).
+  // own host memory, GP_func.py:28-30; results do not depend on it). Sized before the
+  // factorisation is queued, so that a (re)allocation never waits for it; free memory is only
+  // queried when the kept buffers are too small.
+  // the factorisation workspace first: a (re)allocation there frees the query buffers too
+  if (int rw = ensure_work(c, 1)) return rw;
   const int64_t Np = c->Npad;
-  int64_t chunk = std::max<int64_t>(batch, 1);
-  size_t fr = 0, tot = 0;
-  GPF_HIP(c, hipMemGetInfo(&fr, &tot));
-  const int64_t per_col = (Np + c->nt) * 8;
-  const int64_t maxcols = std::max<int64_t>(T, (int64_t)((double)fr * 0.5 / (double)per_col));
-  chunk = std::min<int64_t>(std::max<int64_t>(chunk, 16384), maxcols);
-  chunk = std::min<int64_t>(chunk, M);
-  const int64_t Cp = ((chunk + T - 1) / T) * T;
+  int64_t chunk = std::min<int64_t>(std::max<int64_t>(std::max<int64_t>(batch, 1), 16384), M);
+  int64_t Cp = ((chunk + T - 1) / T) * T;
+  const bool fits = c->p_cols >= Cp && c->p_np == Np && c->p_d == c->d && c->p_nt == c->nt;
+  if (!fits) {
+    size_t fr = 0, tot = 0;
+    GPF_HIP(c, hipMemGetInfo(&fr, &tot));
+    const int64_t per_col = (Np + c->nt) * 8;
+    const int64_t maxcols = std::max<int64_t>(T, (int64_t)((double)fr * 0.5 / (double)per_col));
+    chunk = std::min<int64_t>(chunk, maxcols);
+    Cp = ((chunk + T - 1) / T) * T;
+  }
   // buffers kept from the previous call when they are large enough (a hipMalloc/hipFree of the
-  // Np x Cp cross-covariance per call cost ~1 ms of the call's wall time)
+  // Np x Cp cross-covariance per call cost ~1 ms of the call's wall time); pinned host staging
+  // for the query coordinates and the outputs (pageable copies stage through a bounce buffer)
   if (c->p_cols < Cp || c->p_np != Np || c->p_d != c->d || c->p_nt != c->nt) {
     GPF_HIP(c, hipStreamSynchronize(c->stream));
     free_pred(c);
@@ -1005,19 +1039,27 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
     GPF_HIP(c, hipMalloc(&c->p_vsq, (size_t)c->nt * Cp * 8));
     GPF_HIP(c, hipMalloc(&c->p_mu, (size_t)Cp * 8));
     GPF_HIP(c, hipMalloc(&c->p_sd, (size_t)Cp * 8));
+    GPF_HIP(c, hipHostMalloc((void**)&c->p_hx, (size_t)c->d * Cp * 8, hipHostMallocDefault));
+    GPF_HIP(c, hipHostMalloc((void**)&c->p_hout, (size_t)2 * Cp * 8, hipHostMallocDefault));
     c->p_cols = Cp;
     c->p_np = Np;
     c->p_d = c->d;
     c->p_nt = c->nt;
   }
+  double* alpha = nullptr;
+  int rc = factor_single_async(c, ls, &alpha);
+  if (rc) return rc;
   double *d_xf = c->p_xf, *d_ks = c->p_ks, *d_vsq = c->p_vsq, *d_mu = c->p_mu, *d_sd = c->p_sd;
-  std::vector<double> hx((size_t)c->d * Cp);
+  double* hx = c->p_hx;
   rc = GPF_OK;
   for (int64_t s = 0; s < M && rc == GPF_OK; s += chunk) {
     const int64_t m = std::min<int64_t>(chunk, M - s);
-    for (int k = 0; k < c->d; ++k)
-      std::memcpy(hx.data() + (size_t)k * Cp, xfit + (size_t)k * M + s, (size_t)m * 8);
-    if (hipMemcpyAsync(d_xf, hx.data(), (size_t)c->d * Cp * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+    if (s > 0 && hipStreamSynchronize(c->stream) != hipSuccess) {  // the staging buffer is reused
+      rc = GPF_HIP_ERROR;
+      break;
+    }
+    for (int k = 0; k < c->d; ++k) std::memcpy(hx + (size_t)k * Cp, xfit + (size_t)k * M + s, (size_t)m * 8);
+    if (hipMemcpyAsync(d_xf, hx, (size_t)c->d * Cp * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
       rc = GPF_HIP_ERROR;
       break;
     }
@@ -1040,12 +1082,19 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
                          (int)c->N, c->nt, (int)m, d_ks, (int)Cp, alpha, d_vsq, d_mu, d_sd);
     });
     if (rc) break;
-    if (hipMemcpyAsync(mu + s, d_mu, (size_t)m * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-        hipMemcpyAsync(sd + s, d_sd, (size_t)m * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+    if (hipMemcpyAsync(c->p_hout, d_mu, (size_t)m * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipMemcpyAsync(c->p_hout + Cp, d_sd, (size_t)m * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) {
       rc = GPF_HIP_ERROR;
       c->err = "gpf_predict: copy back failed";
+      break;
     }
+    if (s == 0) {  // the factorisation's status (its copy preceded this synchronisation)
+      rc = factor_status(c);
+      if (rc) break;
+    }
+    std::memcpy(mu + s, c->p_hout, (size_t)m * 8);
+    std::memcpy(sd + s, c->p_hout + Cp, (size_t)m * 8);
   }
   hipStreamSynchronize(c->stream);
   if (c->prof) harvest(c);
@@ -1140,6 +1189,11 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     if (l.S < 1 || (l.split == gpf::SPLIT_CRIT && (l.S < 2 || l.S > Smax || l.S2 != l.S)) ||
         (l.split == gpf::SPLIT_NONE && (l.S != 1 || l.S2 != 1)) || (l.split == gpf::SPLIT_ALL && l.S2 != Smax))
       return plan_fail(msg, msg_len, "J=%d g=%d: split kind %d with S=%d S2=%d", l.J, l.g, l.split, l.S, l.S2);
+    if (l.split != gpf::SPLIT_NONE && Smax < 2)
+      return plan_fail(msg, msg_len, "J=%d g=%d: split launch without split-K buffers (Smax=%d)", l.J, l.g, Smax);
+    // the look-ahead partial a seeded launch reads (slot of J-1) is never the one it writes (slot of J)
+    if ((l.la & 2) && (l.la & 1) && gpf::la_slot(0, l.J - 1) == gpf::la_slot(0, l.J))
+      return plan_fail(msg, msg_len, "J=%d g=%d: look-ahead reads and writes the same slot", l.J, l.g);
     const int tiles = l.gc * ntl;
     auto pieces_of = [&](int w) { return l.split == gpf::SPLIT_ALL ? gpf::split_all_pieces(l.J, w, nt, l.S) : l.S; };
     for (int w = 0; w < ntl; ++w)

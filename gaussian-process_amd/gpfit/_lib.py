@@ -7,6 +7,7 @@ separate, test-only tree.
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 from pathlib import Path
 
@@ -119,6 +120,16 @@ def _ptr(a):
     return a.ctypes.data_as(_dp)
 
 
+def _digest(*arrays):
+    """sha256 over the arrays' shapes and bytes: the key that decides whether an upload can be
+    skipped (a Python hash() collision would silently score stale data)."""
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(repr(a.shape).encode())
+        h.update(a.tobytes())
+    return h.digest()
+
+
 def default_device():
     """One process per GPU: torch.distributed launchers export LOCAL_RANK."""
     return int(os.environ.get("GPFIT_DEVICE", os.environ.get("LOCAL_RANK", "0")))
@@ -168,7 +179,7 @@ class Context:
             raise ValueError("x must be (d, N)")
         y, e = _f64(y), _f64(e)
         d, n = x.shape
-        key = (d, n, hash(x.tobytes()), hash(y.tobytes()), hash(e.tobytes()))
+        key = _digest(x, y, e)
         if key == self._data_key:
             return
         self._check(self.lib.gpf_set_data(self._h, _ptr(x), _ptr(y), _ptr(e), n, d), "gpf_set_data")
@@ -179,7 +190,7 @@ class Context:
     def set_grid(self, sigma_vals, expected, lo, hi):
         s, ex = _f64(sigma_vals), _f64(expected)
         lo, hi = _f64(lo).reshape(-1), _f64(hi).reshape(-1)
-        key = (hash(s.tobytes()), hash(ex.tobytes()), hash(lo.tobytes()), hash(hi.tobytes()))
+        key = _digest(s, ex, lo, hi)
         if key == self._grid_key:
             return
         self._check(self.lib.gpf_set_grid(self._h, _ptr(s), _ptr(ex), s.shape[0], _ptr(lo), _ptr(hi)),

@@ -26,4 +26,4 @@ timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o
 timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_mfma -o m --output-format csv -- $B2 > $O/pmc_mfma.log 2>&1 || exit $?
 python scripts/pmc_traffic.py $O/pmc_fetch $O/pmc_write $O/k_step_traffic.json 4096 3 64
 python scripts/pmc_counters.py $O/k_step_counters.json "per k_step dispatch averages, N=4096 d=3 swarm 64 (rocprofv3 --pmc, separate passes)" $O/pmc_mfma $O/pmc_fetch $O/pmc_write
-TAG=${TAG:-ev}_sec bash scripts/gpu_r3_secondary.sh
+TAG=${TAG:-ev}_sec bash scripts/gpu_secondary.sh

@@ -71,3 +71,19 @@ def test_bad_arguments_are_value_errors_without_touching_device():
     lib = L.load_library()
     assert lib.gpf_set_data(None, None, None, None, 0, 0) == L.GPF_BAD_ARG
     assert lib.gpf_eval_batch(None, None, 0, None, None, None, None) == L.GPF_BAD_ARG
+
+
+def test_comm_transport_codes():
+    """INTEGRATION.md's fallback: the host transport is GPF_COMM_HOST = 2 (RCCL = 1); any other
+    code, 0 included, is rejected with GPF_BAD_ARG before any socket or device is touched."""
+    import gpfit._lib as L
+    lib = L.load_library()
+    assert (L.GPF_COMM_RCCL, L.GPF_COMM_HOST) == (1, 2)
+    out = ctypes.c_void_p()
+    for bad in (0, 3, -1):
+        assert lib.gpf_comm_open(None, 0, 1, b"127.0.0.1", 29999, bad, ctypes.byref(out)) == L.GPF_BAD_ARG
+        assert not out.value
+    # one rank over the host transport needs no rendezvous: opens, exchanges, closes
+    assert lib.gpf_comm_open(None, 0, 1, b"127.0.0.1", 29999, L.GPF_COMM_HOST, ctypes.byref(out)) == L.GPF_OK
+    assert out.value
+    lib.gpf_comm_close(out)

@@ -20,7 +20,7 @@ def _run(args, env=None, timeout=180):
                           timeout=timeout, env=e, cwd=str(ROOT))
 
 
-@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("n", [2, 4, 8])
 def test_gpus_flag_starts_that_many_ranks(n):
     r = _run(["--gpus", str(n), "--plumbing"])
     assert r.returncode == 0, r.stderr[-2000:]
@@ -55,6 +55,8 @@ def test_multi_rank_bench_on_one_gpu():
     assert out["config"]["swarm_per_gpu"] == 32
     assert out["exchange"] == {"transport": "host"} and out["rccl"] is False
     assert 0.0 <= out["exchange_ms_per_step_min_rank"] <= out["exchange_ms_per_step"]
+    # per-rank factorisation rates (imbalance of a scaling line)
+    assert 0.0 < out["factor_tflops_rank_min"] <= out["factor_tflops_rank_max"]
 
 
 @pytest.mark.gpu

@@ -684,6 +684,57 @@ def test_critical_tile_lookahead_bitwise(ctx, monkeypatch, N, d, P):
     assert _rel(on[1][0], mo) < RTOL_MU_SD and _rel(on[2][0], so) < RTOL_MU_SD
 
 
+@pytest.mark.gpu
+def test_lookahead_partials_survive_late_critical_tile(ctx, monkeypatch):
+    """the look-ahead partial of launch J is double-buffered by launch parity
+    (gpf::la_slot), so a critical tile dispatched after its own launch's look-ahead has already
+    written cannot seed from the next tile's partial. GPF_LA_DELAY_TEST=1 makes every seeded
+    critical tile wait ~0.3 ms before it loads the partial (after the SYRK workgroup of the same
+    launch has stored its own): scores, mean and sd stay bitwise equal (config B's schedule)."""
+    import gpfit
+    N, d, P = 1024, 2, 32
+    rng = np.random.default_rng(4242)
+    x = rng.uniform(size=(d, N))
+    y = np.sin(6 * x[0]) * x[1] + 0.1 * rng.standard_normal(N)
+    e = np.full(N, 0.1)
+    s, ex = ref_cpu.sigma_grid()
+    lo, hi = ref_cpu.search_bounds(x)
+    ctx.set_data(x, y, e)
+    ctx.set_grid(s, ex, lo, hi)
+    Q = rng.uniform(0.1, 0.5, size=(P, d))
+    assert gpfit.plan_check(P, N // 128)["syrk_workgroups"] > 0
+    want = ctx.eval_batch(Q, want_mu_sd=True)
+    monkeypatch.setenv("GPF_LA_DELAY_TEST", "1")
+    late = ctx.eval_batch(Q, want_mu_sd=True)
+    monkeypatch.delenv("GPF_LA_DELAY_TEST")
+    for a, b in zip(want, late):
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_split_handoff_timeout_then_correct(ctx, monkeypatch):
+    """a timed-out split-K hand-off (single-particle factorisation: every tile
+    split, the binary reduction tree of gpf::split_part) is reported, and the next factorisation is
+    correct: run_factor re-zeroes the tickets and ready flags a timed-out pair leaves set."""
+    N, d = 2048, 2
+    rng = np.random.default_rng(78)
+    x = rng.uniform(size=(d, N))
+    y = np.sin(4 * x[0]) + 0.1 * rng.standard_normal(N)
+    e = np.full(N, 0.1)
+    ctx.set_data(x, y, e)
+    xf = rng.uniform(size=(d, 700))
+    ls = np.array([0.3, 0.4])
+    want = ctx.predict(ls, xf)
+    monkeypatch.setenv("GPF_WAIT_SPINS", "0")
+    with pytest.raises(RuntimeError, match="timed out"):
+        ctx.predict(ls, xf)
+    monkeypatch.delenv("GPF_WAIT_SPINS")
+    for _ in range(2):
+        got = ctx.predict(ls, xf)
+        np.testing.assert_array_equal(got[0], want[0])
+        np.testing.assert_array_equal(got[1], want[1])
+
+
 @pytest.mark.parametrize("N,d,P", [(1000, 2, 12), (2049, 3, 5), (4096, 3, 1)])
 def test_early_diagonal_factor_matches_fused(ctx, monkeypatch, N, d, P):
     """The early diagonal factor (k_step<SPLIT, 1>: block J factored by extra workgroups at the
