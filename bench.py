@@ -73,7 +73,7 @@ def _profile_order(f):
     return (int(rd.group(1)) if rd else -1, int(rd.group(2) or 0) if rd else 0, int(vm.group(1)) if vm else -1, f.name)
 
 
-def pmc_traffic(N, d, swarm):
+def pmc_traffic(N, d, swarm, kernel="k_step"):
     """HBM bytes per k_step launch from the newest committed rocprofv3 PMC passes
     (scripts/pmc_traffic.py writes profiles/<round>/[vK_]k_step_traffic.json), or None."""
     best = None
@@ -82,7 +82,7 @@ def pmc_traffic(N, d, swarm):
             t = json.loads(f.read_text())
         except (OSError, ValueError):
             continue
-        if t.get("N") == N and t.get("d") == d and t.get("swarm") == swarm:
+        if t.get("N") == N and t.get("d") == d and t.get("swarm") == swarm and t.get("kernel", "k_step") == kernel:
             best = {"bytes_per_launch": t["bytes_per_launch"], "source": str(f.relative_to(ROOT)),
                     "groups": t.get("particle_groups", 1), "per": t.get("per")}
     return best
@@ -350,7 +350,7 @@ def secondary_configs(ctx, args, peak):
         out.append({"config": name, "N": N, "d": d, "particles": P, "hetero_noise": hetero, "seed": seed,
                     "steps": steps, "warmup": warm, "value": v, "unit": "evals/s", "ms_per_step": dt / steps * 1e3,
                     "achieved_tflops": v * fl / 1e12, "frac": v * fl / 1e12 / FP64_MFMA_PEAK_TFLOPS,
-                    "frac_of_box_peak": (v * fl / 1e12 / peak) if peak else None,
+                    "frac_of_box_ceiling": (v * fl / 1e12 / peak) if peak else None,
                     "flops_per_eval": fl, "formulation": "potrf+trtri (2/3 Npad^3 per eval)"})
     return out
 
@@ -557,8 +557,16 @@ def main():
                "live_fraction_rank0": live / max(1, (sw.evals - e0) / world)}
 
     # roofline of the dominant kernel, from HIP events on the library's streams
-    groups = gpfit.plan_check(spg, -(-N // 128))["groups"]
-    if groups == 1:
+    plan = gpfit.plan_check(spg, -(-N // 128))
+    groups = plan["groups"]
+    persistent = bool(plan["persistent"])
+    if persistent:
+        # one k_factor launch per batch covers every block column of every particle (block 0 is
+        # k_diag's, the diagonal blocks' K entries k_build_cov's)
+        achieved = prof["panel_flops"] / (prof["panel_ms"] * 1e-3) / 1e12 if prof["panel_ms"] > 0 else None
+        timing = ("k_factor launch (the persistent factorisation: one launch per batch, every block column of "
+                  "every particle), HIP events on the library stream")
+    elif groups == 1:
         # one stream: the launches do not overlap, per-launch event time is exact
         achieved = prof["panel_flops"] / (prof["panel_ms"] * 1e-3) / 1e12 if prof["panel_ms"] > 0 else None
         timing = "k_step launch average (HIP events on the library stream)"
@@ -576,21 +584,30 @@ def main():
     # SIMD (gpf_mfma_peak), at whatever clock the chip holds under that load; boxes of the pool
     # differ, so fractions against it are checkable per box
     box_peak = ctx.mfma_peak(blocks=1024, iters=8192) if rank == 0 else None
-    traffic = pmc_traffic(N, d, spg)
-    roof = {"kernel": "k_step", "bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
+    traffic = pmc_traffic(N, d, spg, "k_factor" if persistent else "k_step")
+    roof = {"kernel": "k_factor" if persistent else "k_step", "bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
             "traffic": traffic["bytes_per_launch"] if traffic else None,
             "traffic_source": traffic["source"] if traffic else None,
             # per k_step launch, like flops_per_launch: with particle groups a launch covers one
             # group's particles (the PMC pass ran the same schedule)
-            "traffic_per": (f"k_step launch of one of {traffic['groups']} particle groups"
-                            if traffic and traffic["groups"] > 1 else "k_step launch") if traffic else None,
+            "traffic_per": ("k_factor launch (one per batch)" if persistent else
+                            f"k_step launch of one of {traffic['groups']} particle groups"
+                            if traffic["groups"] > 1 else "k_step launch") if traffic else None,
             "timing": timing + "; measured over a second timed pass of the same steps with an event pair "
                                "around every launch (the `value` pass records no events)",
             "ms_per_step_profiled_pass": dt_prof / args.steps * 1e3 if dt_prof else None,
             "particle_groups": groups,
-            "box_fp64_mfma_tflops": box_peak,
-            "frac_of_box_peak": (achieved / box_peak) if (achieved and box_peak) else None,
+            "persistent": persistent,
+            # this box: the shader clock the factor kernels held (in-kernel s_memtime / s_memrealtime
+            # spans of every workgroup, profiled pass) and the FP64 matrix ceiling at that clock
+            # (128 flop per CU per clock; 78.6 TF/s is the 2.4 GHz spec); and a dense MFMA loop's rate
+            # (gpf_mfma_peak: power-bound, it throttles the clock well below what k_step runs at)
+            "box_sclk_mhz": prof["factor_sclk_mhz"] or None,
+            "box_fp64_ceiling_tflops": prof["fp64_ceiling_at_sclk_tflops"] or None,
+            "frac_of_box_ceiling": (achieved / prof["fp64_ceiling_at_sclk_tflops"])
+            if (achieved and prof["fp64_ceiling_at_sclk_tflops"]) else None,
+            "box_dense_mfma_loop_tflops": box_peak,
             "gemm_core_tflops": core,
             "frac_of_gemm_core": (achieved / core) if (achieved and core) else None,
             "launches": prof["panel_launches"], "avg_launch_ms": prof["panel_ms"] / max(prof["panel_launches"], 1),
@@ -624,7 +641,7 @@ def main():
         hull = hull_line(ctx, args)
     secondary = None
     if solo and not args.no_secondary:
-        secondary = secondary_configs(ctx, args, box_peak)
+        secondary = secondary_configs(ctx, args, prof["fp64_ceiling_at_sclk_tflops"] or None)
     if solo and not args.no_cpu:
         cpu = cpu_baselines(x, y, e, lo, hi, N, d, args.seed)
 

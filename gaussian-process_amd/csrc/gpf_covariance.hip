@@ -26,7 +26,8 @@ __global__ __launch_bounds__(NTHR) void k_build_cov(int N, int Npad, int d, cons
                                                     const double* __restrict__ y, const double* __restrict__ e,
                                                     const double* __restrict__ ls, double* __restrict__ Lb,
                                                     double* __restrict__ yb, int* __restrict__ info, int diag_only,
-                                                    int* __restrict__ dflag, int* __restrict__ cflag) {
+                                                    int* __restrict__ dflag, int* __restrict__ cflag,
+                                                    int* __restrict__ pst, long long pstride, int pnt) {
   __shared__ double ai[DMAX][BT];
   __shared__ double aj[DMAX][BT];
   __shared__ double ni[BT], nj[BT];
@@ -51,6 +52,16 @@ __global__ __launch_bounds__(NTHR) void k_build_cov(int N, int Npad, int d, cons
     dflag[p] = -1;  // no diagonal block published yet (early diagonal factor, k_step)
     cflag[p] = -1;  // no critical tile published yet (quadrant finish, k_step)
   }
+  // the persistent factorisation's counters (gpf_persist.hip PState: lcol | ucol | sdone, each
+  // [P][nt], then the queue heads and the abort word): block column I of particle p starts with
+  // nothing finished, except U block 0, which k_diag factors before k_factor runs
+  if (pst && diag_only && (idx % 3) == 0 && tid == 0) {
+    const int I = idx / 3;
+    pst[(size_t)p * pnt + I] = 0;
+    pst[pstride + (size_t)p * pnt + I] = (I == 0) ? 1 : 0;
+    pst[2 * pstride + (size_t)p * pnt + I] = 0;
+  }
+  if (pst && idx == 0 && p == 0 && tid < 16) pst[3 * pstride + tid] = 0;
 
   if (tid < 128) {
     const int t = tid & 63;

@@ -1112,16 +1112,20 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
     }
     __syncthreads();
     if (*flag) return false;  // timed out: the host reports it
-    const double* p0 =
-        launder(pt + (size_t)(sib << l) * T * T + (size_t)(qd.rb + (qd.lane >> 4)) * T + qd.cb + (qd.lane & 15));
-    // two row blocks (8 loads) per scheduling region: issued all at once, the sibling's 32 values
-    // plus the 32 accumulators exceeded the 128-register budget and spilled
+    // the sibling's node sum through a buffer descriptor: one 32-bit per-lane offset and the
+    // element displacements in soffset (64-bit per-element addresses were hoisted out of the tree
+    // loop and spilled)
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(pt + (size_t)(sib << l) * T * T), 0, T * T * 8,
+                                                      0x00020000);
+    const int vo = 8 * ((qd.rb + (qd.lane >> 4)) * T + qd.cb + (qd.lane & 15));
 #pragma unroll
     for (int mi = 0; mi < Acc<T>::MBR; ++mi) {
 #pragma unroll
       for (int ni = 0; ni < Acc<T>::MBC; ++ni)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc.v[mi][ni][r] = acc.v[mi][ni][r] + p0[(mi * 16 + 4 * r) * T + ni * 16];
+        for (int r = 0; r < 4; ++r)
+          acc.v[mi][ni][r] = acc.v[mi][ni][r] + __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                                            rs, vo, 8 * ((mi * 16 + 4 * r) * T + ni * 16), 0));
       if (mi & 1) __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -1390,8 +1394,10 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
                                                   int d, int S, int S2, double* __restrict__ part,
                                                   unsigned* __restrict__ cnt, int* __restrict__ dflag, int ed,
                                                   int* __restrict__ yflag, int defer, int sy, int spins, int la,
-                                                  double* __restrict__ lab) {
+                                                  double* __restrict__ lab, unsigned long long* __restrict__ clk) {
   const int tid = threadIdx.x;
+  ClockSpan span;
+  span.start(clk);
 #ifdef GPF_WG_TRACE
   if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) {
     unsigned hw, xcc;
@@ -1460,6 +1466,7 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
     step_item<SPLIT, ED>(role, J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, S2, sidx, part, cnt, &sflag,
                          dflag, yflag, defer, spins, la, lab, lds);
   }
+  span.stop(clk);
 #ifdef GPF_WG_TRACE
   __syncthreads();
   if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) g_wg_trace[J][blockIdx.x][1] = realtime();

@@ -8,46 +8,62 @@
 
 namespace gpf {
 
-// vsq[t][q*128 + c] = sum over the 128 rows of tile t of (U_t,<=t K_s[:, q-tile])^2.
-// Each wave holds all 128 rows of its 16 columns: the sum runs per lane over the rows of each
-// row half, then over the 4 lane groups, then upper half + lower half (fixed order).
-// grid: (nqt, nt)
+// Row tile t of V = U K_s (GP_func.py:38: v = solve(L, K_s), with U = L^-1), reduced per column
+// in registers and never stored:
+//   vsq[t][q*128 + c] = sum over the 128 rows of tile t of V(r, c)^2        (GP_func.py:39)
+//   vz [t][q*128 + c] = sum over the same rows of V(r, c) z_t(r)
+// where z = U y: sum_t vz[t] = (U K_s)^T U y = K_s^T alpha = mu (GP_func.py:36), so the mean needs
+// neither alpha nor a second pass over K_s. Each wave holds all 128 rows of its 16 columns: the
+// sums run per lane over the rows of each row half, then over the 4 lane groups, then upper half
+// + lower half (fixed order). Row tiles t0 .. t0 + gridDim.y - 1, the deepest first (t = nt-1
+// streams (t+1) x 128 deep: the dispatch order is x fastest, so the longest workgroups start in the
+// first rounds instead of forming the launch's tail).
+// grid: (nqt, rows)
 __global__ __launch_bounds__(Geo<T>::NTH, 4) void k_predict_vsq(int Npad, const double* __restrict__ U,
                                                          const double* __restrict__ Ks, int ldks,
-                                                         double* __restrict__ vsq) {
+                                                         double* __restrict__ vsq, const double* __restrict__ z,
+                                                         double* __restrict__ vz, int t0) {
   __shared__ __attribute__((aligned(16))) double smem[DL_STAGE];
-  // deepest row tiles first (t = nt-1 streams (t+1) x 128 deep): the dispatch order is x fastest,
-  // so the longest workgroups start in the first rounds instead of forming the launch's tail
-  const int q = blockIdx.x, t = (int)gridDim.y - 1 - (int)blockIdx.y;
+  const int q = blockIdx.x, t = t0 + (int)gridDim.y - 1 - (int)blockIdx.y;
   const Quad<T> qd;
   Acc<T> acc;
   acc.zero();
   // U is lower triangular: row tile t needs columns [0, (t+1) * 128)
   gemm_stream_dl<true>(acc, U + (size_t)t * T * Npad, Npad, Ks + (size_t)q * T, ldks, (t + 1) * T, smem, qd);
   constexpr int MBR = Geo<T>::MBR;
-  double half[2];
+  const double* zt = z + (size_t)t * T + (qd.lane >> 4);
+  double half[2], zh[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    double a2 = 0.0;
+    double a2 = 0.0, az = 0.0;
 #pragma unroll
     for (int mi = h * MBR / 2; mi < (h + 1) * MBR / 2; ++mi)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) a2 = fma(acc.v[mi][0][r], acc.v[mi][0][r], a2);
+      for (int r = 0; r < 4; ++r) {
+        a2 = fma(acc.v[mi][0][r], acc.v[mi][0][r], a2);
+        az = fma(acc.v[mi][0][r], zt[mi * 16 + 4 * r], az);
+      }
     half[h] = sum_lane_groups(a2);
+    zh[h] = sum_lane_groups(az);
   }
-  if ((qd.lane >> 4) == 0) vsq[(size_t)t * ldks + (size_t)q * T + qd.col(0)] = half[0] + half[1];
+  if ((qd.lane >> 4) == 0) {
+    const size_t o = (size_t)t * ldks + (size_t)q * T + qd.col(0);
+    vsq[o] = half[0] + half[1];
+    vz[o] = zh[0] + zh[1];
+  }
 }
 
-// mu_q = K_s[:, q]^T alpha (GP_func.py:36); var = clip(1 - sum v^2, 1e-12) (:39-40)
+// mu_q = sum_t vz[t][q] = K_s[:, q]^T alpha (GP_func.py:36; k_predict_vsq: V^T z, the row tiles in
+// order; the reference's GEMV re-read all of K_s, 331 MB per 10k queries at N=4096);
+// var = clip(1 - sum v^2, 1e-12) (:39-40)
 // grid: (ceil(M/256))
-__global__ __launch_bounds__(NTHR) void k_predict_out(int N, int nt, int M, const double* __restrict__ Ks, int ldks,
-                                                      const double* __restrict__ alpha,
+__global__ __launch_bounds__(NTHR) void k_predict_out(int nt, int M, const double* __restrict__ vz, int ldks,
                                                       const double* __restrict__ vsq, double* __restrict__ mu,
                                                       double* __restrict__ sd) {
   const int q = blockIdx.x * NTHR + threadIdx.x;
   if (q >= M) return;
   double m = 0.0;
-  for (int i = 0; i < N; ++i) m = fma(Ks[(size_t)i * ldks + q], alpha[i], m);
+  for (int t = 0; t < nt; ++t) m = m + vz[(size_t)t * ldks + q];
   double s = 0.0;
   for (int t = 0; t < nt; ++t) s = s + vsq[(size_t)t * ldks + q];
   double var = 1.0 - s;

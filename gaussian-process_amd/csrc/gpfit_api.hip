@@ -22,6 +22,7 @@
 #include "gpf_common.hip"
 #include "gpf_covariance.hip"
 #include "gpf_factor.hip"
+#include "gpf_persist.hip"
 #include "gpf_objective.hip"
 #include "gpf_predict.hip"
 #include "gpf_probsurf.hip"
@@ -90,9 +91,14 @@ struct gpf_ctx {
   int* d_info = nullptr;
   int* d_flag = nullptr;  // per particle: last diagonal block published in the running launch (early_diag)
   int* d_cflag = nullptr;  // per particle: last diagonal block reduced by a SYRK workgroup (defer_syrk); reset by k_build_cov
+  int* d_pst = nullptr;    // the persistent factorisation's counters (gpf::PState: 3 x cap x nt, heads, abort); reset by k_build_cov
+  int ncu = 0;             // compute units of the device (the persistent launch's grid: two workgroups per CU)
   // gpf_predict's query-chunk buffers, kept between calls (grow-only; freed with the work buffers)
   double *p_xf = nullptr, *p_ks = nullptr, *p_vsq = nullptr, *p_mu = nullptr, *p_sd = nullptr;
   double *p_hx = nullptr, *p_hout = nullptr;  // pinned staging: query coordinates, (mu, sd)
+  double* p_vz = nullptr;                      // per row tile of V = U K_s: V^T z partials of mu (gpf::k_predict_vsq)
+  std::vector<hipEvent_t> pev;                 // gpf_predict: factor launch J done (row tile J of U final), nt of them
+  hipEvent_t pev_x = nullptr, pev_side = nullptr;
   int64_t p_cols = 0, p_np = 0;
   int p_d = 0, p_nt = 0;
   // gpf_prob_surface's row-chunk buffers, kept between calls like the prediction's
@@ -114,6 +120,7 @@ struct gpf_ctx {
 
   // profiling
   bool prof = false;
+  unsigned long long* d_clk = nullptr;  // shader-clock probe of the factor kernels (gpf::ClockSpan), profiling only
   double acc[PC_N][3] = {};  // ms, launches, work
   double evals = 0;
   std::vector<Pending> pend;
@@ -192,9 +199,9 @@ static void clear_graphs(gpf_ctx* c) {
 }
 
 static void free_pred(gpf_ctx* c) {
-  hipFree(c->p_xf); hipFree(c->p_ks); hipFree(c->p_vsq); hipFree(c->p_mu); hipFree(c->p_sd);
+  hipFree(c->p_xf); hipFree(c->p_ks); hipFree(c->p_vsq); hipFree(c->p_mu); hipFree(c->p_sd); hipFree(c->p_vz);
   hipHostFree(c->p_hx); hipHostFree(c->p_hout);
-  c->p_xf = c->p_ks = c->p_vsq = c->p_mu = c->p_sd = nullptr;
+  c->p_xf = c->p_ks = c->p_vsq = c->p_mu = c->p_sd = c->p_vz = nullptr;
   c->p_hx = c->p_hout = nullptr;
   c->p_cols = c->p_np = 0;
   c->p_d = c->p_nt = 0;
@@ -232,6 +239,8 @@ static void free_work(gpf_ctx* c) {
   c->d_flag = nullptr;
   hipFree(c->d_cflag);
   c->d_cflag = nullptr;
+  hipFree(c->d_pst);
+  c->d_pst = nullptr;
   hipFree(c->d_part); hipFree(c->d_cnt);
   c->d_part = nullptr;
   c->d_cnt = nullptr;
@@ -279,6 +288,7 @@ static int ensure_work(gpf_ctx* c, int want) {
   GPF_HIP(c, hipMalloc(&c->d_info, (size_t)cap * 4));
   GPF_HIP(c, hipMalloc(&c->d_flag, (size_t)cap * 4));  // reset by k_build_cov at every factorisation
   GPF_HIP(c, hipMalloc(&c->d_cflag, (size_t)cap * 4));  // likewise
+  GPF_HIP(c, hipMalloc(&c->d_pst, ((size_t)3 * cap * c->nt + 16) * 4));  // likewise (persistent factorisation)
   GPF_HIP(c, hipMalloc(&c->d_hist, (size_t)cap * (c->K + 1) * 4));
   // on the library stream: the legacy null stream does not order against our non-blocking streams
   GPF_HIP(c, hipMemsetAsync(c->d_hist, 0, (size_t)cap * (c->K + 1) * 4, c->stream));  // k_score re-zeroes what it read
@@ -296,7 +306,17 @@ static int ensure_work(gpf_ctx* c, int want) {
 // evals/s, same box), -19% at N=1024 P=32, 4 groups worse everywhere. Default: 2 groups for
 // chunks with at least 16 block columns, else 1. (With concurrent groups the per-launch times
 // overlap, so bench.py rates the whole factorisation phase instead: no gaps or overlap counted.)
+// Persistent factorisation (gpf::k_factor, gpf_persist.hip) for the slot-bound schedules: more
+// tiles per block column than the 512 workgroup slots (config C, D's and E's per-GPU shares),
+// where the per-block-column launches drain between columns. GPF_PERSIST = 0/1 overrides.
+static bool persist_on(int pc, int nt) {
+  bool on = (long long)pc * (nt - 1) > 512;
+  if (const char* s = getenv("GPF_PERSIST")) on = atoi(s) != 0;
+  return on && nt >= 3;
+}
+
 static int num_groups(int pc, int nt) {
+  if (persist_on(pc, nt)) return 1;  // one launch over every particle
   int g = nt >= 16 ? 2 : 1;
   if (const char* s = getenv("GPF_GROUPS")) g = atoi(s);
   g = std::max(1, std::min(g, MAX_GROUPS));
@@ -543,18 +563,19 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
 // factors block 0 first and each launch J factors block J+1 at the end of its critical tile;
 // with the early diagonal factor launch J itself starts with the factor of block J. Joins back
 // into c->stream.
-static int run_factor(gpf_ctx* c, int pc) {
+static int run_factor(gpf_ctx* c, int pc, hipEvent_t* after = nullptr) {
   const int nt = c->nt, Np = (int)c->Npad, N = (int)c->N;
   const double Tf = (double)T, t3 = Tf * Tf * Tf;
   const int nb = Np / BT;
   const int ntri = nb * (nb + 1) / 2;
   const size_t ld = (size_t)Np;
   const int ng = num_groups(pc, nt);
+  const bool persist = persist_on(pc, nt);
   // algorithmic flops of block-column launch J per particle, potrf + trtri (2/3 N^3) formulation:
   //   L tile: depth-128J GEMM 2 T^3 J + triangular multiply T^3 + look-ahead syrk share T^3
   //   U tile: depth-128(J-K) GEMM with a triangular factor 2 T^3 (J-K) - T^3 + triangular multiply T^3
   //   diagonal block: 2/3 T^3 (block J+1 fused at the end of launch J, or block J early in it)
-  const bool ed = early_diag(pc, nt);
+  const bool ed = !persist && early_diag(pc, nt);
   const int spins = wait_spins();
   auto step_flops = [&](int J) {
     double fl = 0.0;
@@ -601,7 +622,8 @@ static int run_factor(gpf_ctx* c, int pc) {
     const int nbuild = (GPF_KFUSE && nt > 1) ? 3 * nt : ntri;
     int rc = launch_on(c, st, PC_BUILD, 8.0 * nbuild * BT * BT * (double)gc, [&] {
       hipLaunchKernelGGL(gpf::k_build_cov, dim3(nbuild, gc), dim3(NTHR), 0, st, N, Np, c->d, c->d_x, c->d_y, c->d_e,
-                         lsg, Lg, yg, ig, (int)(nbuild != ntri), c->d_flag + p0, c->d_cflag + p0);
+                         lsg, Lg, yg, ig, (int)(nbuild != ntri), c->d_flag + p0, c->d_cflag + p0,
+                         persist ? c->d_pst : nullptr, (long long)c->cap * nt, nt);
     });
     if (rc) return rc;
     if (ed) continue;  // block 0 is factored by launch 0's diagonal workgroups
@@ -612,6 +634,27 @@ static int run_factor(gpf_ctx* c, int pc) {
     });
     if (rc) return rc;
     total += (2.0 / 3.0) * t3 * gc;
+  }
+  if (persist) {
+    // one persistent launch: every block column of every particle (gpf_persist.hip)
+    double fl = 0.0;
+    for (int J = 0; J < nt; ++J) fl += step_flops(J);
+    gpf::PItem a{nt, Np, N, c->d, spins, c->d_L, c->d_U, c->d_yb, c->d_s2p, c->d_szp, c->d_info, c->d_x, c->d_ls};
+    const size_t ps = (size_t)c->cap * nt;
+    gpf::PState ps_{c->d_pst, c->d_pst + ps, c->d_pst + 2 * ps, reinterpret_cast<unsigned*>(c->d_pst + 3 * ps),
+                    c->d_pst + 3 * ps + gpf::PQ_MAX};
+    const int rc = launch_on(c, c->stream, PC_PANEL, fl * pc, [&] {
+      hipLaunchKernelGGL(gpf::k_factor, dim3((unsigned)gpf::p_total_items(pc, nt)), dim3(gpf::STEP_NTH), 0, c->stream, a,
+                         ps_, pc, c->prof ? c->d_clk : nullptr);
+    });
+    if (rc) return rc;
+    total += fl * pc;
+    for (int J = 0; after && J < nt; ++J) GPF_HIP(c, hipEventRecord(after[J], c->stream));
+    if (c->prof && wa && wb) {
+      hipEventRecord(wb, c->stream);
+      c->pend.push_back({wa, wb, PC_FACTOR, total});
+    }
+    return GPF_OK;
   }
   // block-column launches (split-K for launches with few tiles, planned above)
   std::vector<StepLaunch> plan;
@@ -644,10 +687,12 @@ static int run_factor(gpf_ctx* c, int pc) {
                          c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc, l.grp, N, c->d_x,
                          c->d_ls + (size_t)p0 * c->d, c->d, l.S, l.S2, partg, cntg, c->d_flag + p0, l.ed,
                          c->d_cflag + p0, l.defer, l.sy, spins, l.la | ((l.la & 2) ? la_delay : 0),
-                         l.la ? c->d_la + 2 * (size_t)p0 * T * T : nullptr);
+                         l.la ? c->d_la + 2 * (size_t)p0 * T * T : nullptr, c->prof ? c->d_clk : nullptr);
     });
     if (rc) return rc;
     total += fl * gc;
+    // (ng == 1 where events are asked for: the single-particle factorisation of gpf_predict)
+    if (after && l.g == 0) GPF_HIP(c, hipEventRecord(after[l.J], st));
   }
   if (ng > 1) {
     for (int g = 0; g < ng; ++g) {
@@ -737,6 +782,7 @@ int gpf_open(int device, gpf_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return GPF_HIP_ERROR;
   gpf_ctx* c = new gpf_ctx();
   c->device = device;
+  if (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->ncu <= 0) c->ncu = 256;
   bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
   for (int g = 0; ok && g < MAX_GROUPS; ++g)
@@ -757,8 +803,12 @@ void gpf_close(gpf_ctx* c) {
   harvest(c);
   free_work(c);
   hipFree(c->d_x); hipFree(c->d_y); hipFree(c->d_e);
+  hipFree(c->d_clk);
   hipFree(c->d_sig); hipFree(c->d_exp); hipFree(c->d_lo); hipFree(c->d_hi);
   for (auto e : c->pool) hipEventDestroy(e);
+  for (auto e : c->pev) hipEventDestroy(e);
+  if (c->pev_x) hipEventDestroy(c->pev_x);
+  if (c->pev_side) hipEventDestroy(c->pev_side);
   for (int g = 0; g < MAX_GROUPS; ++g) {
     if (c->sub[g]) hipStreamDestroy(c->sub[g]);
     if (c->join[g]) hipEventDestroy(c->join[g]);
@@ -958,13 +1008,17 @@ int gpf_eval_batch(gpf_ctx* c, const double* ls, int P, double* loss, double* mu
 // the factor's status word is copied to the pinned c->h_info[0] behind it on c->stream, and the
 // caller checks it (factor_status) after its next synchronisation — gpf_predict queues the query
 // kernels right behind the factorisation instead of idling the GPU for a host round trip.
-static int factor_single_async(gpf_ctx* c, const double* ls, double** alpha_out) {
+// ls == nullptr: the length scales are already in d_ls (queued on c->stream by the caller).
+// after (nullable): an event per block column, recorded behind its launch.
+static int factor_single_async(gpf_ctx* c, const double* ls, double** alpha_out, hipEvent_t* after = nullptr) {
   int rc = ensure_work(c, 1);
   if (rc) return rc;
-  std::memcpy(c->h_ls, ls, (size_t)c->d * 8);
-  GPF_HIP(c, hipMemcpyAsync(c->d_ls, c->h_ls, (size_t)c->d * 8, hipMemcpyHostToDevice, c->stream));
+  if (ls) {
+    std::memcpy(c->h_ls, ls, (size_t)c->d * 8);
+    GPF_HIP(c, hipMemcpyAsync(c->d_ls, c->h_ls, (size_t)c->d * 8, hipMemcpyHostToDevice, c->stream));
+  }
   GPF_HIP(c, hipMemsetAsync(c->d_info, 0, 4, c->stream));
-  rc = run_factor(c, 1);
+  rc = run_factor(c, 1, after);
   if (rc) return rc;
   // alpha into the mu slot of particle 0
   rc = launch(c, PC_LOSS, 0.0, [&] {
@@ -1023,7 +1077,7 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
   if (!fits) {
     size_t fr = 0, tot = 0;
     GPF_HIP(c, hipMemGetInfo(&fr, &tot));
-    const int64_t per_col = (Np + c->nt) * 8;
+    const int64_t per_col = (Np + 2 * c->nt) * 8;
     const int64_t maxcols = std::max<int64_t>(T, (int64_t)((double)fr * 0.5 / (double)per_col));
     chunk = std::min<int64_t>(chunk, maxcols);
     Cp = ((chunk + T - 1) / T) * T;
@@ -1037,6 +1091,7 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
     GPF_HIP(c, hipMalloc(&c->p_xf, (size_t)c->d * Cp * 8));
     GPF_HIP(c, hipMalloc(&c->p_ks, (size_t)Np * Cp * 8));
     GPF_HIP(c, hipMalloc(&c->p_vsq, (size_t)c->nt * Cp * 8));
+    GPF_HIP(c, hipMalloc(&c->p_vz, (size_t)c->nt * Cp * 8));
     GPF_HIP(c, hipMalloc(&c->p_mu, (size_t)Cp * 8));
     GPF_HIP(c, hipMalloc(&c->p_sd, (size_t)Cp * 8));
     GPF_HIP(c, hipHostMalloc((void**)&c->p_hx, (size_t)c->d * Cp * 8, hipHostMallocDefault));
@@ -1046,40 +1101,87 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
     c->p_d = c->d;
     c->p_nt = c->nt;
   }
-  double* alpha = nullptr;
-  int rc = factor_single_async(c, ls, &alpha);
-  if (rc) return rc;
-  double *d_xf = c->p_xf, *d_ks = c->p_ks, *d_vsq = c->p_vsq, *d_mu = c->p_mu, *d_sd = c->p_sd;
+  // Pipelined (GPF_PREDICT_PIPE, default on): the first query chunk's cross-covariance and its
+  // V = U K_s run on a side stream beside the factorisation, row tile t of V as soon as the
+  // factor's launch t has finished row tile t of U (and z_t): the single-particle factorisation
+  // is a chain of nt latency-bound launches that leave most of the chip idle, and V's row tiles
+  // fill it (GP_fit.py:32 -> GP_func.py:22-40). Later chunks follow on the main stream.
+  bool pipe = c->nt >= 2;
+  if (const char* e = getenv("GPF_PREDICT_PIPE")) pipe = pipe && atoi(e) != 0;
+  hipStream_t side = c->sub[MAX_GROUPS - 1];  // (the group streams: the single-particle factor uses one)
+  if (pipe) {
+    if (!c->pev_x) GPF_HIP(c, hipEventCreateWithFlags(&c->pev_x, hipEventDisableTiming));
+    if (!c->pev_side) GPF_HIP(c, hipEventCreateWithFlags(&c->pev_side, hipEventDisableTiming));
+    while ((int)c->pev.size() < c->nt) {
+      hipEvent_t e = nullptr;
+      GPF_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      c->pev.push_back(e);
+    }
+  }
+  double *d_xf = c->p_xf, *d_ks = c->p_ks, *d_vsq = c->p_vsq, *d_vz = c->p_vz, *d_mu = c->p_mu, *d_sd = c->p_sd;
   double* hx = c->p_hx;
-  rc = GPF_OK;
-  for (int64_t s = 0; s < M && rc == GPF_OK; s += chunk) {
-    const int64_t m = std::min<int64_t>(chunk, M - s);
-    if (s > 0 && hipStreamSynchronize(c->stream) != hipSuccess) {  // the staging buffer is reused
-      rc = GPF_HIP_ERROR;
-      break;
-    }
-    for (int k = 0; k < c->d; ++k) std::memcpy(hx + (size_t)k * Cp, xfit + (size_t)k * M + s, (size_t)m * 8);
-    if (hipMemcpyAsync(d_xf, hx, (size_t)c->d * Cp * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
-      rc = GPF_HIP_ERROR;
-      break;
-    }
-    const int nqt = (int)((m + T - 1) / T);
-    const int Cm = nqt * T;
-    rc = launch(c, PC_PREDK, 8.0 * Np * Cm, [&] {
-      gpf::launch_cross_cov(c->stream, (int)c->N, (int)m, (int)Np, Cm, c->d, c->d_x, (int)c->N, d_xf, (int)Cp, c->d_ls, d_ks,
+  const double* d_z = c->d_yb;  // z = U y of particle slot 0 (row tile t final after factor launch t)
+  auto stage_chunk = [&](int64_t s0, int64_t m) -> int {
+    for (int k = 0; k < c->d; ++k) std::memcpy(hx + (size_t)k * Cp, xfit + (size_t)k * M + s0, (size_t)m * 8);
+    GPF_HIP(c, hipMemcpyAsync(d_xf, hx, (size_t)c->d * Cp * 8, hipMemcpyHostToDevice, c->stream));
+    return GPF_OK;
+  };
+  auto cross_cov = [&](hipStream_t st, int64_t m, int Cm) {
+    return launch_on(c, st, PC_PREDK, 8.0 * Np * Cm, [&] {
+      gpf::launch_cross_cov(st, (int)c->N, (int)m, (int)Np, Cm, c->d, c->d_x, (int)c->N, d_xf, (int)Cp, c->d_ls, d_ks,
                             (int64_t)Cp);
     });
-    if (rc) break;
-    // V = U K_s: row tile t of U has (t+1) column tiles, the last one triangular
-    const double vflops = 2.0 * T * T * (double)Cm * (c->nt * (c->nt + 1) / 2) - (double)T * T * Cm * c->nt;
-    rc = launch(c, PC_PRED, vflops, [&] {
-      hipLaunchKernelGGL(gpf::k_predict_vsq, dim3(nqt, c->nt), dim3(gpf::Geo<T>::NTH), 0, c->stream, (int)Np, c->d_U, d_ks,
-                         (int)Cp, d_vsq);
+  };
+  // V = U K_s for row tiles [t0, t0 + rows): row tile t of U has (t+1) column tiles, the last triangular
+  auto vsq = [&](hipStream_t st, int nqt, int t0, int rows) {
+    const double Cm = (double)nqt * T;
+    const double vflops = 2.0 * T * T * Cm * ((double)(t0 + rows) * (t0 + rows + 1) / 2 - (double)t0 * (t0 + 1) / 2) -
+                          (double)T * T * Cm * rows;
+    return launch_on(c, st, PC_PRED, vflops, [&] {
+      hipLaunchKernelGGL(gpf::k_predict_vsq, dim3(nqt, rows), dim3(gpf::Geo<T>::NTH), 0, st, (int)Np, c->d_U, d_ks,
+                         (int)Cp, d_vsq, d_z, d_vz, t0);
     });
-    if (rc) break;
+  };
+  // the length scales and chunk 0's coordinates first, then the factorisation
+  std::memcpy(c->h_ls, ls, (size_t)c->d * 8);
+  GPF_HIP(c, hipMemcpyAsync(c->d_ls, c->h_ls, (size_t)c->d * 8, hipMemcpyHostToDevice, c->stream));
+  int rc = stage_chunk(0, std::min<int64_t>(chunk, M));
+  if (rc) return rc;
+  if (pipe) GPF_HIP(c, hipEventRecord(c->pev_x, c->stream));
+  double* alpha = nullptr;
+  rc = factor_single_async(c, nullptr, &alpha, pipe ? c->pev.data() : nullptr);
+  if (rc) return rc;
+  if (pipe) {
+    const int64_t m = std::min<int64_t>(chunk, M);
+    const int nqt = (int)((m + T - 1) / T);
+    GPF_HIP(c, hipStreamWaitEvent(side, c->pev_x, 0));
+    rc = cross_cov(side, m, nqt * T);
+    for (int t = 0; rc == GPF_OK && t < c->nt; ++t) {
+      GPF_HIP(c, hipStreamWaitEvent(side, c->pev[t], 0));
+      rc = vsq(side, nqt, t, 1);
+    }
+    if (rc) return rc;
+    GPF_HIP(c, hipEventRecord(c->pev_side, side));
+    GPF_HIP(c, hipStreamWaitEvent(c->stream, c->pev_side, 0));
+  }
+  for (int64_t s = 0; s < M && rc == GPF_OK; s += chunk) {
+    const int64_t m = std::min<int64_t>(chunk, M - s);
+    const int nqt = (int)((m + T - 1) / T);
+    const int Cm = nqt * T;
+    if (s > 0) {
+      if (hipStreamSynchronize(c->stream) != hipSuccess) {  // the staging buffer is reused
+        rc = GPF_HIP_ERROR;
+        break;
+      }
+      if ((rc = stage_chunk(s, m))) break;
+    }
+    if (!(pipe && s == 0)) {
+      if ((rc = cross_cov(c->stream, m, Cm))) break;
+      if ((rc = vsq(c->stream, nqt, 0, c->nt))) break;
+    }
     rc = launch(c, PC_LOSS, 0.0, [&] {
-      hipLaunchKernelGGL(gpf::k_predict_out, dim3((unsigned)((m + NTHR - 1) / NTHR)), dim3(NTHR), 0, c->stream,
-                         (int)c->N, c->nt, (int)m, d_ks, (int)Cp, alpha, d_vsq, d_mu, d_sd);
+      hipLaunchKernelGGL(gpf::k_predict_out, dim3((unsigned)((m + NTHR - 1) / NTHR)), dim3(NTHR), 0, c->stream, c->nt,
+                         (int)m, d_vz, (int)Cp, d_vsq, d_mu, d_sd);
     });
     if (rc) break;
     if (hipMemcpyAsync(c->p_hout, d_mu, (size_t)m * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
@@ -1096,6 +1198,7 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
     std::memcpy(mu + s, c->p_hout, (size_t)m * 8);
     std::memcpy(sd + s, c->p_hout + Cp, (size_t)m * 8);
   }
+  if (pipe) hipStreamSynchronize(side);
   hipStreamSynchronize(c->stream);
   if (c->prof) harvest(c);
   // keep the query-chunk buffers for the next call only while they are modest (a huge batch_size
@@ -1164,9 +1267,88 @@ static int plan_fail(char* msg, int len, const char* fmt, ...) {
 }
 
 // Host-only structural check of the k_step dispatch plan (no device, no context): see gpfit.h.
+// The persistent factorisation's queues (gpf::p_decode, as k_factor decodes its tickets): every
+// (block column, particle, tile) exactly once, one SYRK item per particle for 1 <= J <= nt-2, every
+// particle in one queue, and each item's inputs (the counters it waits for) produced by items
+// earlier in that queue — the deadlock-freedom argument of gpf_persist.hip.
+static int persist_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
+  const int nq = gpf::p_nq(pc);
+  // done[p][...]: the ticket position at which each counter value first becomes available
+  std::vector<long long> seen((size_t)pc * nt * nt, 0), syrk((size_t)pc * nt, 0);
+  std::vector<int> lcol((size_t)pc * nt, 0), ucol((size_t)pc * nt, 0), sdone((size_t)pc * nt, 0);
+  for (int p = 0; p < pc; ++p) ucol[(size_t)p * nt] = 1;  // k_diag before the launch
+  long long items = 0, tiles = 0, syrks = 0;
+  for (int q = 0; q < nq; ++q) {
+    const long long n = gpf::p_queue_items(pc, nt, q);
+    int Jc = 0;
+    long long bc = 0;
+    for (long long t = 0; t < n; ++t) {
+      int p = -1, w = -2;
+      const int kind = gpf::p_decode(t, pc, nt, q, Jc, bc, p, w);
+      const int J = Jc;
+      if (p < 0 || p >= pc || p % nq != q || J < 0 || J >= nt)
+        return plan_fail(msg, msg_len, "persistent queue %d ticket %lld decodes out of range (J=%d p=%d)", q, t, J, p);
+      int* lc = &lcol[(size_t)p * nt];
+      int* uc = &ucol[(size_t)p * nt];
+      int* sd = &sdone[(size_t)p * nt];
+      // items run in ticket order here: a wait that is not yet satisfied would wait for a later item
+      if (kind == gpf::PK_SYRK) {
+        if (!gpf::p_sy(J, nt) || syrk[(size_t)p * nt + J]++)
+          return plan_fail(msg, msg_len, "persistent: misplaced or duplicate SYRK item J=%d p=%d", J, p);
+        if (lc[J + 1] < J) return plan_fail(msg, msg_len, "persistent: SYRK J=%d p=%d before its row", J, p);
+        sd[J + 1] = 1;
+        ++syrks;
+      } else {
+        if (w < 0 || w >= nt - 1) return plan_fail(msg, msg_len, "persistent: tile %d out of range (J=%d)", w, J);
+        long long& cnt = seen[((size_t)p * nt + J) * nt + w];
+        if (cnt++) return plan_fail(msg, msg_len, "persistent: tile J=%d p=%d w=%d twice", J, p, w);
+        if (kind == gpf::PK_LTILE) {
+          const int I = J + 1 + w;
+          if ((J > 0 && (lc[I] < J || lc[J] < J)) || uc[J] < J + 1 || (I == J + 1 && J > 0 && !sd[I]))
+            return plan_fail(msg, msg_len, "persistent: L tile (%d, %d) of p=%d ahead of its inputs", J, I, p);
+          if (lc[I] != J) return plan_fail(msg, msg_len, "persistent: row %d of p=%d out of order", I, p);
+          lc[I] = J + 1;
+          if (I == J + 1) uc[I] = I + 1;  // the critical tile factors block I
+        } else {
+          const int K = w - (nt - 1 - J);
+          if (K < 0 || K >= J || lc[J] < J || uc[K] < J || uc[J] < J + 1)
+            return plan_fail(msg, msg_len, "persistent: U tile (%d, %d) of p=%d ahead of its inputs", J, K, p);
+          if (uc[K] != J) return plan_fail(msg, msg_len, "persistent: U column %d of p=%d out of order", K, p);
+          uc[K] = J + 1;
+        }
+        ++tiles;
+      }
+      ++items;
+    }
+  }
+  for (int p = 0; p < pc; ++p)
+    for (int J = 0; J < nt; ++J) {
+      if (syrk[(size_t)p * nt + J] != gpf::p_sy(J, nt))
+        return plan_fail(msg, msg_len, "persistent: particle %d column %d has %lld SYRK items", p, J, syrk[(size_t)p * nt + J]);
+      for (int w = 0; w < nt - 1; ++w)
+        if (seen[((size_t)p * nt + J) * nt + w] != 1)
+          return plan_fail(msg, msg_len, "persistent: tile J=%d p=%d w=%d run %lld times", J, p, w,
+                           seen[((size_t)p * nt + J) * nt + w]);
+    }
+  if (stats) {
+    stats[0] = 1;
+    stats[1] = items;
+    stats[2] = tiles;
+    stats[3] = 0;
+    stats[4] = 1;
+    stats[5] = 1;
+    stats[6] = 1;
+    stats[7] = 0;
+    stats[8] = syrks;
+    stats[9] = 1;
+  }
+  return GPF_OK;
+}
+
 int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
   if (msg && msg_len > 0) msg[0] = 0;
   if (pc <= 0 || nt <= 0) return plan_fail(msg, msg_len, "bad arguments pc=%d nt=%d", pc, nt);
+  if (persist_on(pc, nt)) return persist_check(pc, nt, stats, msg, msg_len);
   int S = 1, Smax = 1;
   split_sizes(pc, nt, S, Smax);
   std::vector<StepLaunch> plan;
@@ -1302,6 +1484,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     stats[6] = ng;
     stats[7] = diag_wgs;
     stats[8] = syrk_wgs;
+    stats[9] = 0;
   }
   return GPF_OK;
 }
@@ -1316,15 +1499,23 @@ int gpf_sync(gpf_ctx* c) {
 int gpf_set_profiling(gpf_ctx* c, int on) {
   if (!c) return GPF_BAD_ARG;
   c->prof = on != 0;  // (profiled batches take the plain launch path, never a graph)
+  if (c->prof && !c->d_clk) {
+    hipSetDevice(c->device);
+    GPF_HIP(c, hipMalloc(&c->d_clk, 2 * sizeof(unsigned long long)));
+    GPF_HIP(c, hipMemsetAsync(c->d_clk, 0, 2 * sizeof(unsigned long long), c->stream));
+  }
   return GPF_OK;
 }
 
 int gpf_reset_profile(gpf_ctx* c) {
   if (!c) return GPF_BAD_ARG;
+  hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   harvest(c);
   std::memset(c->acc, 0, sizeof(c->acc));
   c->evals = 0;
+  if (!c->d_clk) GPF_HIP(c, hipMalloc(&c->d_clk, 2 * sizeof(unsigned long long)));
+  GPF_HIP(c, hipMemsetAsync(c->d_clk, 0, 2 * sizeof(unsigned long long), c->stream));
   return GPF_OK;
 }
 
@@ -1339,8 +1530,15 @@ int gpf_get_profile(gpf_ctx* c, double* out, int n) {
                   c->acc[PC_PRED][0],   c->acc[PC_PRED][1],   c->acc[PC_PRED][2],
                   c->acc[PC_PREDK][0],  c->acc[PC_PREDK][1],  c->acc[PC_PREDK][2],
                   c->acc[PC_PSURF][0],  c->acc[PC_PSURF][1],  c->acc[PC_PSURF][2]};
-  const int m = std::min(n, 24);
-  for (int i = 0; i < m; ++i) out[i] = v[i];
+  // [24] shader clock (MHz) the factor kernels held while they ran (gpf::ClockSpan), [25] the
+  // device's compute units, [26] the FP64 matrix ceiling at that clock (TFLOP/s, 128 flop per CU
+  // per clock)
+  unsigned long long clk[2] = {0, 0};
+  if (c->d_clk) hipMemcpy(clk, c->d_clk, sizeof(clk), hipMemcpyDeviceToHost);
+  const double mhz = clk[1] > 0 ? 100.0 * (double)clk[0] / (double)clk[1] : 0.0;
+  const double w[27 - 24] = {mhz, (double)c->ncu, 128.0 * c->ncu * mhz * 1e6 / 1e12};
+  const int m = std::min(n, 27);
+  for (int i = 0; i < m; ++i) out[i] = i < 24 ? v[i] : w[i - 24];
   return m;
 }
 

@@ -102,13 +102,13 @@ def plan_check(particles, nt):
     """Host-side check of the k_step dispatch plan (gpf_plan_check); raises AssertionError
     naming the first violation, else returns the stats dict. Reads the GPF_* environment."""
     lib = load_library()
-    stats = (ctypes.c_longlong * 9)()
+    stats = (ctypes.c_longlong * 10)()
     msg = ctypes.create_string_buffer(256)
     rc = lib.gpf_plan_check(int(particles), int(nt), stats, msg, 256)
     if rc != GPF_OK:
         raise AssertionError(f"plan_check(pc={particles}, nt={nt}): {msg.value.decode()}")
     keys = ("launches", "workgroups", "whole_tiles", "split_tiles", "S", "Smax", "groups", "diag_workgroups",
-            "syrk_workgroups")
+            "syrk_workgroups", "persistent")
     return dict(zip(keys, list(stats)))
 
 
@@ -261,13 +261,13 @@ class Context:
         self._check(self.lib.gpf_reset_profile(self._h), "gpf_reset_profile")
 
     def profile(self):
-        buf = np.zeros(24)
-        self.lib.gpf_get_profile(self._h, _ptr(buf), 24)
+        buf = np.zeros(27)
+        self.lib.gpf_get_profile(self._h, _ptr(buf), 27)
         keys = ["panel_ms", "panel_launches", "panel_flops", "diag_ms", "diag_launches", "diag_flops",
                 "build_ms", "build_launches", "build_bytes", "loss_ms", "loss_launches", "evals",
                 "factor_wall_ms", "factor_calls", "factor_flops", "predict_ms", "predict_launches",
                 "predict_flops", "predict_cov_ms", "predict_cov_launches", "predict_cov_bytes",
-                "psurf_ms", "psurf_launches", "psurf_bytes"]
+                "psurf_ms", "psurf_launches", "psurf_bytes", "factor_sclk_mhz", "cus", "fp64_ceiling_at_sclk_tflops"]
         return dict(zip(keys, buf.tolist()))
 
     def debug_factor(self, lengths):

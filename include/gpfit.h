@@ -181,6 +181,9 @@ int gpf_set_profiling(gpf_ctx* ctx, int on);
  *  [15] prediction V = U K_s kernel ms  [16] launches  [17] algorithmic flops
  *  [18] prediction cross-covariance ms  [19] launches  [20] algorithmic bytes
  *  [21] probability-surface kernel ms  [22] launches  [23] algorithmic bytes
+ *  [24] shader clock (MHz) the factor kernels held while they ran (every workgroup's span in
+ *       s_memtime clocks over its span in the 100 MHz s_memrealtime clock; profiled batches only)
+ *  [25] compute units  [26] FP64 matrix ceiling at that clock, TFLOP/s (128 flop / CU / clock)
  * Returns the number of values written. */
 int gpf_get_profile(gpf_ctx* ctx, double* out, int n);
 int gpf_reset_profile(gpf_ctx* ctx);
@@ -205,9 +208,14 @@ const char* gpf_build_info(void);
  * diagonal workgroup per particle, ahead of all tiles; with the deferred diagonal update
  * (GPF_DEFER_SYRK, default on) that launches 1 .. nt-2 without the all-tile split carry exactly
  * one SYRK workgroup per particle right behind the diagonal workgroups, and no other launch any.
- * stats (nullable, 9 entries): launches, workgroups, whole tiles, split tiles, S (all-tile
- * split factor), largest split factor, particle groups, diagonal workgroups, SYRK
- * workgroups. Returns GPF_OK, or
+ * Under the persistent factorisation (GPF_PERSIST; default for chunks with more tiles per block
+ * column than 512 workgroup slots) it instead decodes every ticket of every work queue with the
+ * kernel's own decoder (gpf::p_decode): every (block column, particle, tile) exactly once, one
+ * SYRK item per particle and block column 1 .. nt-2, and every item's inputs produced by items
+ * earlier in its queue (what makes the persistent launch deadlock-free).
+ * stats (nullable, 10 entries): launches, workgroups (persistent: items), whole tiles, split
+ * tiles, S (all-tile split factor), largest split factor, particle groups, diagonal
+ * workgroups, SYRK workgroups (items), persistent (0/1). Returns GPF_OK, or
  * GPF_BAD_ARG with a description of the first violation in msg. */
 int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len);
 

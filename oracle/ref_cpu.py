@@ -93,6 +93,30 @@ def GP_train_identity(x_known, y_known, e_known, lengths):
     return mu, np.sqrt(var)
 
 
+def GP_train_identity_tri(x_known, y_known, e_known, lengths):
+    """GP_train_identity with triangular LAPACK kernels (dpotrf, dtrtri): the same identity
+    (find_len_scales.py:159 -> GP_func.py:21-40 at the training points) in (2/3) N^3 flops
+    instead of inv()'s general LU, for the N=16384 checks (config E's share) that the dense
+    inverse makes too slow. Rounding differs from GP_train_identity; both are checked against
+    the HIP path at the north_star tolerance, not bitwise."""
+    from scipy.linalg import lapack
+    K = kernel_func(x_known, x_known, lengths) + np.diag(e_known ** 2)
+    L, info = lapack.dpotrf(K, lower=1, clean=1, overwrite_a=1)
+    del K
+    if info != 0:
+        raise np.linalg.LinAlgError("Matrix is not positive definite")
+    U, info = lapack.dtrtri(L, lower=1, overwrite_c=1)
+    del L
+    assert info == 0
+    z = U @ y_known
+    alpha = U.T @ z
+    dinv = np.einsum("ij,ij->j", U, U)
+    e2 = e_known ** 2
+    mu = y_known - e2 * alpha
+    var = np.clip(e2 - e2 * e2 * dinv, 1e-12, None)
+    return mu, np.sqrt(var)
+
+
 def log_marginal_likelihood(x_known, y_known, e_known, lengths):
     """Diagnostic only: the reference never computes an LML.
 

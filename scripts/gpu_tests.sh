@@ -12,7 +12,8 @@ if [ "${BENCH:-0}" = 1 ]; then
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 r = d["roofline"]
-print("C", round(d["value"], 1), d["unit"], "frac", round(r["frac"], 3), "box peak", r.get("box_fp64_mfma_tflops"))
+print("C", round(d["value"], 1), d["unit"], "frac", round(r["frac"], 3), r["kernel"], "sclk", r.get("box_sclk_mhz"),
+      "ceiling", r.get("box_fp64_ceiling_tflops"), "of ceiling", r.get("frac_of_box_ceiling"))
 for c in d.get("configs") or []:
     print(c["config"], round(c["value"], 1), "evals/s frac", round(c["frac"], 3), "ms/step", round(c["ms_per_step"], 2))
 p = d.get("predict") or {}

@@ -274,6 +274,33 @@ def test_chunked_batches_equal_single_batch(f3, monkeypatch):
     np.testing.assert_array_equal(full, chunked)
 
 
+@pytest.mark.parametrize("N,d,M", [(1500, 2, 20000), (4096, 3, 3000)])
+def test_predict_pipeline_bitwise(ctx, monkeypatch, N, d, M):
+    """gpf_predict's pipelined schedule (the first query chunk's K_s and V = U K_s on a side
+    stream, row tile t of V behind the factor's launch t) against the serial one
+    (GPF_PREDICT_PIPE=0): the same kernels on the same data, so mu and sd bitwise equal; with two
+    query chunks (M > 16384: the second chunk runs on the main stream after the first) and with
+    one; mu = sum_t V_t^T z_t (no alpha) against the oracle's GP() on a sample of the queries."""
+    rng = np.random.default_rng(N + M)
+    x = rng.uniform(size=(d, N))
+    y = np.sin(5 * x[0]) * np.cos(2 * x[-1]) + 0.1 * rng.standard_normal(N)
+    e = rng.uniform(0.05, 0.2, size=N)
+    xf = rng.uniform(-0.1, 1.1, size=(d, M))
+    ls = rng.uniform(0.1, 0.4, size=d)
+    ctx.set_data(x, y, e)
+    monkeypatch.delenv("GPF_PREDICT_PIPE", raising=False)
+    a = ctx.predict(ls, xf)
+    monkeypatch.setenv("GPF_PREDICT_PIPE", "0")
+    b = ctx.predict(ls, xf)
+    monkeypatch.delenv("GPF_PREDICT_PIPE")
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    k = np.linspace(0, M - 1, 64).astype(int)
+    with _blas_threads():
+        m0, s0 = ref_cpu.GP(x, y, e, xf[:, k], ls, batch_size=10000)
+    assert _rel(a[0][k], m0) < RTOL_MU_SD and _rel(a[1][k], s0) < RTOL_MU_SD
+
+
 @pytest.mark.parametrize("keep_mb", [None, "0"])
 def test_predict_buffer_reuse_across_calls(monkeypatch, keep_mb):
     """gpf_predict keeps its query-chunk buffers in the context between calls (grow-only): a
@@ -522,21 +549,27 @@ def test_random_configs_vs_oracle(ctx, N, d, hetero, seed):
 
 
 def _reference_share(ctx, monkeypatch, fx, P, slots, rounds=2):
-    """Score P (with the fixture's particles at `slots`) on the default schedule, twice, and
-    once more with one particle group; returns (loss, mu, sd) of the default run."""
+    """Score P (with the fixture's particles at `slots`) on the default schedule, twice; then on
+    the per-block-column launches (GPF_PERSIST=0: two concurrent particle groups where the
+    default plan has them, and one group); returns (loss, mu, sd) of the default run."""
     from conftest import fixture_data
     x, y, e = fixture_data(fx["meta"], fx["data_sha256"])
     ctx.set_data(x, y, e)
     ctx.set_grid(fx["sigma_vals"], fx["expected"], fx["lo"], fx["hi"])
     monkeypatch.delenv("GPF_GROUPS", raising=False)
+    monkeypatch.delenv("GPF_PERSIST", raising=False)
     runs = [ctx.eval_batch(P, want_mu_sd=True) for _ in range(rounds)]
     for a, b in zip(runs[0], runs[1]):
         np.testing.assert_array_equal(a, b)  # deterministic
-    monkeypatch.setenv("GPF_GROUPS", "1")
-    one = ctx.eval_batch(P, want_mu_sd=True)
+    monkeypatch.setenv("GPF_PERSIST", "0")
+    for groups in (None, "1"):
+        if groups:
+            monkeypatch.setenv("GPF_GROUPS", groups)
+        other = ctx.eval_batch(P, want_mu_sd=True)
+        for a, b in zip(runs[0], other):
+            np.testing.assert_array_equal(a, b)  # the schedule changes, not the arithmetic
     monkeypatch.delenv("GPF_GROUPS", raising=False)
-    for a, b in zip(runs[0], one):
-        np.testing.assert_array_equal(a, b)  # the group split changes the schedule only
+    monkeypatch.delenv("GPF_PERSIST", raising=False)
     loss, mu, sd = runs[0]
     for j, k in enumerate(slots):
         assert _rel(mu[k], fx["mu"][j]) < RTOL_MU_SD, j
@@ -546,14 +579,15 @@ def _reference_share(ctx, monkeypatch, fx, P, slots, rounds=2):
 
 
 def test_configD_share_two_groups_vs_reference(ctx, monkeypatch):
-    """Config D's per-GPU share (N=4096 d=3, 32 particles) on its default schedule: two
-    particle groups on concurrent streams (gpfit.plan_check). The 4 particles of F8 (the
-    reference's own evaluate_loss and the GP() mu/sd inside it, make_golden_big.py) sit among
-    28 others: mu/sd at 1e-6, objective at 1e-8 or threshold ties; deterministic; bitwise
-    equal to the one-group schedule; 4 of the others against the oracle's identity form."""
+    """Config D's per-GPU share (N=4096 d=3, 32 particles) on its default schedule: the
+    persistent factorisation (gpfit.plan_check). The 4 particles of F8 (the reference's own
+    evaluate_loss and the GP() mu/sd inside it, make_golden_big.py) sit among 28 others: mu/sd
+    at 1e-6, objective at 1e-8 or threshold ties; deterministic; bitwise equal to the
+    per-block-column launches (two groups and one); 4 of the others against the oracle's
+    identity form."""
     import gpfit
     from conftest import load_golden
-    assert gpfit.plan_check(32, 32)["groups"] == 2
+    assert gpfit.plan_check(32, 32)["persistent"] == 1
     fx = load_golden("f8_configC.npz")
     rng = np.random.default_rng(404)
     P = rng.uniform(0.05, 0.6, size=(32, 3))
@@ -571,19 +605,19 @@ def test_configD_share_two_groups_vs_reference(ctx, monkeypatch):
 
 def test_configC_full_swarm_vs_reference(ctx, monkeypatch):
     """BASELINE config C exactly as bench.py times it: N=4096 d=3, one 64-particle batch on the
-    default schedule (two particle groups of 32 on concurrent streams, 992 workgroups per
-    launch, two slot rounds). The 4 particles of F8 (the reference's evaluate_loss and the GP()
-    mu/sd inside it, make_golden_big.py) sit among 60 others, two in each group: mu/sd at 1e-6,
-    objective at 1e-8 or threshold ties; deterministic; bitwise equal to the one-group
-    schedule; 4 further particles against the oracle's identity form."""
+    default schedule (the persistent factorisation: one launch of 64 x 1022 items from 8 work
+    queues). The 4 particles of F8 (the reference's evaluate_loss and the GP() mu/sd inside it,
+    make_golden_big.py) sit among 60 others, in 4 different queues: mu/sd at 1e-6, objective at
+    1e-8 or threshold ties; deterministic; bitwise equal to the per-block-column launches (two
+    concurrent groups, and one); 4 further particles against the oracle's identity form."""
     import gpfit
     from conftest import load_golden
     plan = gpfit.plan_check(64, 32)
-    assert plan["groups"] == 2 and plan["diag_workgroups"] == 0  # the slot-bound fused schedule
+    assert plan["persistent"] == 1 and plan["diag_workgroups"] == 0  # the slot-bound fused schedule
     fx = load_golden("f8_configC.npz")
     rng = np.random.default_rng(6464)
     P = rng.uniform(0.05, 0.6, size=(64, 3))
-    slots = [0, 21, 40, 63]  # groups are particles [0, 32) and [32, 64)
+    slots = [0, 21, 40, 63]  # queues p mod 8 = 0, 5, 0, 7; launch groups [0, 32) and [32, 64)
     P[slots] = fx["P"]
     x, y, e, loss, mu, sd = _reference_share(ctx, monkeypatch, fx, P, slots)
     s, ex, lo, hi = fx["sigma_vals"], fx["expected"], fx["lo"], fx["hi"]
@@ -634,18 +668,86 @@ def _config_e_fixture():
 
 def test_configE_share_two_groups_vs_reference(ctx, monkeypatch):
     """Config E's per-GPU share (N=16384 d=4 heteroscedastic, 16 particles, 128 block columns)
-    on its default two-group schedule. The 4 particles of F9 + F9b (the reference's
-    evaluate_loss at this size, make_golden_big.py), two in each group, among 12 others: mu/sd
-    at 1e-6, objective at 1e-8 or threshold ties; deterministic; bitwise equal to the one-group
-    schedule."""
+    on its default schedule (the persistent factorisation). The 4 particles of F9 + F9b (the
+    reference's evaluate_loss at this size, make_golden_big.py) among 12 others: mu/sd at 1e-6,
+    objective at 1e-8 or threshold ties; deterministic; bitwise equal to the per-block-column
+    launches (two groups and one); and 2 of the 12 others against the oracle's identity form
+    (dpotrf + dtrtri on the host)."""
     import gpfit
-    assert gpfit.plan_check(16, 128)["groups"] == 2
+    assert gpfit.plan_check(16, 128)["persistent"] == 1
     fx = _config_e_fixture()
     rng = np.random.default_rng(1604)
     P = rng.uniform(0.05, 0.6, size=(16, 4))
     slots = [3, 6, 12, 15]
     P[slots] = fx["P"]
-    _reference_share(ctx, monkeypatch, fx, P, slots)
+    x, y, e, loss, mu, sd = _reference_share(ctx, monkeypatch, fx, P, slots)
+    s, ex, lo, hi = fx["sigma_vals"], fx["expected"], fx["lo"], fx["hi"]
+    with _blas_threads():
+        for k in (0, 9):
+            m0, s0 = ref_cpu.GP_train_identity_tri(x, y, e, P[k])
+            assert _rel(mu[k], m0) < RTOL_MU_SD and _rel(sd[k], s0) < RTOL_MU_SD, k
+            w = ref_cpu.coverage_loss(m0, s0, y, s, ex) + 0.01 * ref_cpu.proximity_penalty(P[k], lo, hi)
+            assert_loss_or_ties(loss[k], w, m0, s0, y, s, what=k)
+
+
+@pytest.mark.parametrize("N,d,P", [(1000, 3, 24), (2048, 2, 13), (1536, 4, 3), (4096, 3, 64)])
+def test_persistent_factor_bitwise(ctx, monkeypatch, N, d, P):
+    """The persistent factorisation (gpf::k_factor: one launch, items taken from per-XCD work
+    queues in dependency order, hand-offs through per-particle counters) runs the arithmetic of
+    the per-block-column launches: scores, mean and sd bitwise equal to GPF_PERSIST=0, for queue
+    counts 8 (P = 24, 64), 8 with uneven queues (P = 13) and 3 (P = 3); one particle against the
+    oracle's identity form; the host-side plan check decodes the same queues. (The launches
+    compared against are unsplit: split-K pieces would sum in another order.)"""
+    import gpfit
+    rng = np.random.default_rng(N + 31 * P + d)
+    x = rng.uniform(size=(d, N))
+    y = np.sin(3 * x[0]) + x[-1] ** 2 + 0.1 * rng.standard_normal(N)
+    e = rng.uniform(0.05, 0.2, size=N)
+    s, ex = ref_cpu.sigma_grid()
+    lo, hi = ref_cpu.search_bounds(x)
+    ctx.set_data(x, y, e)
+    ctx.set_grid(s, ex, lo, hi)
+    Q = rng.uniform(0.08, 0.5, size=(P, d))
+    monkeypatch.setenv("GPF_PERSIST", "1")
+    assert gpfit.plan_check(P, -(-N // 128))["persistent"] == 1
+    on = ctx.eval_batch(Q, want_mu_sd=True)
+    again = ctx.eval_batch(Q, want_mu_sd=True)
+    monkeypatch.setenv("GPF_PERSIST", "0")
+    monkeypatch.setenv("GPF_SPLIT_K", "1")  # (few-tile launches would otherwise sum split-K pieces: other rounding)
+    off = ctx.eval_batch(Q, want_mu_sd=True)
+    monkeypatch.delenv("GPF_PERSIST")
+    monkeypatch.delenv("GPF_SPLIT_K")
+    for a, b, c in zip(on, again, off):
+        np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(a, c)
+    if N <= 2048:
+        mo, so = ref_cpu.GP_train_identity(x, y, e, Q[-1])
+        assert _rel(on[1][-1], mo) < RTOL_MU_SD and _rel(on[2][-1], so) < RTOL_MU_SD
+
+
+def test_persistent_timeout_reported_then_correct(ctx, monkeypatch):
+    """A hand-off wait of the persistent factorisation that times out (GPF_WAIT_SPINS=0) sets the
+    abort word, every other wait gives up, the launch drains and the host reports the timeout;
+    the next batch (k_build_cov resets the counters, the queue heads and the abort word) is
+    bitwise equal to a clean run."""
+    N, d = 2048, 3
+    rng = np.random.default_rng(2718)
+    x = rng.uniform(size=(d, N))
+    y = np.cos(5 * x[1]) + 0.1 * rng.standard_normal(N)
+    e = np.full(N, 0.1)
+    s, ex = ref_cpu.sigma_grid()
+    lo, hi = ref_cpu.search_bounds(x)
+    ctx.set_data(x, y, e)
+    ctx.set_grid(s, ex, lo, hi)
+    Q = rng.uniform(0.1, 0.5, size=(48, d))
+    monkeypatch.setenv("GPF_PERSIST", "1")
+    want = ctx.eval_batch(Q)
+    monkeypatch.setenv("GPF_WAIT_SPINS", "0")
+    with pytest.raises(RuntimeError, match="timed out"):
+        ctx.eval_batch(Q)
+    monkeypatch.delenv("GPF_WAIT_SPINS")
+    np.testing.assert_array_equal(ctx.eval_batch(Q), want)
+    monkeypatch.delenv("GPF_PERSIST")
 
 
 @pytest.mark.parametrize("N,d,P", [(1024, 2, 12), (2048, 3, 32)])

@@ -18,7 +18,8 @@ import gpfit
 NT = list(range(1, 21)) + [31, 32, 33, 64, 127, 128, 129, 130]
 
 ENVS = [
-    {},                                            # the defaults
+    {},                                            # the defaults (persistent where slot-bound)
+    {"GPF_PERSIST": "1"},                          # the persistent factorisation everywhere (nt >= 3)
     {"GPF_GROUPS": "2"}, {"GPF_GROUPS": "3"}, {"GPF_GROUPS": "4"},
     {"GPF_SPLIT_K": "2"}, {"GPF_SPLIT_K": "7"}, {"GPF_SPLIT_K": "16"},
     {"GPF_SPLIT_K": "7", "GPF_GROUPS": "3"},
@@ -38,8 +39,10 @@ ENVS = [
 def env(monkeypatch):
     def apply(kv):
         for k in ("GPF_GROUPS", "GPF_SPLIT_K", "GPF_SPLIT_CRIT", "GPF_SPLIT_CRIT_MIN", "GPF_STEP_GROUP", "GPF_EARLY_DIAG",
-                  "GPF_DEFER_SYRK", "GPF_SPLIT_K_SLOTS", "GPF_SPLIT_K_MINCH"):
+                  "GPF_DEFER_SYRK", "GPF_SPLIT_K_SLOTS", "GPF_SPLIT_K_MINCH", "GPF_PERSIST"):
             monkeypatch.delenv(k, raising=False)
+        if kv and "GPF_PERSIST" not in kv:  # the launch-plan knobs: on the per-block-column launches
+            monkeypatch.setenv("GPF_PERSIST", "0")
         for k, v in kv.items():
             monkeypatch.setenv(k, v)
     return apply
@@ -48,12 +51,18 @@ def env(monkeypatch):
 @pytest.mark.parametrize("kv", ENVS, ids=lambda kv: ",".join(f"{k}={v}" for k, v in kv.items()) or "default")
 def test_every_tile_has_exactly_one_finisher(env, kv):
     env(kv)
-    seen_split = seen_groups = 0
+    seen_split = seen_groups = seen_persist = 0
     for nt in NT:
         # all chunk sizes up to 64 at small nt; a spread at large nt (the check is O(pc nt^2))
         pcs = range(1, 65) if nt <= 33 else (1, 2, 7, 8, 15, 16, 17, 31, 32, 33, 63, 64)
         for pc in pcs:
             st = gpfit.plan_check(pc, nt)
+            if st["persistent"]:  # one launch, every tile an item, one SYRK item per column 1 .. nt-2
+                assert (st["launches"], st["groups"], st["split_tiles"], st["diag_workgroups"]) == (1, 1, 0, 0)
+                assert st["whole_tiles"] == pc * (nt - 1) * nt and st["syrk_workgroups"] == pc * max(0, nt - 2)
+                assert st["workgroups"] == st["whole_tiles"] + st["syrk_workgroups"]
+                seen_persist += 1
+                continue
             assert st["launches"] == (nt * st["groups"] if nt > 1 else 0)
             assert st["whole_tiles"] + st["split_tiles"] == pc * (nt - 1) * nt  # every (J, p, w)
             # early diagonal factor: one diagonal workgroup per particle in every launch
@@ -66,19 +75,29 @@ def test_every_tile_has_exactly_one_finisher(env, kv):
             seen_groups += st["groups"] > 1
     if kv.get("GPF_SPLIT_K") or kv.get("GPF_SPLIT_CRIT") or not kv:
         assert seen_split, "the sweep never reached a split launch"
-    if "GPF_GROUPS" in kv or not kv:
+    if "GPF_GROUPS" in kv:
         assert seen_groups, "the sweep never reached a multi-group plan"
+    if not kv or kv.get("GPF_PERSIST") == "1":
+        assert seen_persist, "the sweep never reached the persistent factorisation"
 
 
 def test_default_plans_of_the_baseline_configs(env):
     """The schedules the bench and the GPU tests rely on."""
     env({})
-    c = gpfit.plan_check(64, 32)            # config C: two concurrent groups, no split
-    assert (c["groups"], c["Smax"]) == (2, 1)
-    d = gpfit.plan_check(32, 32)            # config D's per-GPU share: two concurrent groups
-    assert d["groups"] == 2
+    # the slot-bound configs run the persistent factorisation: one launch, 32 x 31 tiles + 30 SYRK
+    # items per particle at N=4096
+    c = gpfit.plan_check(64, 32)            # config C
+    assert (c["persistent"], c["launches"], c["groups"], c["Smax"]) == (1, 1, 1, 1)
+    assert c["workgroups"] == 64 * (32 * 31 + 30)
+    d = gpfit.plan_check(32, 32)            # config D's per-GPU share
     e = gpfit.plan_check(16, 128)           # config E's per-GPU share at N=16384
-    assert e["groups"] == 2
+    assert d["persistent"] == e["persistent"] == 1
+    env({"GPF_PERSIST": "0"})               # ... the per-block-column launches: two concurrent groups
+    c0, d0, e0 = gpfit.plan_check(64, 32), gpfit.plan_check(32, 32), gpfit.plan_check(16, 128)
+    assert (c0["groups"], c0["Smax"], d0["groups"], e0["groups"]) == (2, 1, 2, 2)
+    assert (c0["diag_workgroups"], d0["diag_workgroups"], e0["diag_workgroups"]) == (0, 0, 0)
+    assert (c0["syrk_workgroups"], d0["syrk_workgroups"], e0["syrk_workgroups"]) == (64 * 30, 32 * 30, 16 * 126)
+    env({})
     b = gpfit.plan_check(32, 8)             # config B: one group, no split (critical split off by default)
     assert b["groups"] == 1 and b["S"] == 1 and b["Smax"] == 1 and b["split_tiles"] == 0
     env({"GPF_SPLIT_CRIT": "4"})            # ... and with the critical-tile split asked for
@@ -91,29 +110,35 @@ def test_default_plans_of_the_baseline_configs(env):
     # and the critical tile of the deep launches gets the most pieces
     assert one["workgroups"] <= 32 * 256 and one["Smax"] > 8
     # early diagonal factor where launches leave slots idle (B, the prediction), the fused factor
-    # where they are slot-bound (C, D's and E's shares)
-    assert e["diag_workgroups"] == 0
-    assert (c["diag_workgroups"], d["diag_workgroups"]) == (0, 0)
+    # in the persistent factorisation (C, D's and E's shares)
+    assert (c["diag_workgroups"], d["diag_workgroups"], e["diag_workgroups"]) == (0, 0, 0)
     assert b["diag_workgroups"] == 32 * 8 and one["diag_workgroups"] == 32
-    # deferred diagonal update (one SYRK workgroup per particle and launch 1 .. nt-2) everywhere
-    # but the all-tile split of the prediction
+    # deferred diagonal update (one SYRK workgroup / item per particle and column 1 .. nt-2)
+    # everywhere but the all-tile split of the prediction
     assert (b["syrk_workgroups"], c["syrk_workgroups"]) == (32 * 6, 64 * 30)
     assert (d["syrk_workgroups"], e["syrk_workgroups"], one["syrk_workgroups"]) == (32 * 30, 16 * 126, 0)
 
 
 def test_early_diag_override(env):
-    env({"GPF_EARLY_DIAG": "1"})
+    env({"GPF_EARLY_DIAG": "1", "GPF_PERSIST": "0"})
     assert gpfit.plan_check(64, 32)["diag_workgroups"] == 64 * 32
     env({"GPF_EARLY_DIAG": "0"})
     assert gpfit.plan_check(32, 8)["diag_workgroups"] == 0
 
 
 def test_defer_syrk_override(env):
-    env({"GPF_DEFER_SYRK": "0"})
+    env({"GPF_DEFER_SYRK": "0", "GPF_PERSIST": "0"})
     assert gpfit.plan_check(32, 8)["syrk_workgroups"] == 0
     assert gpfit.plan_check(64, 32)["syrk_workgroups"] == 0
     env({"GPF_DEFER_SYRK": "1", "GPF_SPLIT_K": "4"})  # the all-tile split never defers
     assert gpfit.plan_check(8, 16)["syrk_workgroups"] == 0
+
+
+def test_persistent_override(env):
+    env({"GPF_PERSIST": "0"})
+    assert gpfit.plan_check(64, 32)["persistent"] == 0
+    env({"GPF_PERSIST": "1"})
+    assert gpfit.plan_check(4, 8)["persistent"] == 1 and gpfit.plan_check(4, 2)["persistent"] == 0  # (nt >= 3)
 
 
 def test_env_is_read_per_call(env):
