@@ -676,12 +676,16 @@ __device__ __forceinline__ void zero_tile64(double* __restrict__ g, size_t gld) 
 // the 100 MHz reference clock (s_memrealtime) to clk[0] / clk[1], so the host gets the clock the
 // chip actually held while the kernel ran: clk[0] / clk[1] x 100 MHz. Times the FP64 MFMA rate
 // per clock (128 flop per CU) it is the box's FP64 matrix ceiling during that kernel.
-struct ClockSpan {
-  unsigned long long t0 = 0, r0 = 0;
-  __device__ __forceinline__ void start(const unsigned long long* clk) {
+struct ClockSpan {  // the two start stamps wait in LDS (kept in registers they spilled in k_step)
+  unsigned long long* s;
+  __device__ __forceinline__ explicit ClockSpan(unsigned long long* lds2) : s(lds2) {}
+  __device__ __forceinline__ void start(const unsigned long long* clk) const {
     if (clk && threadIdx.x == 0) {
+      unsigned long long t0, r0;
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
       asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r0)::"memory");
+      s[0] = t0;
+      s[1] = r0;
     }
   }
   __device__ __forceinline__ void stop(unsigned long long* clk) const {
@@ -689,8 +693,8 @@ struct ClockSpan {
       unsigned long long t1, r1;
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
       asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r1)::"memory");
-      __hip_atomic_fetch_add(clk, t1 - t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(clk + 1, r1 - r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(clk, t1 - s[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(clk + 1, r1 - s[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 };

@@ -1396,7 +1396,8 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
                                                   int* __restrict__ yflag, int defer, int sy, int spins, int la,
                                                   double* __restrict__ lab, unsigned long long* __restrict__ clk) {
   const int tid = threadIdx.x;
-  ClockSpan span;
+  __shared__ unsigned long long sclk[2];
+  const ClockSpan span(sclk);
   span.start(clk);
 #ifdef GPF_WG_TRACE
   if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) {
@@ -1414,6 +1415,9 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
   // 0-3 and lose every arbitration by age otherwise; MI355X_MICROARCH "Two waves per SIMD" item 4)
   if (__builtin_amdgcn_readfirstlane(tid >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
+  // la bit 8: foreground (gpf_predict's pipelined V runs beside this factorisation on the same
+  // CUs): this launch's waves win issue arbitration against it
+  if (la & 8) __builtin_amdgcn_s_setprio(2);
   int p, w, sidx;
   const int role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, SPLIT != SPLIT_ALL && sy,
                                       SPLIT == SPLIT_NONE && ED && (la & 1) && !sy, p, w, sidx);

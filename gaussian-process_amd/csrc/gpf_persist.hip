@@ -51,6 +51,10 @@
 
 namespace gpf {
 
+#ifndef GPF_PERSIST_WT
+#define GPF_PERSIST_WT 1  // (0: plain tile stores — a timing probe only, NOT coherent across XCDs)
+#endif
+
 struct PState {
   int* lcol;       // [P][nt]
   int* ucol;       // [P][nt]
@@ -213,7 +217,7 @@ __device__ __forceinline__ void p_ltile(const PItem& a, const PState& st, int J,
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        gst<true>(&lrow[16 * (2 * P + j) + 4 * e], o[j][e]);
+        gst<GPF_PERSIST_WT>(&lrow[16 * (2 * P + j) + 4 * e], o[j][e]);
         yr = fma(o[j][e], zj[16 * (2 * P + j) + 4 * e + g], yr);
       }
   }
@@ -279,7 +283,7 @@ __device__ __forceinline__ void p_utile(const PItem& a, const PState& st, int J,
       for (int e = 0; e < 4; ++e) {
         const int row = 16 * (2 * P + j) + 4 * e;  // + g
         const double v = o[j][e];
-        gst<true>(&ucol[(size_t)row * ld], v);
+        gst<GPF_PERSIST_WT>(&ucol[(size_t)row * ld], v);
         a2[h] = fma(v, v, a2[h]);
         az[h] = fma(v, zj[row + g], az[h]);
       }
@@ -306,7 +310,8 @@ __device__ __forceinline__ void p_utile(const PItem& a, const PState& st, int J,
 // and spilled). The grid equals the number of items, so every workgroup finds a ticket.
 __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_factor(PItem a, PState st, int P,
                                                                                 unsigned long long* __restrict__ clk) {
-  ClockSpan span;
+  __shared__ unsigned long long sclk[2];
+  const ClockSpan span(sclk);
   span.start(clk);
   __shared__ __attribute__((aligned(16))) double lds[STEP_LDS];
   __shared__ int sflag;

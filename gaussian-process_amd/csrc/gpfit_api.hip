@@ -53,6 +53,7 @@ struct gpf_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t sub[MAX_GROUPS] = {};  // one stream per particle group (run_factor)
+  hipStream_t pside = nullptr;       // gpf_predict's side stream (lowest priority: V beside the factor)
   hipEvent_t fork = nullptr, join[MAX_GROUPS] = {};
   std::string err;
 
@@ -312,7 +313,7 @@ static int ensure_work(gpf_ctx* c, int want) {
 static bool persist_on(int pc, int nt) {
   bool on = (long long)pc * (nt - 1) > 512;
   if (const char* s = getenv("GPF_PERSIST")) on = atoi(s) != 0;
-  return on && nt >= 3;
+  return on && nt >= 3 && pc >= 2;  // (a single particle — the prediction — keeps its split launches)
 }
 
 static int num_groups(int pc, int nt) {
@@ -686,7 +687,7 @@ static int run_factor(gpf_ctx* c, int pc, hipEvent_t* after = nullptr) {
                          c->d_U + (size_t)p0 * ld * ld, c->d_yb + (size_t)p0 * ld, c->d_s2p + (size_t)p0 * nt * ld,
                          c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc, l.grp, N, c->d_x,
                          c->d_ls + (size_t)p0 * c->d, c->d, l.S, l.S2, partg, cntg, c->d_flag + p0, l.ed,
-                         c->d_cflag + p0, l.defer, l.sy, spins, l.la | ((l.la & 2) ? la_delay : 0),
+                         c->d_cflag + p0, l.defer, l.sy, spins, l.la | ((l.la & 2) ? la_delay : 0) | (after ? 8 : 0),
                          l.la ? c->d_la + 2 * (size_t)p0 * T * T : nullptr, c->prof ? c->d_clk : nullptr);
     });
     if (rc) return rc;
@@ -788,6 +789,9 @@ int gpf_open(int device, gpf_ctx** out) {
   for (int g = 0; ok && g < MAX_GROUPS; ++g)
     ok = hipStreamCreateWithFlags(&c->sub[g], hipStreamNonBlocking) == hipSuccess &&
          hipEventCreateWithFlags(&c->join[g], hipEventDisableTiming) == hipSuccess;
+  int prio_least = 0, prio_greatest = 0;
+  ok = ok && hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) == hipSuccess &&
+       hipStreamCreateWithPriority(&c->pside, hipStreamNonBlocking, prio_least) == hipSuccess;
   if (!ok) {
     gpf_close(c);
     return GPF_HIP_ERROR;
@@ -809,6 +813,7 @@ void gpf_close(gpf_ctx* c) {
   for (auto e : c->pev) hipEventDestroy(e);
   if (c->pev_x) hipEventDestroy(c->pev_x);
   if (c->pev_side) hipEventDestroy(c->pev_side);
+  if (c->pside) hipStreamDestroy(c->pside);
   for (int g = 0; g < MAX_GROUPS; ++g) {
     if (c->sub[g]) hipStreamDestroy(c->sub[g]);
     if (c->join[g]) hipEventDestroy(c->join[g]);
@@ -1108,7 +1113,7 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
   // fill it (GP_fit.py:32 -> GP_func.py:22-40). Later chunks follow on the main stream.
   bool pipe = c->nt >= 2;
   if (const char* e = getenv("GPF_PREDICT_PIPE")) pipe = pipe && atoi(e) != 0;
-  hipStream_t side = c->sub[MAX_GROUPS - 1];  // (the group streams: the single-particle factor uses one)
+  hipStream_t side = c->pside;
   if (pipe) {
     if (!c->pev_x) GPF_HIP(c, hipEventCreateWithFlags(&c->pev_x, hipEventDisableTiming));
     if (!c->pev_side) GPF_HIP(c, hipEventCreateWithFlags(&c->pev_side, hipEventDisableTiming));
@@ -1133,12 +1138,16 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
     });
   };
   // V = U K_s for row tiles [t0, t0 + rows): row tile t of U has (t+1) column tiles, the last triangular
+  // beside the factor, V's workgroups are held to one per CU (dynamic LDS: 64 + 17 KiB > half a
+  // CU's 160 KiB), so every CU keeps a slot for the factor's workgroups (one per CU under the
+  // balanced split), and the factor's waves run at a higher issue priority (k_step, la bit 8)
   auto vsq = [&](hipStream_t st, int nqt, int t0, int rows) {
+    const size_t pad = st == side ? 17 * 1024 : 0;
     const double Cm = (double)nqt * T;
     const double vflops = 2.0 * T * T * Cm * ((double)(t0 + rows) * (t0 + rows + 1) / 2 - (double)t0 * (t0 + 1) / 2) -
                           (double)T * T * Cm * rows;
     return launch_on(c, st, PC_PRED, vflops, [&] {
-      hipLaunchKernelGGL(gpf::k_predict_vsq, dim3(nqt, rows), dim3(gpf::Geo<T>::NTH), 0, st, (int)Np, c->d_U, d_ks,
+      hipLaunchKernelGGL(gpf::k_predict_vsq, dim3(nqt, rows), dim3(gpf::Geo<T>::NTH), pad, st, (int)Np, c->d_U, d_ks,
                          (int)Cp, d_vsq, d_z, d_vz, t0);
     });
   };
@@ -1156,9 +1165,13 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
     const int nqt = (int)((m + T - 1) / T);
     GPF_HIP(c, hipStreamWaitEvent(side, c->pev_x, 0));
     rc = cross_cov(side, m, nqt * T);
-    for (int t = 0; rc == GPF_OK && t < c->nt; ++t) {
-      GPF_HIP(c, hipStreamWaitEvent(side, c->pev[t], 0));
-      rc = vsq(side, nqt, t, 1);
+    // row tiles in batches of >= 512 workgroups (a batch of nqt workgroups per row tile alone
+    // would leave most slots idle and serialise the side stream behind the factor)
+    const int rows = std::max(1, std::min(c->nt, (512 + nqt - 1) / nqt));
+    for (int t = 0; rc == GPF_OK && t < c->nt; t += rows) {
+      const int r = std::min(rows, c->nt - t);
+      GPF_HIP(c, hipStreamWaitEvent(side, c->pev[t + r - 1], 0));
+      rc = vsq(side, nqt, t, r);
     }
     if (rc) return rc;
     GPF_HIP(c, hipEventRecord(c->pev_side, side));

@@ -139,6 +139,7 @@ def test_persistent_override(env):
     assert gpfit.plan_check(64, 32)["persistent"] == 0
     env({"GPF_PERSIST": "1"})
     assert gpfit.plan_check(4, 8)["persistent"] == 1 and gpfit.plan_check(4, 2)["persistent"] == 0  # (nt >= 3)
+    assert gpfit.plan_check(1, 32)["persistent"] == 0  # the prediction's single particle keeps its split launches
 
 
 def test_env_is_read_per_call(env):
