@@ -71,11 +71,18 @@ __device__ double pairwise_leaf(const double* a, int len) {
 
 // numpy's recursion: n <= 128 is a leaf, else split at (n/2) rounded down to a multiple
 // of 8 and return left + right. Explicit stack, same order; `leaf(off, len)` supplies
-// the value of each leaf, visited left to right.
-template <typename Leaf>
-__device__ double pairwise_tree(int n, Leaf leaf) {
+// the value of each leaf, visited left to right. The stack (run by one thread) lives in LDS:
+// as a dynamically indexed private array it went to scratch.
+struct PwStack {
   int off[32], len[32], stage[32];
   double left[32];
+};
+template <typename Leaf>
+__device__ double pairwise_tree(int n, Leaf leaf, PwStack& st) {
+  int* off = st.off;
+  int* len = st.len;
+  int* stage = st.stage;
+  double* left = st.left;
   int sp = 0;
   off[0] = 0; len[0] = n; stage[0] = 0;
   for (;;) {
@@ -104,16 +111,13 @@ __device__ double pairwise_tree(int n, Leaf leaf) {
   }
 }
 
-__device__ double pairwise_sum_seq(const double* a, int n) {
-  return pairwise_tree(n, [&](int off, int len) { return pairwise_leaf(a + off, len); });
-}
-
 // Same sum, leaves in parallel: thread 0 lists the leaves, one thread per leaf sums it,
 // thread 0 combines them in the tree's order. Block-wide (all threads call); the result
 // is returned in thread 0. Scratch: leaf tables of PW_LEAVES entries.
 constexpr int PW_LEAVES = 64;  // K <= KGRID_MAX = 4096 -> at most 64 leaves of >= 64
 __device__ double pairwise_sum_block(const double* a, int n, int* loff, int* llen, double* lsum, int* nleaf) {
   const int tid = threadIdx.x;
+  __shared__ PwStack st;
   if (tid == 0) {
     int cnt = 0;
     pairwise_tree(n, [&](int off, int len) {
@@ -121,7 +125,7 @@ __device__ double pairwise_sum_block(const double* a, int n, int* loff, int* lle
       llen[cnt] = len;
       ++cnt;
       return 0.0;
-    });
+    }, st);
     *nleaf = cnt;
   }
   __syncthreads();
@@ -130,7 +134,7 @@ __device__ double pairwise_sum_block(const double* a, int n, int* loff, int* lle
   double r = 0.0;
   if (tid == 0) {
     int idx = 0;
-    r = pairwise_tree(n, [&](int, int) { return lsum[idx++]; });
+    r = pairwise_tree(n, [&](int, int) { return lsum[idx++]; }, st);
   }
   return r;
 }

@@ -307,11 +307,16 @@ static int ensure_work(gpf_ctx* c, int want) {
 // evals/s, same box), -19% at N=1024 P=32, 4 groups worse everywhere. Default: 2 groups for
 // chunks with at least 16 block columns, else 1. (With concurrent groups the per-launch times
 // overlap, so bench.py rates the whole factorisation phase instead: no gaps or overlap counted.)
-// Persistent factorisation (gpf::k_factor, gpf_persist.hip) for the slot-bound schedules: more
-// tiles per block column than the 512 workgroup slots (config C, D's and E's per-GPU shares),
-// where the per-block-column launches drain between columns. GPF_PERSIST = 0/1 overrides.
+// Persistent factorisation (gpf::k_factor, gpf_persist.hip) for slot-bound schedules with many
+// block columns: more tiles per block column than the 512 workgroup slots and nt >= 64 (config
+// E's per-GPU share: 22.2-22.3 vs 22.0 evals/s, 0.945 vs 0.937 of the FP64 ceiling at the clock
+// the chip held). At nt = 32 (configs C, D) the per-block-column launches on two group streams
+// stay faster: 1344-1368 vs 1310-1331 evals/s — per clock the two are within 0.5%, but the chip
+// holds ~40 MHz less under the persistent launch (profiles/r4/ab_persist_clock.txt,
+// ab_r4g_summary.txt). B-like launches (fewer tiles than slots) lose 24% (no early diagonal
+// factor in it). GPF_PERSIST = 0/1 overrides.
 static bool persist_on(int pc, int nt) {
-  bool on = (long long)pc * (nt - 1) > 512;
+  bool on = (long long)pc * (nt - 1) > 512 && nt >= 64;
   if (const char* s = getenv("GPF_PERSIST")) on = atoi(s) != 0;
   return on && nt >= 3 && pc >= 2;  // (a single particle — the prediction — keeps its split launches)
 }
@@ -1111,8 +1116,12 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
   // factor's launch t has finished row tile t of U (and z_t): the single-particle factorisation
   // is a chain of nt latency-bound launches that leave most of the chip idle, and V's row tiles
   // fill it (GP_fit.py:32 -> GP_func.py:22-40). Later chunks follow on the main stream.
-  bool pipe = c->nt >= 2;
-  if (const char* e = getenv("GPF_PREDICT_PIPE")) pipe = pipe && atoi(e) != 0;
+  // Off by default: beside V's row tiles the factorisation's latency-bound chain slowed from
+  // 2.99 to 7.7 ms at N=4096 (M=10,000: 7.41-7.45 ms vs 5.52 ms serial, one box,
+  // profiles/r4/ab_r4g_summary.txt), despite V's lowest-priority stream, one V workgroup per CU
+  // and the factor's raised wave priority. GPF_PREDICT_PIPE=1 enables it.
+  bool pipe = false;
+  if (const char* e = getenv("GPF_PREDICT_PIPE")) pipe = atoi(e) != 0 && c->nt >= 2;
   hipStream_t side = c->pside;
   if (pipe) {
     if (!c->pev_x) GPF_HIP(c, hipEventCreateWithFlags(&c->pev_x, hipEventDisableTiming));

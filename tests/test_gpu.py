@@ -276,9 +276,9 @@ def test_chunked_batches_equal_single_batch(f3, monkeypatch):
 
 @pytest.mark.parametrize("N,d,M", [(1500, 2, 20000), (4096, 3, 3000)])
 def test_predict_pipeline_bitwise(ctx, monkeypatch, N, d, M):
-    """gpf_predict's pipelined schedule (the first query chunk's K_s and V = U K_s on a side
-    stream, row tile t of V behind the factor's launch t) against the serial one
-    (GPF_PREDICT_PIPE=0): the same kernels on the same data, so mu and sd bitwise equal; with two
+    """gpf_predict's pipelined schedule (GPF_PREDICT_PIPE=1, opt-in: the first query chunk's K_s
+    and V = U K_s on a side stream, row tiles of V behind the factor's launches) against the
+    serial default: the same kernels on the same data, so mu and sd bitwise equal; with two
     query chunks (M > 16384: the second chunk runs on the main stream after the first) and with
     one; mu = sum_t V_t^T z_t (no alpha) against the oracle's GP() on a sample of the queries."""
     rng = np.random.default_rng(N + M)
@@ -288,11 +288,10 @@ def test_predict_pipeline_bitwise(ctx, monkeypatch, N, d, M):
     xf = rng.uniform(-0.1, 1.1, size=(d, M))
     ls = rng.uniform(0.1, 0.4, size=d)
     ctx.set_data(x, y, e)
-    monkeypatch.delenv("GPF_PREDICT_PIPE", raising=False)
+    monkeypatch.setenv("GPF_PREDICT_PIPE", "1")  # (opt-in)
     a = ctx.predict(ls, xf)
-    monkeypatch.setenv("GPF_PREDICT_PIPE", "0")
-    b = ctx.predict(ls, xf)
     monkeypatch.delenv("GPF_PREDICT_PIPE")
+    b = ctx.predict(ls, xf)
     np.testing.assert_array_equal(a[0], b[0])
     np.testing.assert_array_equal(a[1], b[1])
     k = np.linspace(0, M - 1, 64).astype(int)
@@ -550,8 +549,9 @@ def test_random_configs_vs_oracle(ctx, N, d, hetero, seed):
 
 def _reference_share(ctx, monkeypatch, fx, P, slots, rounds=2):
     """Score P (with the fixture's particles at `slots`) on the default schedule, twice; then on
-    the per-block-column launches (GPF_PERSIST=0: two concurrent particle groups where the
-    default plan has them, and one group); returns (loss, mu, sd) of the default run."""
+    the persistent factorisation (GPF_PERSIST=1) and on the per-block-column launches with one
+    particle group (GPF_PERSIST=0, GPF_GROUPS=1): all bitwise equal; returns (loss, mu, sd) of
+    the default run."""
     from conftest import fixture_data
     x, y, e = fixture_data(fx["meta"], fx["data_sha256"])
     ctx.set_data(x, y, e)
@@ -561,8 +561,8 @@ def _reference_share(ctx, monkeypatch, fx, P, slots, rounds=2):
     runs = [ctx.eval_batch(P, want_mu_sd=True) for _ in range(rounds)]
     for a, b in zip(runs[0], runs[1]):
         np.testing.assert_array_equal(a, b)  # deterministic
-    monkeypatch.setenv("GPF_PERSIST", "0")
-    for groups in (None, "1"):
+    for persist, groups in (("1", None), ("0", "1")):
+        monkeypatch.setenv("GPF_PERSIST", persist)
         if groups:
             monkeypatch.setenv("GPF_GROUPS", groups)
         other = ctx.eval_batch(P, want_mu_sd=True)
@@ -579,15 +579,14 @@ def _reference_share(ctx, monkeypatch, fx, P, slots, rounds=2):
 
 
 def test_configD_share_two_groups_vs_reference(ctx, monkeypatch):
-    """Config D's per-GPU share (N=4096 d=3, 32 particles) on its default schedule: the
-    persistent factorisation (gpfit.plan_check). The 4 particles of F8 (the reference's own
+    """Config D's per-GPU share (N=4096 d=3, 32 particles) on its default schedule: two particle
+    groups on concurrent streams (gpfit.plan_check). The 4 particles of F8 (the reference's own
     evaluate_loss and the GP() mu/sd inside it, make_golden_big.py) sit among 28 others: mu/sd
-    at 1e-6, objective at 1e-8 or threshold ties; deterministic; bitwise equal to the
-    per-block-column launches (two groups and one); 4 of the others against the oracle's
-    identity form."""
+    at 1e-6, objective at 1e-8 or threshold ties; deterministic; bitwise equal to the persistent
+    factorisation and to one group; 4 of the others against the oracle's identity form."""
     import gpfit
     from conftest import load_golden
-    assert gpfit.plan_check(32, 32)["persistent"] == 1
+    assert gpfit.plan_check(32, 32)["groups"] == 2
     fx = load_golden("f8_configC.npz")
     rng = np.random.default_rng(404)
     P = rng.uniform(0.05, 0.6, size=(32, 3))
@@ -605,19 +604,20 @@ def test_configD_share_two_groups_vs_reference(ctx, monkeypatch):
 
 def test_configC_full_swarm_vs_reference(ctx, monkeypatch):
     """BASELINE config C exactly as bench.py times it: N=4096 d=3, one 64-particle batch on the
-    default schedule (the persistent factorisation: one launch of 64 x 1022 items from 8 work
-    queues). The 4 particles of F8 (the reference's evaluate_loss and the GP() mu/sd inside it,
-    make_golden_big.py) sit among 60 others, in 4 different queues: mu/sd at 1e-6, objective at
-    1e-8 or threshold ties; deterministic; bitwise equal to the per-block-column launches (two
-    concurrent groups, and one); 4 further particles against the oracle's identity form."""
+    default schedule (two particle groups of 32 on concurrent streams, 992 workgroups per
+    launch, two slot rounds). The 4 particles of F8 (the reference's evaluate_loss and the GP()
+    mu/sd inside it, make_golden_big.py) sit among 60 others, two in each group: mu/sd at 1e-6,
+    objective at 1e-8 or threshold ties; deterministic; bitwise equal to the persistent
+    factorisation (4 different work queues) and to one group; 4 further particles against the
+    oracle's identity form."""
     import gpfit
     from conftest import load_golden
     plan = gpfit.plan_check(64, 32)
-    assert plan["persistent"] == 1 and plan["diag_workgroups"] == 0  # the slot-bound fused schedule
+    assert plan["groups"] == 2 and plan["diag_workgroups"] == 0  # the slot-bound fused schedule
     fx = load_golden("f8_configC.npz")
     rng = np.random.default_rng(6464)
     P = rng.uniform(0.05, 0.6, size=(64, 3))
-    slots = [0, 21, 40, 63]  # queues p mod 8 = 0, 5, 0, 7; launch groups [0, 32) and [32, 64)
+    slots = [0, 21, 40, 63]  # launch groups [0, 32) and [32, 64); persistent queues p mod 8 = 0, 5, 0, 7
     P[slots] = fx["P"]
     x, y, e, loss, mu, sd = _reference_share(ctx, monkeypatch, fx, P, slots)
     s, ex, lo, hi = fx["sigma_vals"], fx["expected"], fx["lo"], fx["hi"]

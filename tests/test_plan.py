@@ -84,19 +84,21 @@ def test_every_tile_has_exactly_one_finisher(env, kv):
 def test_default_plans_of_the_baseline_configs(env):
     """The schedules the bench and the GPU tests rely on."""
     env({})
-    # the slot-bound configs run the persistent factorisation: one launch, 32 x 31 tiles + 30 SYRK
-    # items per particle at N=4096
+    # configs C and D: per-block-column launches on two concurrent group streams; config E's
+    # share (128 block columns): the persistent factorisation, one launch of 128 x 127 tiles + 126
+    # SYRK items per particle
     c = gpfit.plan_check(64, 32)            # config C
-    assert (c["persistent"], c["launches"], c["groups"], c["Smax"]) == (1, 1, 1, 1)
-    assert c["workgroups"] == 64 * (32 * 31 + 30)
+    assert (c["persistent"], c["groups"], c["Smax"]) == (0, 2, 1)
     d = gpfit.plan_check(32, 32)            # config D's per-GPU share
+    assert (d["persistent"], d["groups"]) == (0, 2)
     e = gpfit.plan_check(16, 128)           # config E's per-GPU share at N=16384
-    assert d["persistent"] == e["persistent"] == 1
-    env({"GPF_PERSIST": "0"})               # ... the per-block-column launches: two concurrent groups
-    c0, d0, e0 = gpfit.plan_check(64, 32), gpfit.plan_check(32, 32), gpfit.plan_check(16, 128)
-    assert (c0["groups"], c0["Smax"], d0["groups"], e0["groups"]) == (2, 1, 2, 2)
-    assert (c0["diag_workgroups"], d0["diag_workgroups"], e0["diag_workgroups"]) == (0, 0, 0)
-    assert (c0["syrk_workgroups"], d0["syrk_workgroups"], e0["syrk_workgroups"]) == (64 * 30, 32 * 30, 16 * 126)
+    assert (e["persistent"], e["launches"], e["groups"]) == (1, 1, 1)
+    assert e["workgroups"] == 16 * (128 * 127 + 126)
+    env({"GPF_PERSIST": "1"})               # ... C persistent on request: 64 x (32 x 31 + 30) items
+    assert gpfit.plan_check(64, 32)["workgroups"] == 64 * (32 * 31 + 30)
+    env({"GPF_PERSIST": "0"})               # ... E on the launches: two concurrent groups
+    e0 = gpfit.plan_check(16, 128)
+    assert (e0["groups"], e0["diag_workgroups"], e0["syrk_workgroups"]) == (2, 0, 16 * 126)
     env({})
     b = gpfit.plan_check(32, 8)             # config B: one group, no split (critical split off by default)
     assert b["groups"] == 1 and b["S"] == 1 and b["Smax"] == 1 and b["split_tiles"] == 0
