@@ -577,13 +577,18 @@ def main():
         achieved = fl / (prof["factor_wall_ms"] * 1e-3) / 1e12 if prof["factor_wall_ms"] > 0 else None
         timing = f"factorisation-phase wall over {groups} concurrent group streams (non-overlapping)"
     # practical ceiling: the same GEMM core alone on L-tile-shaped operands (gpf_gemm_bench,
-    # direct-to-LDS, N=4096-sized panels, depth 2048, 960 workgroups)
-    core = ctx.gemm_bench(mode=2, npad=4096, particles=64, tiles=15, depth=2048, iters=3) \
+    # direct-to-LDS, N=4096-sized panels, depth 2048, 960 workgroups), on non-zero operand data
+    # (r4: the MFMA's power depends on its operand bits — on zero operands the chip held ~2.39 GHz,
+    # on real data ~2.09 GHz, profiles/r4/clock_probe_*.json), sustained for ~0.3 s so the clock
+    # has settled (a 3-launch run starts below it)
+    core = ctx.gemm_bench(mode=2, npad=4096, particles=64, tiles=15, depth=2048, iters=300) \
         if (rank == 0 and N >= 2048) else None
+    core_sclk = ctx.bench_clock() if core else None
     # this box's FP64 matrix ceiling: back-to-back independent v_mfma_f64_16x16x4 chains on every
     # SIMD (gpf_mfma_peak), at whatever clock the chip holds under that load; boxes of the pool
     # differ, so fractions against it are checkable per box
     box_peak = ctx.mfma_peak(blocks=1024, iters=8192) if rank == 0 else None
+    peak_sclk = ctx.bench_clock() if box_peak else None
     traffic = pmc_traffic(N, d, spg, "k_factor" if persistent else "k_step")
     roof = {"kernel": "k_factor" if persistent else "k_step", "bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
@@ -608,8 +613,15 @@ def main():
             "frac_of_box_ceiling": (achieved / prof["fp64_ceiling_at_sclk_tflops"])
             if (achieved and prof["fp64_ceiling_at_sclk_tflops"]) else None,
             "box_dense_mfma_loop_tflops": box_peak,
+            "box_dense_mfma_loop_sclk_mhz": peak_sclk or None,
             "gemm_core_tflops": core,
+            "gemm_core_sclk_mhz": core_sclk or None,
             "frac_of_gemm_core": (achieved / core) if (achieved and core) else None,
+            # per clock: achieved / (128 flop/CU/clock x CUs x the clock each one held)
+            "gemm_core_frac_of_its_clock_ceiling": (core / (FP64_MFMA_PEAK_TFLOPS * core_sclk / 2400.0))
+            if (core and core_sclk) else None,
+            "dense_mfma_loop_frac_of_its_clock_ceiling": (box_peak / (FP64_MFMA_PEAK_TFLOPS * peak_sclk / 2400.0))
+            if (box_peak and peak_sclk) else None,
             "launches": prof["panel_launches"], "avg_launch_ms": prof["panel_ms"] / max(prof["panel_launches"], 1),
             "flops_per_launch": prof["panel_flops"] / max(prof["panel_launches"], 1),
             "formulation": "potrf+trtri (2/3 N^3 per eval)",

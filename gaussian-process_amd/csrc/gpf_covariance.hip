@@ -188,7 +188,12 @@ __global__ __launch_bounds__(NTHR) void k_cross_cov(int N1, int N2, int R, int C
   }
 }
 
-// k_cross_cov for dimension d on `stream` (grid and LDS as above)
+// k_cross_cov for dimension d on `stream` (grid and LDS as above). (r4: a form with two columns per
+// lane, 16-B non-temporal stores and row blocks strided over a resident grid was bitwise equal and
+// 3-5% slower on the prediction's 331 MB K_s — the kernel is bound by its exp() issue, not by the
+// store path; and an exp with the libm's algorithm and constants but one v_fma_f64 per Horner step
+// (28 instead of ~45 VALU instructions per output, bitwise the libm's) was 10-20% slower, its loop
+// no longer unrolled; profiles/r4/ab_cross_cov_pair.txt.)
 inline void launch_cross_cov(hipStream_t stream, int N1, int N2, int R, int C, int d, const double* x1, int ld1,
                              const double* x2, int ld2, const double* l, double* out, int64_t ldo) {
   const dim3 grid((unsigned)((C + CC_C - 1) / CC_C), (unsigned)((R + CC_R - 1) / CC_R));

@@ -1506,10 +1506,27 @@ __global__ __launch_bounds__(DNTH) void k_debug_factor64(const double* __restric
 // L2-resident, isolates the core from HBM); +4: the U-tile shape (B given as a [k][c] row panel).
 // The tile goes to C + b*T*T.
 // ----------------------------------------------------------------------------
+// Operand fill of the GEMM-core measurement: values in [-1, 1) from a hash of the index (the MFMA's
+// power, and so the clock the chip holds, depends on its operand bits: zero operands ran the core at
+// ~2.39 GHz where k_step's real data holds ~2.18 GHz).
+__global__ __launch_bounds__(NTHR) void k_fill_hash(double* __restrict__ p, long long n) {
+  for (long long i = blockIdx.x * (long long)NTHR + threadIdx.x; i < n; i += (long long)gridDim.x * NTHR) {
+    unsigned long long h = (unsigned long long)i * 0x9e3779b97f4a7c15ull;
+    h ^= h >> 31;
+    h *= 0xbf58476d1ce4e5b9ull;
+    h ^= h >> 29;
+    p[i] = (double)(h >> 11) * 0x1.0p-52 - 1.0;
+  }
+}
+
 __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_gemm_bench(int mode, int D, int Npad, int P,
                                                                                    const double* __restrict__ Lb,
-                                                                                   double* __restrict__ C) {
+                                                                                   double* __restrict__ C,
+                                                                                   unsigned long long* clk) {
   __shared__ __attribute__((aligned(16))) double smem[DL_STAGE];
+  __shared__ unsigned long long cs[2];
+  const ClockSpan span(cs);
+  span.start(clk);
   const int b = blockIdx.x;
   const bool shared = (mode & 1) != 0;
   const int p = shared ? 0 : b % P, w = shared ? 0 : b / P;
@@ -1524,6 +1541,7 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_gemm_benc
   else
     gemm_stream_dl<false, true>(acc, Lp + (size_t)J * T * ld, Npad, Lp + (size_t)I * T * ld, Npad, D, smem, qd);
   acc.store(qd, C + (size_t)b * T * T, T);
+  span.stop(clk);
 }
 
 }  // namespace gpf

@@ -92,7 +92,10 @@ __global__ void k_selftest_mfma(const double* a, const double* b, double* c) {
 
 // FP64 MFMA issue-rate probe: every wave runs `iters` rounds of 8 independent
 // v_mfma_f64_16x16x4_f64 chains (2048 flops each); out[block] keeps the result live.
-__global__ __launch_bounds__(NTHR) void k_mfma_rate(int iters, double seed, double* out) {
+__global__ __launch_bounds__(NTHR) void k_mfma_rate(int iters, double seed, double* out, unsigned long long* clk) {
+  __shared__ unsigned long long cs[2];
+  const ClockSpan span(cs);
+  span.start(clk);
   d4 acc[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) acc[i] = d4{0.0, 0.0, 0.0, 0.0};
@@ -105,6 +108,7 @@ __global__ __launch_bounds__(NTHR) void k_mfma_rate(int iters, double seed, doub
 #pragma unroll
   for (int i = 0; i < 8; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
   if (s == 12345.678) out[blockIdx.x] = s;  // practically never taken; keeps the chains live
+  span.stop(clk);
 }
 
 }  // namespace gpf

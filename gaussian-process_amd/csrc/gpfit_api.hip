@@ -54,6 +54,10 @@ struct gpf_ctx {
   hipStream_t stream = nullptr;
   hipStream_t sub[MAX_GROUPS] = {};  // one stream per particle group (run_factor)
   hipStream_t pside = nullptr;       // gpf_predict's side stream (lowest priority: V beside the factor)
+  // gpf_predict's CU-partitioned pipeline (GPF_PRED_VCU > 0): V's row tiles on p_vcu CUs (pv), the
+  // single-particle factorisation on the others (pf); created on first use, sized by p_vcu
+  hipStream_t pv = nullptr, pf = nullptr;
+  int p_vcu = 0;
   hipEvent_t fork = nullptr, join[MAX_GROUPS] = {};
   std::string err;
 
@@ -99,7 +103,7 @@ struct gpf_ctx {
   double *p_hx = nullptr, *p_hout = nullptr;  // pinned staging: query coordinates, (mu, sd)
   double* p_vz = nullptr;                      // per row tile of V = U K_s: V^T z partials of mu (gpf::k_predict_vsq)
   std::vector<hipEvent_t> pev;                 // gpf_predict: factor launch J done (row tile J of U final), nt of them
-  hipEvent_t pev_x = nullptr, pev_side = nullptr;
+  hipEvent_t pev_x = nullptr, pev_side = nullptr, pev_cc = nullptr, pev_v = nullptr, pev_f = nullptr;
   int64_t p_cols = 0, p_np = 0;
   int p_d = 0, p_nt = 0;
   // gpf_prob_surface's row-chunk buffers, kept between calls like the prediction's
@@ -122,6 +126,7 @@ struct gpf_ctx {
   // profiling
   bool prof = false;
   unsigned long long* d_clk = nullptr;  // shader-clock probe of the factor kernels (gpf::ClockSpan), profiling only
+  double bench_sclk = 0.0;              // shader clock (MHz) of the last gpf_mfma_peak / gpf_gemm_bench
   double acc[PC_N][3] = {};  // ms, launches, work
   double evals = 0;
   std::vector<Pending> pend;
@@ -818,6 +823,10 @@ void gpf_close(gpf_ctx* c) {
   for (auto e : c->pev) hipEventDestroy(e);
   if (c->pev_x) hipEventDestroy(c->pev_x);
   if (c->pev_side) hipEventDestroy(c->pev_side);
+  for (hipEvent_t e : {c->pev_cc, c->pev_v, c->pev_f})
+    if (e) hipEventDestroy(e);
+  if (c->pv) hipStreamDestroy(c->pv);
+  if (c->pf) hipStreamDestroy(c->pf);
   if (c->pside) hipStreamDestroy(c->pside);
   for (int g = 0; g < MAX_GROUPS; ++g) {
     if (c->sub[g]) hipStreamDestroy(c->sub[g]);
@@ -1064,6 +1073,48 @@ static int factor_single(gpf_ctx* c, const double* ls, double** alpha_out) {
   return rc;
 }
 
+// The V set of the CU-partitioned prediction (include/gpfit.h): the CUs f(r) of ranks r < vcu,
+// f(r) = r[2:0] | r[4:3] << 3 | (r[2:0] ^ r[7:5]) << 5 — any 8 consecutive ranks cover the 8 values
+// of both bits [2:0] and bits [7:5] of the CU index, so a multiple of 8 CUs splits evenly over the
+// XCDs whether the mask bits interleave over them or block them (f is a bijection of 0..255).
+int gpf_cu_partition(int ncu, int vcu, uint32_t* mask, int words) {
+  if (ncu <= 0 || vcu < 0 || !mask || words * 32 < ncu) return -1;
+  for (int w = 0; w < words; ++w) mask[w] = 0;
+  int n = 0;
+  const int span = ncu <= 256 ? 256 : ncu;
+  for (int r = 0; r < span && n < vcu; ++r) {
+    const int i = ncu <= 256 ? ((r & 7) | (((r >> 3) & 3) << 3) | ((((r & 7) ^ (r >> 5)) & 7) << 5)) : r;
+    if (i >= ncu) continue;
+    mask[i >> 5] |= 1u << (i & 31);
+    ++n;
+  }
+  return n;
+}
+
+// gpf_predict's masked streams for vcu V CUs (created once per vcu; the old pair is destroyed
+// after the library stream drained, as gpf_predict enters with nothing of its own in flight)
+static int ensure_pred_streams(gpf_ctx* c, int vcu) {
+  if (c->pv && c->pf && c->p_vcu == vcu) return GPF_OK;
+  GPF_HIP(c, hipDeviceSynchronize());
+  if (c->pv) hipStreamDestroy(c->pv);
+  if (c->pf) hipStreamDestroy(c->pf);
+  c->pv = c->pf = nullptr;
+  c->p_vcu = 0;
+  const int words = (c->ncu + 31) / 32;
+  std::vector<uint32_t> mv(words), mf(words);
+  if (gpf_cu_partition(c->ncu, vcu, mv.data(), words) != vcu) return bad_arg(c, "GPF_PRED_VCU: bad CU count");
+  for (int w = 0; w < words; ++w) {
+    const int bits = std::min(32, c->ncu - 32 * w);
+    mf[w] = ~mv[w] & (bits == 32 ? 0xffffffffu : ((1u << bits) - 1u));
+  }
+  GPF_HIP(c, hipExtStreamCreateWithCUMask(&c->pv, (uint32_t)words, mv.data()));
+  GPF_HIP(c, hipExtStreamCreateWithCUMask(&c->pf, (uint32_t)words, mf.data()));
+  for (hipEvent_t* e : {&c->pev_cc, &c->pev_v, &c->pev_f})
+    if (!*e) GPF_HIP(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
+  c->p_vcu = vcu;
+  return GPF_OK;
+}
+
 int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int64_t batch, double* mu,
                 double* sd) {
   if (!c) return GPF_BAD_ARG;
@@ -1123,6 +1174,18 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
   bool pipe = false;
   if (const char* e = getenv("GPF_PREDICT_PIPE")) pipe = atoi(e) != 0 && c->nt >= 2;
   hipStream_t side = c->pside;
+  // CU-partitioned pipeline (GPF_PRED_VCU = V's CUs, with GPF_PREDICT_PIPE): beside the
+  // factorisation V's row tiles run on their own CUs (a stream CU mask, gpf_cu_partition) and the
+  // factor's workgroups on the others, so no V workgroup shares a CU with the factor's
+  // latency-bound chain; the row tiles of the factor's last GPF_PRED_VTAIL launches run after it on
+  // the whole chip
+  int vcu = 0, vtail = 4;
+  if (const char* e = getenv("GPF_PRED_VCU")) vcu = pipe ? std::max(0, std::min(c->ncu - 8, atoi(e))) : 0;
+  if (const char* e = getenv("GPF_PRED_VTAIL")) vtail = std::max(1, atoi(e));
+  const bool masked = vcu > 0;
+  if (masked)
+    if (int rs = ensure_pred_streams(c, vcu)) return rs;
+  hipStream_t vst = masked ? c->pv : side;  // V's row tiles beside the factorisation
   if (pipe) {
     if (!c->pev_x) GPF_HIP(c, hipEventCreateWithFlags(&c->pev_x, hipEventDisableTiming));
     if (!c->pev_side) GPF_HIP(c, hipEventCreateWithFlags(&c->pev_side, hipEventDisableTiming));
@@ -1151,7 +1214,7 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
   // CU's 160 KiB), so every CU keeps a slot for the factor's workgroups (one per CU under the
   // balanced split), and the factor's waves run at a higher issue priority (k_step, la bit 8)
   auto vsq = [&](hipStream_t st, int nqt, int t0, int rows) {
-    const size_t pad = st == side ? 17 * 1024 : 0;
+    const size_t pad = (st == side && !masked) ? 17 * 1024 : 0;
     const double Cm = (double)nqt * T;
     const double vflops = 2.0 * T * T * Cm * ((double)(t0 + rows) * (t0 + rows + 1) / 2 - (double)t0 * (t0 + 1) / 2) -
                           (double)T * T * Cm * rows;
@@ -1167,24 +1230,46 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
   if (rc) return rc;
   if (pipe) GPF_HIP(c, hipEventRecord(c->pev_x, c->stream));
   double* alpha = nullptr;
+  if (masked) {  // the factorisation on its CUs: run_factor queues on c->stream, so lend it pf
+    GPF_HIP(c, hipStreamWaitEvent(c->pf, c->pev_x, 0));
+    std::swap(c->stream, c->pf);
+  }
   rc = factor_single_async(c, nullptr, &alpha, pipe ? c->pev.data() : nullptr);
+  if (masked) {
+    std::swap(c->stream, c->pf);
+    if (!rc) rc = hipEventRecord(c->pev_f, c->pf) == hipSuccess && hipStreamWaitEvent(c->stream, c->pev_f, 0) == hipSuccess
+                      ? GPF_OK
+                      : GPF_HIP_ERROR;
+  }
   if (rc) return rc;
   if (pipe) {
     const int64_t m = std::min<int64_t>(chunk, M);
     const int nqt = (int)((m + T - 1) / T);
-    GPF_HIP(c, hipStreamWaitEvent(side, c->pev_x, 0));
-    rc = cross_cov(side, m, nqt * T);
+    GPF_HIP(c, hipStreamWaitEvent(vst, c->pev_x, 0));
+    rc = cross_cov(vst, m, nqt * T);
+    if (!rc && masked) GPF_HIP(c, hipEventRecord(c->pev_cc, vst));
     // row tiles in batches of >= 512 workgroups (a batch of nqt workgroups per row tile alone
-    // would leave most slots idle and serialise the side stream behind the factor)
-    const int rows = std::max(1, std::min(c->nt, (512 + nqt - 1) / nqt));
-    for (int t = 0; rc == GPF_OK && t < c->nt; t += rows) {
-      const int r = std::min(rows, c->nt - t);
-      GPF_HIP(c, hipStreamWaitEvent(side, c->pev[t + r - 1], 0));
-      rc = vsq(side, nqt, t, r);
+    // would leave most slots idle and serialise the side stream behind the factor); on the V CUs,
+    // batches of about two workgroups per CU, then the last vtail row tiles in one batch on the
+    // whole chip once the factorisation is done
+    const int rows = masked ? std::max(1, (2 * vcu + nqt - 1) / nqt) : std::max(1, std::min(c->nt, (512 + nqt - 1) / nqt));
+    const int tlate = masked ? std::max(0, c->nt - vtail) : c->nt;
+    for (int t = 0; rc == GPF_OK && t < c->nt;) {
+      const bool late = t >= tlate;
+      const int r = late ? c->nt - t : std::min(rows, tlate - t);
+      hipStream_t st = late ? side : vst;
+      if (late) GPF_HIP(c, hipStreamWaitEvent(side, c->pev_cc, 0));
+      GPF_HIP(c, hipStreamWaitEvent(st, c->pev[t + r - 1], 0));
+      rc = vsq(st, nqt, t, r);
+      t += r;
     }
     if (rc) return rc;
     GPF_HIP(c, hipEventRecord(c->pev_side, side));
     GPF_HIP(c, hipStreamWaitEvent(c->stream, c->pev_side, 0));
+    if (masked) {
+      GPF_HIP(c, hipEventRecord(c->pev_v, vst));
+      GPF_HIP(c, hipStreamWaitEvent(c->stream, c->pev_v, 0));
+    }
   }
   for (int64_t s = 0; s < M && rc == GPF_OK; s += chunk) {
     const int64_t m = std::min<int64_t>(chunk, M - s);
@@ -1221,6 +1306,10 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
     std::memcpy(sd + s, c->p_hout + Cp, (size_t)m * 8);
   }
   if (pipe) hipStreamSynchronize(side);
+  if (masked) {
+    hipStreamSynchronize(c->pv);
+    hipStreamSynchronize(c->pf);
+  }
   hipStreamSynchronize(c->stream);
   if (c->prof) harvest(c);
   // keep the query-chunk buffers for the next call only while they are modest (a huge batch_size
@@ -1597,6 +1686,19 @@ int gpf_debug_factor(gpf_ctx* c, const double* ls, double* L, double* U, double*
   return rc;
 }
 
+// Shader clock (MHz) from a ClockSpan buffer: shader clocks over 100 MHz reference clocks.
+static double read_clock(const unsigned long long* dclk) {
+  unsigned long long h[2] = {0, 0};
+  if (hipMemcpy(h, dclk, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess || h[1] == 0) return 0.0;
+  return 100.0 * (double)h[0] / (double)h[1];
+}
+
+int gpf_bench_clock(gpf_ctx* c, double* mhz) {
+  if (!c || !mhz) return GPF_BAD_ARG;
+  *mhz = c->bench_sclk;
+  return GPF_OK;
+}
+
 int gpf_mfma_peak(gpf_ctx* c, int blocks, int iters, double* tflops) {
   if (!c || !tflops || blocks <= 0 || iters <= 0) return GPF_BAD_ARG;
   hipSetDevice(c->device);
@@ -1605,11 +1707,16 @@ int gpf_mfma_peak(gpf_ctx* c, int blocks, int iters, double* tflops) {
   hipEvent_t a, b;
   GPF_HIP(c, hipEventCreate(&a));
   GPF_HIP(c, hipEventCreate(&b));
-  hipLaunchKernelGGL(gpf::k_mfma_rate, dim3(blocks), dim3(NTHR), 0, c->stream, iters, 1.0, out);  // warm-up
+  unsigned long long* clk = nullptr;
+  GPF_HIP(c, hipMalloc(&clk, 2 * sizeof(unsigned long long)));
+  GPF_HIP(c, hipMemsetAsync(clk, 0, 2 * sizeof(unsigned long long), c->stream));
+  hipLaunchKernelGGL(gpf::k_mfma_rate, dim3(blocks), dim3(NTHR), 0, c->stream, iters, 1.0, out, nullptr);  // warm-up
   GPF_HIP(c, hipEventRecord(a, c->stream));
-  hipLaunchKernelGGL(gpf::k_mfma_rate, dim3(blocks), dim3(NTHR), 0, c->stream, iters, 1.0, out);
+  hipLaunchKernelGGL(gpf::k_mfma_rate, dim3(blocks), dim3(NTHR), 0, c->stream, iters, 1.0, out, clk);
   GPF_HIP(c, hipEventRecord(b, c->stream));
   GPF_HIP(c, hipEventSynchronize(b));
+  c->bench_sclk = read_clock(clk);
+  hipFree(clk);
   float ms = 0.f;
   GPF_HIP(c, hipEventElapsedTime(&ms, a, b));
   *tflops = (double)blocks * 4.0 * iters * 8.0 * 2048.0 / (ms * 1e-3) / 1e12;
@@ -1746,17 +1853,26 @@ int gpf_gemm_bench(gpf_ctx* c, int mode, int Npad, int P, int tiles, int D, int 
   const size_t n = (size_t)P * Npad * Npad;
   GPF_HIP(c, hipMalloc(&L, n * 8));
   GPF_HIP(c, hipMalloc(&C, (size_t)P * tiles * T * T * 8));
-  GPF_HIP(c, hipMemsetAsync(L, 0, n * 8, c->stream));
+  // mode bit 8: zero operands (rounds 1-3); otherwise hashed values in [-1, 1) (gpf::k_fill_hash)
+  if (mode & 8)
+    GPF_HIP(c, hipMemsetAsync(L, 0, n * 8, c->stream));
+  else
+    hipLaunchKernelGGL(gpf::k_fill_hash, dim3(4096), dim3(NTHR), 0, c->stream, L, (long long)n);
   hipEvent_t a, b;
   GPF_HIP(c, hipEventCreate(&a));
   GPF_HIP(c, hipEventCreate(&b));
   const int W = P * tiles;
-  hipLaunchKernelGGL(gpf::k_gemm_bench, dim3(W), dim3(gpf::STEP_NTH), 0, c->stream, mode, D, Npad, P, L, C);
+  unsigned long long* clk = nullptr;
+  GPF_HIP(c, hipMalloc(&clk, 2 * sizeof(unsigned long long)));
+  GPF_HIP(c, hipMemsetAsync(clk, 0, 2 * sizeof(unsigned long long), c->stream));
+  hipLaunchKernelGGL(gpf::k_gemm_bench, dim3(W), dim3(gpf::STEP_NTH), 0, c->stream, mode, D, Npad, P, L, C, nullptr);
   GPF_HIP(c, hipEventRecord(a, c->stream));
   for (int i = 0; i < iters; ++i)
-    hipLaunchKernelGGL(gpf::k_gemm_bench, dim3(W), dim3(gpf::STEP_NTH), 0, c->stream, mode, D, Npad, P, L, C);
+    hipLaunchKernelGGL(gpf::k_gemm_bench, dim3(W), dim3(gpf::STEP_NTH), 0, c->stream, mode, D, Npad, P, L, C, clk);
   GPF_HIP(c, hipEventRecord(b, c->stream));
   GPF_HIP(c, hipEventSynchronize(b));
+  c->bench_sclk = read_clock(clk);
+  hipFree(clk);
   float ms = 0.f;
   GPF_HIP(c, hipEventElapsedTime(&ms, a, b));
   *tflops = 2.0 * T * T * (double)D * W * iters / (ms * 1e-3) / 1e12;

@@ -66,6 +66,8 @@ SIGNATURES = {
     "gpf_eval_batch_sharded": (ctypes.c_int, [_vp, _vp, _dp, ctypes.c_int, _dp, _ip]),
     "gpf_plan_check": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_longlong),
                                       ctypes.c_char_p, ctypes.c_int]),
+    "gpf_bench_clock": (ctypes.c_int, [_vp, _dp]),
+    "gpf_cu_partition": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]),
 }
 
 _LIB = None
@@ -110,6 +112,16 @@ def plan_check(particles, nt):
     keys = ("launches", "workgroups", "whole_tiles", "split_tiles", "S", "Smax", "groups", "diag_workgroups",
             "syrk_workgroups", "persistent")
     return dict(zip(keys, list(stats)))
+
+
+def cu_partition(ncu, vcu):
+    """The CU indices gpf_predict's V stream gets under GPF_PRED_VCU=vcu (gpf_cu_partition)."""
+    words = (int(ncu) + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    n = load_library().gpf_cu_partition(int(ncu), int(vcu), mask, words)
+    if n < 0:
+        raise ValueError("gpf_cu_partition: bad arguments")
+    return [i for i in range(ncu) if (mask[i >> 5] >> (i & 31)) & 1]
 
 
 def _f64(a):
@@ -293,6 +305,12 @@ class Context:
     def mfma_peak(self, blocks=1024, iters=4096):
         out = ctypes.c_double(0.0)
         self._check(self.lib.gpf_mfma_peak(self._h, int(blocks), int(iters), ctypes.byref(out)), "gpf_mfma_peak")
+        return out.value
+
+    def bench_clock(self):
+        """Shader clock (MHz) the last mfma_peak / gemm_bench held (gpf_bench_clock)."""
+        out = ctypes.c_double(0.0)
+        self._check(self.lib.gpf_bench_clock(self._h, ctypes.byref(out)), "gpf_bench_clock")
         return out.value
 
     def prob_surface(self, tails):

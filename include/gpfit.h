@@ -219,6 +219,13 @@ const char* gpf_build_info(void);
  * GPF_BAD_ARG with a description of the first violation in msg. */
 int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len);
 
+/* Host-only: the CU mask (words x 32 bits, bit i = CU i) that gpf_predict gives its V stream
+ * under GPF_PRED_VCU = vcu (the factorisation's stream gets the complement): CU i is the V set's
+ * if its rank in an order that deals consecutive CUs over the 8 XCDs whether the mask bits
+ * interleave over the XCDs (XCD = i % 8) or block them (XCD = i / 32) is < vcu. Returns the
+ * number of CUs set, or -1 on bad arguments. */
+int gpf_cu_partition(int ncu, int vcu, uint32_t* mask, int words);
+
 /* Self-test of the f64 MFMA fragment layout: C = A(16x4) B(4x16) on device,
  * compared on the host by the caller. a: 16x4 row-major, b: 4x16 row-major,
  * c: 16x16 row-major. */
@@ -239,9 +246,15 @@ int gpf_debug_factor64(gpf_ctx* ctx, const double* in, double* out, int* bad);
  * v_mfma_f64_16x16x4_f64 loop over `blocks` workgroups of 4 waves. */
 int gpf_mfma_peak(gpf_ctx* ctx, int blocks, int iters, double* tflops);
 
+/* The shader clock (MHz) the timed launches of the last gpf_mfma_peak or gpf_gemm_bench call
+ * held (every workgroup's span in s_memtime clocks over its span in the 100 MHz s_memrealtime
+ * clock; 0 before any such call). */
+int gpf_bench_clock(gpf_ctx* ctx, double* mhz);
+
 /* Measurement hook: TF/s of the block-column GEMM core alone (no factorisation):
  * P particles' Npad x Npad matrices, `tiles` workgroups per particle, depth D, `iters`
- * timed launches; mode 0 = per-particle operands, mode 1 = one shared (L2-resident) pair. */
+ * timed launches; mode 0 = per-particle operands, mode 1 = one shared (L2-resident) pair; mode
+ * bit 2 (4): U-tile-shaped operands; bit 3 (8): zero operands instead of hashed values in [-1, 1). */
 int gpf_gemm_bench(gpf_ctx* ctx, int mode, int Npad, int P, int tiles, int D, int iters, double* tflops);
 
 #ifdef __cplusplus

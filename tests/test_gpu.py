@@ -274,13 +274,18 @@ def test_chunked_batches_equal_single_batch(f3, monkeypatch):
     np.testing.assert_array_equal(full, chunked)
 
 
+@pytest.mark.parametrize("vcu", [None, "96", "128"])
 @pytest.mark.parametrize("N,d,M", [(1500, 2, 20000), (4096, 3, 3000)])
-def test_predict_pipeline_bitwise(ctx, monkeypatch, N, d, M):
-    """gpf_predict's pipelined schedule (GPF_PREDICT_PIPE=1, opt-in: the first query chunk's K_s
-    and V = U K_s on a side stream, row tiles of V behind the factor's launches) against the
-    serial default: the same kernels on the same data, so mu and sd bitwise equal; with two
-    query chunks (M > 16384: the second chunk runs on the main stream after the first) and with
-    one; mu = sum_t V_t^T z_t (no alpha) against the oracle's GP() on a sample of the queries."""
+def test_predict_pipeline_bitwise(ctx, monkeypatch, N, d, M, vcu):
+    """gpf_predict's pipelined schedule (GPF_PREDICT_PIPE=1: the first query chunk's K_s and
+    V = U K_s on a side stream, row tiles of V behind the factor's launches; with GPF_PRED_VCU the
+    CU-partitioned form, V on its own CUs by a stream CU mask and the factorisation on the others,
+    the last row tiles on the whole chip) against the serial schedule: the same kernels on the same
+    data, so mu and sd bitwise equal; with two query chunks (M > 16384: the second chunk runs on
+    the main stream after the first) and with one; mu = sum_t V_t^T z_t (no alpha) against the
+    oracle's GP() on a sample of the queries."""
+    if vcu is not None:
+        monkeypatch.setenv("GPF_PRED_VCU", vcu)
     rng = np.random.default_rng(N + M)
     x = rng.uniform(size=(d, N))
     y = np.sin(5 * x[0]) * np.cos(2 * x[-1]) + 0.1 * rng.standard_normal(N)
@@ -288,9 +293,9 @@ def test_predict_pipeline_bitwise(ctx, monkeypatch, N, d, M):
     xf = rng.uniform(-0.1, 1.1, size=(d, M))
     ls = rng.uniform(0.1, 0.4, size=d)
     ctx.set_data(x, y, e)
-    monkeypatch.setenv("GPF_PREDICT_PIPE", "1")  # (opt-in)
+    monkeypatch.setenv("GPF_PREDICT_PIPE", "1")
     a = ctx.predict(ls, xf)
-    monkeypatch.delenv("GPF_PREDICT_PIPE")
+    monkeypatch.setenv("GPF_PREDICT_PIPE", "0")
     b = ctx.predict(ls, xf)
     np.testing.assert_array_equal(a[0], b[0])
     np.testing.assert_array_equal(a[1], b[1])
