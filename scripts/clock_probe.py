@@ -13,7 +13,7 @@ ctx = gpfit.Context(0)
 FP64_SPEC, SPEC_MHZ = 78.6, 2400.0
 out = {}
 for name, mode, iters in (("core_zero_3", 10, 3), ("core_zero_1500", 10, 1500), ("core_3", 2, 3), ("core_300", 2, 300),
-                          ("core_1500", 2, 1500)):
+                          ("core_1500", 2, 1500), ("core_shared_1500", 1, 1500)):
     t = time.time()
     tf = ctx.gemm_bench(mode=mode, npad=4096, particles=64, tiles=15, depth=2048, iters=iters)
     mhz = ctx.bench_clock()
