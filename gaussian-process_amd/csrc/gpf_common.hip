@@ -420,6 +420,46 @@ __device__ __forceinline__ void gemm_stream_dl(Acc<128>& acc, const double* __re
   __syncthreads();
 }
 
+// gemm_stream_dl over [0, K) that stops after the first K1 (a multiple of 16, 0 <= K1 < K) for
+// wait(): the chunks [0, K1/16) run (the last of them prefetches nothing), then wait() — a
+// workgroup-uniform hand-off that returns true to abandon the GEMM (the result is then not used) —
+// then chunk K1/16 is issued and the rest runs. One DenseRun and one set of per-lane offsets for both
+// parts (two gemm_stream_dl calls around a wait kept both sets and the accumulators live across it
+// and spilled); the same chunks and MFMAs in the same order: bitwise the one-piece GEMM.
+// TRI: TRI_NONE, or TRI_B_KGEC with K1 at or past the triangular first 128 rows.
+template <bool NN, bool NEG, int TRI, typename W>
+__device__ __forceinline__ bool gemm_stream_dl_wait(Acc<128>& acc, const double* __restrict__ Ap, int lda,
+                                                    const double* __restrict__ Bp, int ldb, int K, int K1, double* smem,
+                                                    const Quad<128>& qd, W wait) {
+  static_assert(TRI == TRI_NONE || TRI == TRI_B_KGEC, "gemm_stream_dl_wait: known-zero pattern");
+  const int nch = K / DL_KC, n1 = K1 / DL_KC;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const double* Ar = uniform_ptr(Ap);
+  const double* Br = uniform_ptr(Bp);
+  const DenseRun<NN, NEG> dr(qd, lda, ldb, wave);
+  if (n1 > 0) {
+    dr.template issue<0>(Ar, Br, ldb, 0, smem);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // (as in gemm_stream_dl)
+    if constexpr (TRI == TRI_B_KGEC) {
+      const int t1 = min(n1, qd.cb / 16);
+      dr.template run<8>(acc, Ar, Br, ldb, 0, t1, n1, smem);
+      dr.template run<0>(acc, Ar, Br, ldb, t1, n1, n1, smem);
+    } else {
+      dr.template run<0>(acc, Ar, Br, ldb, 0, n1, n1, smem);
+    }
+    __syncthreads();  // every wave's reads of the last buffer are done
+  }
+  if (wait()) return false;
+  if (n1 & 1)
+    dr.template issue<1>(Ar, Br, ldb, n1, smem);
+  else
+    dr.template issue<0>(Ar, Br, ldb, n1, smem);
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  dr.template run<0>(acc, Ar, Br, ldb, n1, nch, nch, smem);
+  __syncthreads();
+  return true;
+}
+
 // Symmetric rank-K update of a 128x128 tile: C -= A A^T for its lower triangle only, A (128 x K)
 // a [r][k] row panel streamed through the direct-to-LDS pipeline. The wave with column slab s
 // owns the row blocks mi >= s of its slab (the others lie above the diagonal and are never read):

@@ -26,8 +26,10 @@
 //   ucol[K] = number of block rows of U finished in block column K   (diagonal K stores K+1 once
 //             U_KK and z_K are out, U tile (J, K) stores J+1)
 //   sdone[I] = 1 once the SYRK item has published S for diagonal block I
-// so L tile (J, I) waits for lcol[I] >= J and lcol[J] >= J before its GEMM and for ucol[J] >= J+1
-// before its finish; U tile (J, K) for lcol[J] >= J and ucol[K] >= J, then ucol[J] >= J+1; SYRK
+// so L tile (J, I) waits for lcol[I] >= J-1 and lcol[J] >= J-1 before the GEMM over the columns
+// < J-1 (r4 look-ahead), for lcol[I] >= J and lcol[J] >= J before the last block column, and for
+// ucol[J] >= J+1 before its finish; U tile (J, K) for lcol[J] >= J and ucol[K] >= J, then
+// ucol[J] >= J+1; SYRK
 // (J) for lcol[J+1] >= J; the critical tile also for sdone[J+1]. Each counter is written in
 // increasing order because each of its writers depends on the previous one.
 //
@@ -191,12 +193,20 @@ __device__ __forceinline__ void p_ltile(const PItem& a, const PState& st, int J,
   const int g = qd.lane >> 4, cl = qd.lane & 15;
   double* zj = lds + STEP_ZJ;
   double* Aij = Lp + (size_t)I * T * ld + (size_t)J * T;
-  // D = C^T = A_JI - L_J,<J L_I,<J^T (rows I and J through column J-1)
-  if (J > 0 && p_wait(lc + I, J, lc + J, J, info, st.abort, a.spins, sflag)) return;
+  // D = C^T = A_JI - L_J,<J L_I,<J^T (rows I and J through column J-1). Look-ahead (r4): the GEMM
+  // over the columns < J-1 needs rows I and J only through column J-2, so it starts as soon as
+  // block column J-2 has them — while column J-1's chain (its critical tile, which produces
+  // L_{J,J-1}, and diagonal factor) still runs; the last block column J-1 follows once rows I and
+  // J have it. The same chunks in the same order: bitwise the one-piece GEMM.
   Acc<T> acc;
+  if (J > 1 && p_wait(lc + I, J - 1, lc + J, J - 1, info, st.abort, a.spins, sflag)) return;
   cov_tile_acc(acc, qd, a.x, a.ls + (size_t)p * a.d, a.d, a.N, J, I, lds);
-  if (J > 0)
-    gemm_stream_dl<false, true>(acc, Lp + (size_t)J * T * ld, a.Npad, Lp + (size_t)I * T * ld, a.Npad, J * T, lds, qd);
+  if (J > 0 && !gemm_stream_dl_wait<false, true, TRI_NONE>(acc, Lp + (size_t)J * T * ld, a.Npad, Lp + (size_t)I * T * ld,
+                                                           a.Npad, J * T, (J - 1) * T, lds, qd, [&] {
+                                                             return p_wait(lc + I, J, lc + J, J, info, st.abort, a.spins,
+                                                                           sflag);
+                                                           }))
+    return;
   // U_JJ and z_J (diagonal block J)
   if (p_wait(uc + J, J + 1, uc + J, J + 1, info, st.abort, a.spins, sflag)) return;
   if (tid < T) zj[tid] = p_ld(yp + J * T + tid);
@@ -334,9 +344,15 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_factor(PI
     squeue = q;
   }
   __syncthreads();
-  const long long tk = sticket;
+  // (the ticket and queue come through LDS: readfirstlane makes them — and the particle, column
+  // and tile decoded from them, and every counter address — scalar, so they do not occupy vector
+  // registers across the tile's GEMM)
+  const long long tk0 = sticket;
+  const long long tk = (long long)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)((unsigned long long)tk0 >> 32))
+                                    << 32) |
+                                   (unsigned)__builtin_amdgcn_readfirstlane((unsigned)tk0));
   if (tk < 0) return;
-  const int q = squeue;
+  const int q = __builtin_amdgcn_readfirstlane(squeue);
   // column of ticket tk: items before column J = npq (J (nt-1) + #SYRK columns < J), monotone in J
   const long long npq = p_npq(P, q);
   int lo = 0, hi = nt - 1;
