@@ -879,11 +879,34 @@ __host__ __device__ __forceinline__ int split_all_pieces(int J, int w, int nt, i
 // w = -1), reduces the next diagonal block (ROLE_SYRK, w = -1), runs the whole tile, one depth
 // range (piece sidx of S) of it, or nothing. The kernel and the host-side plan check
 // (gpf_plan_check) both decode through this function.
+// ro (r4, "reordered"; launches with diagonal and SYRK workgroups, no split, particle-fastest
+// tiles): the dispatcher deals a launch's workgroups over the CUs in block order, so with more
+// workgroups than CUs the last ones land on the CUs of the first — the diagonal workgroups, in the
+// order above: every diagonal factor of config B's launches 1..nt-2 shared its CU, 56-61 us instead
+// of 46 alone (profiles/r4/diag_coresidence_B.txt). Reordered: first the lightest tile of each
+// particle (the U tile K = J-1, one 128-deep block, that then waits for the diagonal block), then
+// the SYRK and the diagonal workgroups, then the other tiles, the lightest last, so the CUs that
+// take two workgroups pair two light tiles and both chains (the diagonal factor; the SYRK update
+// and the look-ahead) run alone. (SYRK workgroups last, paired with the light U tiles, ran the
+// diagonal factor alone too but cost B 2%: profiles/r4/diag_coresidence_B_reorder1.txt.)
 template <int SPLIT>
 __host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt, int grp, int S, int ed, int sy, int la,
-                                                    int& p, int& w, int& sidx) {
+                                                    int& p, int& w, int& sidx, int ro = 0) {
   const int tiles = P * (nt - 1);
   sidx = 0;
+  if (SPLIT == SPLIT_NONE && ro) {  // (ed, sy, J >= 1, grp == 0: gpf_plan_check)
+    p = b % P;
+    if (b < P) {
+      w = nt - 2;  // U tile K = J - 1
+      return ROLE_WHOLE;
+    }
+    if (b < 3 * P) {
+      w = -1;
+      return b < 2 * P ? ROLE_SYRK : ROLE_DIAG;
+    }
+    w = (b - 3 * P) / P;  // tiles w = 0 .. nt-3, particle fastest
+    return ROLE_WHOLE;
+  }
   if (ed) {
     if (b < P) {
       p = b;
@@ -1420,7 +1443,8 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
   if (la & 8) __builtin_amdgcn_s_setprio(2);
   int p, w, sidx;
   const int role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, SPLIT != SPLIT_ALL && sy,
-                                      SPLIT == SPLIT_NONE && ED && (la & 1) && !sy, p, w, sidx);
+                                      SPLIT == SPLIT_NONE && ED && (la & 1) && !sy, p, w, sidx,
+                                      SPLIT == SPLIT_NONE && ED && (la & 32) != 0);
 #ifdef GPF_CHECK
   // diagnostic build (-DGPF_CHECK): every index the workgroup derives its addresses from, checked
   // against the launch's extents before any access (an out-of-range role prints and does nothing)

@@ -430,6 +430,14 @@ static bool look_ahead(int pc, int nt) {
   return on && nt >= 4;
 }
 
+// Reordered dispatch of early-diagonal launches with SYRK workgroups (gpf::step_decode ro): the
+// diagonal factors get their CUs alone. GPF_REORDER = 0/1 overrides.
+static bool reorder_on() {
+  bool on = true;
+  if (const char* s = getenv("GPF_REORDER")) on = atoi(s) != 0;
+  return on;
+}
+
 // Bound of the early-diagonal hand-off spin (gpf::wait_diag, polls of ~1 us): ~2 s by default;
 // GPF_WAIT_SPINS lowers it to exercise the timeout report (tests/test_gpu.py).
 static int wait_spins() {
@@ -526,6 +534,7 @@ struct StepLaunch {
   int J, g, p0, gc, split, S, S2, grp, ed;  // S: pieces per split tile (SPLIT_ALL: chunks per piece); S2: partial
                                             // slots per tile; ed: the launch starts with gc diagonal workgroups
   int defer, sy;                        // deferred diagonal update; sy: gc SYRK workgroups follow
+  int ro;  // reordered dispatch (gpf::step_decode ro): light U tiles, diagonal, other tiles, SYRK workgroups
   int la;  // look-ahead: bit 0: gc LA workgroups follow (gpf::la_item); bit 1: the critical tiles seed from launch J-1's
   unsigned grid;
   size_t part_off, cnt_off;
@@ -556,6 +565,9 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
       const bool prev_none = J >= 1 && (S > 1 ? false : split_crit(pc, nt, J - 1, l.grp, S) <= 1);
       const bool next_none = S > 1 ? false : split_crit(pc, nt, J + 1, l.grp, S) <= 1;
       l.la = ((la_ok && next_none && J >= 1 && J <= nt - 3) ? 1 : 0) | ((la_ok && prev_none && J >= 2 && J <= nt - 2) ? 2 : 0);
+      // reordered dispatch: only where the first 3 gc workgroups (the light U tiles, which wait for
+      // the diagonal workgroups behind them, and the SYRK workgroups) fit the chip's CUs at once
+      l.ro = (reorder_on() && l.ed && l.sy && l.split == gpf::SPLIT_NONE && l.grp == 0 && J >= 1 && 3 * l.gc <= 256) ? 1 : 0;
       int nall = 0;
       for (int w = 0; S > 1 && w < nt - 1; ++w) nall += gpf::split_all_pieces(J, w, nt, l.S);
       l.grid = (S > 1 ? l.gc * nall : l.gc * (nt - 1) + l.gc * (Sc - 1)) + (l.ed ? l.gc : 0) + (l.sy ? l.gc : 0) +
@@ -697,7 +709,8 @@ static int run_factor(gpf_ctx* c, int pc, hipEvent_t* after = nullptr) {
                          c->d_U + (size_t)p0 * ld * ld, c->d_yb + (size_t)p0 * ld, c->d_s2p + (size_t)p0 * nt * ld,
                          c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc, l.grp, N, c->d_x,
                          c->d_ls + (size_t)p0 * c->d, c->d, l.S, l.S2, partg, cntg, c->d_flag + p0, l.ed,
-                         c->d_cflag + p0, l.defer, l.sy, spins, l.la | ((l.la & 2) ? la_delay : 0) | (after ? 8 : 0),
+                         c->d_cflag + p0, l.defer, l.sy, spins,
+                         l.la | ((l.la & 2) ? la_delay : 0) | (after ? 8 : 0) | (l.ro ? 32 : 0),
                          l.la ? c->d_la + 2 * (size_t)p0 * T * T : nullptr, c->prof ? c->d_clk : nullptr);
     });
     if (rc) return rc;
@@ -1507,6 +1520,9 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     if ((la_prev[l.g] & 1) && !(l.la & 2))
       return plan_fail(msg, msg_len, "J=%d g=%d: look-ahead partials of launch J-1 left unused", l.J, l.g);
     la_prev[l.g] = l.la;
+    if (l.ro && (!l.ed || !l.sy || l.split != gpf::SPLIT_NONE || l.grp != 0 || l.J < 1 || 3 * l.gc > 256 ||
+                 l.grid != (unsigned)(l.gc * (nt - 1) + 2 * l.gc)))
+      return plan_fail(msg, msg_len, "J=%d g=%d: reordered dispatch out of place", l.J, l.g);
     std::vector<int> lawg((size_t)l.gc, 0);
     for (unsigned b = 0; b < l.grid; ++b) {
       int p = -1, w = -1, sidx = -1;
@@ -1514,9 +1530,10 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
           l.split == gpf::SPLIT_ALL    ? gpf::step_decode<gpf::SPLIT_ALL>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, 0, 0, p, w, sidx)
           : l.split == gpf::SPLIT_CRIT ? gpf::step_decode<gpf::SPLIT_CRIT>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.sy, 0, p, w, sidx)
                                        : gpf::step_decode<gpf::SPLIT_NONE>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.sy,
-                                                                           (l.la & 1) && !l.sy, p, w, sidx);
+                                                                           (l.la & 1) && !l.sy, p, w, sidx, l.ro);
       if (role == gpf::ROLE_DIAG) {  // one diagonal workgroup per particle, ahead of every tile of the launch
-        if (!l.ed || p < 0 || p >= l.gc || (unsigned)p != b || diag[p]++)
+        // (reordered: right behind the particles' light U tiles, which wait for it, and the SYRK workgroups)
+        if (!l.ed || p < 0 || p >= l.gc || (unsigned)p + (l.ro ? 2 * l.gc : 0) != b || diag[p]++)
           return plan_fail(msg, msg_len, "J=%d block %u: misplaced or duplicate diagonal workgroup (p=%d)", l.J, b, p);
         ++wgs;
         continue;
@@ -1527,8 +1544,8 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
         ++wgs;
         continue;
       }
-      if (role == gpf::ROLE_SYRK) {  // one per particle, right behind the diagonal workgroups
-        if (!l.sy || p < 0 || p >= l.gc || (unsigned)p + (l.ed ? l.gc : 0) != b || syrk[p]++)
+      if (role == gpf::ROLE_SYRK) {  // one per particle, right behind the diagonal workgroups (reordered: the light U tiles)
+        if (!l.sy || p < 0 || p >= l.gc || (unsigned)p + (l.ro || l.ed ? l.gc : 0) != b || syrk[p]++)
           return plan_fail(msg, msg_len, "J=%d block %u: misplaced or duplicate SYRK workgroup (p=%d)", l.J, b, p);
         ++wgs;
         continue;

@@ -792,6 +792,35 @@ def test_critical_tile_lookahead_bitwise(ctx, monkeypatch, N, d, P):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("N,d,P", [(1024, 2, 32), (2048, 3, 20), (1500, 2, 7)])
+def test_reordered_dispatch_bitwise(ctx, monkeypatch, N, d, P):
+    """The reordered dispatch of early-diagonal launches with SYRK workgroups (r4, gpf::step_decode
+    ro: the light U tiles first, then the diagonal workgroups, the other tiles, the SYRK workgroups
+    last, so that the diagonal factors do not share their CUs) only changes which workgroup runs
+    where: scores, mean and sd bitwise equal with it off (GPF_REORDER=0), config B's shape included."""
+    import gpfit
+    rng = np.random.default_rng(N + 3 * P)
+    x = rng.uniform(size=(d, N))
+    y = np.sin(3 * x[0]) + x[-1] ** 2 + 0.1 * rng.standard_normal(N)
+    e = rng.uniform(0.05, 0.2, size=N)
+    s, ex = ref_cpu.sigma_grid()
+    lo, hi = ref_cpu.search_bounds(x)
+    ctx.set_data(x, y, e)
+    ctx.set_grid(s, ex, lo, hi)
+    Q = rng.uniform(0.1, 0.5, size=(P, d))
+    st = gpfit.plan_check(P, -(-N // 128))
+    assert st["diag_workgroups"] > 0 and st["syrk_workgroups"] > 0 and st["S"] == 1
+    on = ctx.eval_batch(Q, want_mu_sd=True)
+    monkeypatch.setenv("GPF_REORDER", "0")
+    off = ctx.eval_batch(Q, want_mu_sd=True)
+    monkeypatch.delenv("GPF_REORDER")
+    for a, b in zip(on, off):
+        np.testing.assert_array_equal(a, b)
+    mo, so = ref_cpu.GP_train_identity(x, y, e, Q[-1])
+    assert _rel(on[1][-1], mo) < RTOL_MU_SD and _rel(on[2][-1], so) < RTOL_MU_SD
+
+
+@pytest.mark.gpu
 def test_lookahead_partials_survive_late_critical_tile(ctx, monkeypatch):
     """the look-ahead partial of launch J is double-buffered by launch parity
     (gpf::la_slot), so a critical tile dispatched after its own launch's look-ahead has already
