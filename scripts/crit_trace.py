@@ -98,6 +98,11 @@ for J in range(nt - 1):
         ids = [b for b in range(ed, ed + np0 * P, P) if live[b]]
     else:  # critical-tile split (csrc/gpfit_api.hip split_crit, off by default): pieces at b = off + s * P
         off = ed + (P if (plan["syrk_workgroups"] > 0 and 1 <= J <= nt - 2) else 0)
+        # r4 reordered dispatch (GPF_REORDER, default on): light U tiles, SYRK, diagonal, then w = 0
+        ro = (os.environ.get("GPF_REORDER", "1") != "0" and ed and plan["syrk_workgroups"] > 0 and 1 <= J <= nt - 2
+              and 3 * P <= 256)
+        if ro:
+            off = 3 * P
         if os.environ.get("GPF_LOOKAHEAD", "0") != "0" and ed and 1 <= J <= nt - 3 and plan["syrk_workgroups"] == 0:
             off += P  # look-ahead workgroups of their own (gpf::la_item; with SYRK workgroups it rides on them)
         S = 1 if (J == 0 or J >= nt - 1 or nt < 4) else min(int(os.environ.get("GPF_SPLIT_CRIT", 1)), max(1, J * T // 16 // 16))
@@ -105,7 +110,9 @@ for J in range(nt - 1):
             S -= 1
         ids = [off + s * P for s in range(S) if live[off + s * P]]
     last = int(np.argmax(np.where(live, en, 0)))
-    dg = f" diag end {(en[0] - t0) * 1e-2:6.1f}" if ed else ""
+    d0 = 2 * P if (mode != "predict" and ed and plan["syrk_workgroups"] > 0 and 1 <= J <= nt - 2 and 3 * P <= 256
+                   and os.environ.get("GPF_REORDER", "1") != "0") else 0
+    dg = f" diag end {(en[d0] - t0) * 1e-2:6.1f}" if ed else ""
     if not ids:
         print(f"{J:2d} {span:7.1f}")
         continue
