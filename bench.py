@@ -266,6 +266,34 @@ def hull_line(ctx, args):
     return out
 
 
+def kmeans_line(ctx, args):
+    """Secondary measurement, SURVEY.md §8f row 2: the KMeans subsample of len_scale_opt
+    (find_len_scales.py:25-47) at config E's size (N=16384, d=4 -> 100 points): the fit with its
+    Lloyd E/M-steps on the GPU (gpfit.kmeans; sklearn's seeding on the host) beside sklearn's own
+    KMeans.fit (the reference's call) on the host, both timed whole, labels compared."""
+    from sklearn.cluster import KMeans
+    from gpfit.kmeans import kmeans_fit
+    rng = np.random.default_rng(args.seed + 5)
+    X = rng.uniform(size=(16384, 4))
+    kmeans_fit(ctx, X[:2048], 100)  # warm-up (first launches, sklearn import)
+    t0 = time.perf_counter()
+    labels, _ = kmeans_fit(ctx, X, 100)
+    gdt = time.perf_counter() - t0
+    out = {"N": 16384, "d": 4, "clusters": 100, "ms": gdt * 1e3,
+           "note": "GPU: the Lloyd iterations' E/M-steps (gpf_kmeans_step); host: k-means++ seeding (sklearn) "
+                   "and the O(k d) loop bookkeeping"}
+    if not args.no_cpu:
+        KMeans(n_clusters=100, n_init="auto", random_state=0).fit(X[:2048])
+        t1 = time.perf_counter()
+        km = KMeans(n_clusters=100, n_init="auto", random_state=0).fit(X)
+        cdt = time.perf_counter() - t1
+        out["cpu_baseline"] = {"ms": cdt * 1e3, "kind": "reference call", "threads": "sklearn/OpenMP default",
+                               "sample": "sklearn KMeans(100, n_init='auto', random_state=0).fit, the full case"}
+        out["labels_equal"] = bool(np.array_equal(labels, km.labels_))
+        out["iterations_sklearn"] = int(km.n_iter_)
+    return out
+
+
 def psurf_line(ctx, args):
     """Secondary measurement, SURVEY.md §8f row 4: probability surface of a merged frame of
     `psurf_rows` grid rows x 4 experiments (calc_prob_surf.py:15-30,67-81), kernel time from
@@ -448,6 +476,7 @@ def main():
                     help="secondary (SURVEY.md §8f row 1): GP prediction at this many query points, 0 = skip")
     ap.add_argument("--cpu-predict-points", type=int, default=256, help="CPU GP sample for the prediction line")
     ap.add_argument("--no-hull", action="store_true", help="skip the convex-hull grid line (SURVEY.md §8f row 3)")
+    ap.add_argument("--no-kmeans", action="store_true", help="skip the KMeans subsample line (SURVEY.md §8f row 2)")
     ap.add_argument("--psurf-rows", type=int, default=100000,
                     help="secondary (SURVEY.md §8f row 4): probability-surface rows, 0 = skip")
     ap.add_argument("--plumbing", action="store_true", help="CPU-only multi-rank plumbing check (no measurement)")
@@ -651,6 +680,9 @@ def main():
     hull = None
     if solo and not args.no_hull:
         hull = hull_line(ctx, args)
+    kmeans = None
+    if solo and not args.no_kmeans:
+        kmeans = kmeans_line(ctx, args)
     secondary = None
     if solo and not args.no_secondary:
         secondary = secondary_configs(ctx, args, prof["fp64_ceiling_at_sclk_tflops"] or None)
@@ -679,6 +711,7 @@ def main():
             "predict": predict,
             "prob_surface": psurf,
             "hull_grid": hull,
+            "kmeans": kmeans,
             "roofline": roof,
             "cpu_baseline": cpu,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,

@@ -27,6 +27,7 @@
 #include "gpf_predict.hip"
 #include "gpf_probsurf.hip"
 #include "gpf_hull.hip"
+#include "gpf_kmeans.hip"
 
 using gpf::BT;
 using gpf::NTHR;
@@ -117,6 +118,11 @@ struct gpf_ctx {
   double* h_ls = nullptr;
   double* h_loss = nullptr;
   int* h_info = nullptr;
+  // KMeans subsample (gpf_kmeans_set / gpf_kmeans_step): the centred points and the per-step buffers
+  double *km_x = nullptr, *km_c = nullptr, *km_dist = nullptr, *km_sums = nullptr, *km_cnt = nullptr;
+  int* km_lab = nullptr;
+  int64_t km_n = 0;
+  int km_d = 0, km_kcap = 0;
   // last convex-hull grid (gpf_hull_fill -> gpf_hull_fetch)
   std::vector<double> hull_rows;
   int hull_d = 0;
@@ -832,6 +838,7 @@ void gpf_close(gpf_ctx* c) {
   hipFree(c->d_x); hipFree(c->d_y); hipFree(c->d_e);
   hipFree(c->d_clk);
   hipFree(c->d_sig); hipFree(c->d_exp); hipFree(c->d_lo); hipFree(c->d_hi);
+  hipFree(c->km_x); hipFree(c->km_c); hipFree(c->km_dist); hipFree(c->km_sums); hipFree(c->km_cnt); hipFree(c->km_lab);
   for (auto e : c->pool) hipEventDestroy(e);
   for (auto e : c->pev) hipEventDestroy(e);
   if (c->pev_x) hipEventDestroy(c->pev_x);
@@ -1329,6 +1336,65 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
   // can size them up to half of free HBM; see keep_bytes)
   if ((double)c->p_np * (double)c->p_cols * 8.0 > keep_bytes()) free_pred(c);
   return rc;
+}
+
+// ---- KMeans subsample (find_len_scales.py:25-47; gpf_kmeans.hip) ----
+int gpf_kmeans_set(gpf_ctx* c, const double* X, int64_t n, int d) {
+  if (!c) return GPF_BAD_ARG;
+  if (n <= 0 || d <= 0 || d > gpf::DMAX || !X) return bad_arg(c, "gpf_kmeans_set: bad arguments");
+  hipSetDevice(c->device);
+  GPF_HIP(c, hipStreamSynchronize(c->stream));
+  if (n != c->km_n || d != c->km_d) {
+    hipFree(c->km_x); hipFree(c->km_dist); hipFree(c->km_lab);
+    c->km_x = c->km_dist = nullptr;
+    c->km_lab = nullptr;
+    c->km_n = 0;
+    GPF_HIP(c, hipMalloc(&c->km_x, (size_t)n * d * 8));
+    GPF_HIP(c, hipMalloc(&c->km_dist, (size_t)n * 8));
+    GPF_HIP(c, hipMalloc(&c->km_lab, (size_t)n * 4));
+    c->km_n = n;
+    c->km_d = d;
+  }
+  GPF_HIP(c, hipMemcpyAsync(c->km_x, X, (size_t)n * d * 8, hipMemcpyHostToDevice, c->stream));
+  GPF_HIP(c, hipStreamSynchronize(c->stream));
+  return GPF_OK;
+}
+
+int gpf_kmeans_step(gpf_ctx* c, const double* centers, int k, int update, int* labels, double* sums,
+                    double* counts, double* dist) {
+  if (!c) return GPF_BAD_ARG;
+  if (c->km_n <= 0) return bad_arg(c, "gpf_kmeans_step: call gpf_kmeans_set first");
+  const int d = c->km_d;
+  if (k <= 0 || (int64_t)k * d > gpf::KM_MAXKD || !centers || !labels || (update && (!sums || !counts)))
+    return bad_arg(c, "gpf_kmeans_step: bad arguments");
+  hipSetDevice(c->device);
+  if (k > c->km_kcap) {
+    GPF_HIP(c, hipStreamSynchronize(c->stream));
+    hipFree(c->km_c); hipFree(c->km_sums); hipFree(c->km_cnt);
+    c->km_c = c->km_sums = c->km_cnt = nullptr;
+    c->km_kcap = 0;
+    GPF_HIP(c, hipMalloc(&c->km_c, (size_t)k * d * 8));
+    GPF_HIP(c, hipMalloc(&c->km_sums, (size_t)k * d * 8));
+    GPF_HIP(c, hipMalloc(&c->km_cnt, (size_t)k * 8));
+    c->km_kcap = k;
+  }
+  const int64_t n = c->km_n;
+  GPF_HIP(c, hipMemcpyAsync(c->km_c, centers, (size_t)k * d * 8, hipMemcpyHostToDevice, c->stream));
+  const size_t lds = (size_t)(k * d + k) * 8;
+  hipLaunchKernelGGL(gpf::k_km_assign, dim3((unsigned)((n + NTHR - 1) / NTHR)), dim3(NTHR), lds, c->stream, n, d, k,
+                     c->km_x, c->km_c, c->km_lab, c->km_dist);
+  GPF_HIP(c, hipGetLastError());
+  if (update) {
+    hipLaunchKernelGGL(gpf::k_km_sums, dim3((unsigned)k), dim3(NTHR), 0, c->stream, n, d, c->km_x, c->km_lab, c->km_sums,
+                       c->km_cnt);
+    GPF_HIP(c, hipGetLastError());
+    GPF_HIP(c, hipMemcpyAsync(sums, c->km_sums, (size_t)k * d * 8, hipMemcpyDeviceToHost, c->stream));
+    GPF_HIP(c, hipMemcpyAsync(counts, c->km_cnt, (size_t)k * 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  GPF_HIP(c, hipMemcpyAsync(labels, c->km_lab, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+  if (dist) GPF_HIP(c, hipMemcpyAsync(dist, c->km_dist, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+  GPF_HIP(c, hipStreamSynchronize(c->stream));
+  return GPF_OK;
 }
 
 int gpf_kernel(gpf_ctx* c, const double* x1, int64_t N1, const double* x2, int64_t N2, int d, const double* l,

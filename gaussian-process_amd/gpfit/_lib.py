@@ -67,6 +67,8 @@ SIGNATURES = {
     "gpf_plan_check": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_longlong),
                                       ctypes.c_char_p, ctypes.c_int]),
     "gpf_bench_clock": (ctypes.c_int, [_vp, _dp]),
+    "gpf_kmeans_set": (ctypes.c_int, [_vp, _dp, ctypes.c_int64, ctypes.c_int]),
+    "gpf_kmeans_step": (ctypes.c_int, [_vp, _dp, ctypes.c_int, ctypes.c_int, _ip, _dp, _dp, _dp]),
     "gpf_cu_partition": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]),
 }
 
@@ -312,6 +314,28 @@ class Context:
         out = ctypes.c_double(0.0)
         self._check(self.lib.gpf_bench_clock(self._h, ctypes.byref(out)), "gpf_bench_clock")
         return out.value
+
+    def kmeans_set(self, X):
+        """Keep the (n, d) centred points on the device for kmeans_step (gpf_kmeans_set)."""
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        self._check(self.lib.gpf_kmeans_set(self._h, _ptr(X), X.shape[0], X.shape[1]), "gpf_kmeans_set")
+        self._km_n = X.shape[0]
+
+    def kmeans_step(self, centers, update=True, want_dist=False):
+        """One Lloyd E-step (+ M-step sums) against centers (k, d) (gpf_kmeans_step):
+        (labels, sums, counts, dist or None)."""
+        C = np.ascontiguousarray(centers, dtype=np.float64)
+        k, d = C.shape
+        labels = np.empty(self._km_n, dtype=np.int32)
+        sums = np.empty((k, d)) if update else None
+        counts = np.empty(k) if update else None
+        dist = np.empty(self._km_n) if want_dist else None
+        nul = ctypes.POINTER(ctypes.c_double)()
+        self._check(self.lib.gpf_kmeans_step(self._h, _ptr(C), k, int(bool(update)),
+                                             labels.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                             _ptr(sums) if update else nul, _ptr(counts) if update else nul,
+                                             _ptr(dist) if want_dist else nul), "gpf_kmeans_step")
+        return labels, sums, counts, dist
 
     def prob_surface(self, tails):
         """(y (M,100), p (M,100), ok (M,) bool) for each row of tail entries (gpf_prob_surface)."""

@@ -217,12 +217,18 @@ class Swarm:
             self.restarts += 1
 
 
-def prepare(x_known, y_known, e_known, *, max_points=MAX_POINTS, verbose=True):
-    """KMeans subsample above max_points (:25-47), bounds (:56-61), sigma grid (:66-67)."""
+def prepare(x_known, y_known, e_known, *, max_points=MAX_POINTS, verbose=True, ctx=None):
+    """KMeans subsample above max_points (:25-47), bounds (:56-61), sigma grid (:66-67). With a GPU
+    context the KMeans fit's Lloyd iterations run on it (gpfit.kmeans, r4); without one (the
+    injected-evaluator path of the CPU tests) sklearn's fit runs on the host, as in the reference."""
     if x_known.shape[1] > max_points:
         if verbose:
             print(f"Dataset too large ({x_known.shape[1]} points). Subsampling to {max_points} for hyperparameter optimisation.")
-        x_known, y_known, e_known = kmeans_representatives(x_known, y_known, e_known, max_points)
+        if ctx is not None:
+            from .kmeans import kmeans_representatives_gpu
+            x_known, y_known, e_known = kmeans_representatives_gpu(ctx, x_known, y_known, e_known, max_points)
+        else:
+            x_known, y_known, e_known = kmeans_representatives(x_known, y_known, e_known, max_points)
     lower, upper = search_bounds(x_known)
     sigma_vals, expected = sigma_grid()
     return x_known, y_known, e_known, lower, upper, sigma_vals, expected
@@ -258,8 +264,10 @@ def particle_swarm(x_known, y_known, e_known, PSO_progress, *, num_particles=NUM
     Returns (global_best_position, info) where info holds the final score,
     restart count and evaluation count.
     """
+    if evaluator is None and ctx is None:  # the GPU path: this process's context, the KMeans fit included
+        ctx = default_context()
     x_known, y_known, e_known, lower, upper, sigma_vals, expected = prepare(
-        x_known, y_known, e_known, max_points=max_points, verbose=verbose)
+        x_known, y_known, e_known, max_points=max_points, verbose=verbose, ctx=ctx if evaluator is None else None)
 
     score = make_scorer(x_known, y_known, e_known, sigma_vals, expected, lower, upper,
                         evaluator=evaluator, ctx=ctx, comm=comm)

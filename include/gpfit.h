@@ -110,6 +110,18 @@ int gpf_hull_fill(gpf_ctx* ctx, const double* shell, int64_t n, int d, const dou
                   int64_t* m);
 int gpf_hull_fetch(gpf_ctx* ctx, double* out);
 
+/* KMeans subsample (the Lloyd iterations of find_len_scales.py:27-31, sklearn KMeans(n_clusters,
+ * n_init='auto', random_state=0)). gpf_kmeans_set keeps n points x d
+ * (row-major, already centred by their mean as sklearn's fit does) on the device. One
+ * gpf_kmeans_step = the E-step (and with update != 0 the M-step sums) of sklearn's
+ * lloyd_iter_chunked_dense with unit weights against k centres (k x d, row-major, k*d <= 8192):
+ * labels[i] = the first j minimising ||c_j||^2 - 2 x_i.c_j; sums (k x d) and counts (k) of each
+ * cluster's members; dist[i] = ||x_i - c_labels[i]||^2 (optional, may be NULL). The host runs
+ * sklearn's loop around it (gaussian-process_amd/gpfit/kmeans.py). */
+int gpf_kmeans_set(gpf_ctx* ctx, const double* X, int64_t n, int d);
+int gpf_kmeans_step(gpf_ctx* ctx, const double* centers, int k, int update, int* labels, double* sums, double* counts,
+                    double* dist);
+
 /* ---- swarm exchange across ranks (one process per GPU) ----
  *
  * Replaces the cross-process half of the particle fan-out: the reference's single process

@@ -16,11 +16,11 @@ for r in $(seq ${REPS:-2}); do
       envs=${envs//,/ }
       tag=${spec//[^A-Za-z0-9_]/_}_${c}_$r
       if [ "$c" = PRED ]; then  # the prediction line: GP at 10k query points, N=4096 (median of 3 calls)
-        env $envs GPFIT_LIB=$PWD/gaussian-process_amd/libgpfit_$v.so timeout -k 10 300 python bench.py --steps 1 --warmup 1 --no-cpu --pso-steps 0 --no-hull --psurf-rows 0 --no-secondary > $O/$tag.log 2>&1 || exit $?
+        env $envs GPFIT_LIB=$PWD/gaussian-process_amd/libgpfit_$v.so timeout -k 10 300 python bench.py --steps 1 --warmup 1 --no-cpu --pso-steps 0 --no-hull --no-kmeans --psurf-rows 0 --no-secondary > $O/$tag.log 2>&1 || exit $?
         python -c "import json; d=json.loads(open('$O/$tag.log').read().strip().splitlines()[-1])['predict']; print('$spec $c #$r', round(d['ms'],3), 'ms (profiled', round(d.get('ms_profiled_pass',0),3), ') factor', round(d['factor_ms'],3), 'ms  cross_cov', round(d['k_cross_cov_GBps']), 'GB/s  vsq', round(d['k_predict_vsq_ms'],3), 'ms', round(d['k_predict_vsq_tflops'],1), 'TF')"
         continue
       fi
-      env $envs GPFIT_LIB=$PWD/gaussian-process_amd/libgpfit_$v.so timeout -k 10 300 python bench.py ${CFG[$c]} --steps ${STEPS:-8} --warmup 2 --no-cpu --pso-steps 0 --predict-points 0 --no-hull --psurf-rows 0 --no-secondary > $O/$tag.log 2>&1 || exit $?
+      env $envs GPFIT_LIB=$PWD/gaussian-process_amd/libgpfit_$v.so timeout -k 10 300 python bench.py ${CFG[$c]} --steps ${STEPS:-8} --warmup 2 --no-cpu --pso-steps 0 --predict-points 0 --no-hull --no-kmeans --psurf-rows 0 --no-secondary > $O/$tag.log 2>&1 || exit $?
       python -c "import json; d=json.loads(open('$O/$tag.log').read().strip().splitlines()[-1]); r=d['roofline']; print('$spec $c #$r', round(d['value'],1), 'evals/s  ', round(r['achieved'],2), 'TF', r['kernel'], 'sclk', r.get('box_sclk_mhz'), 'of ceiling', r.get('frac_of_box_ceiling'))"
     done
   done

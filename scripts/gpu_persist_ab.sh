@@ -7,7 +7,7 @@ timeout -k 10 900 python -u -m pytest tests/test_gpu.py -x -v -m gpu --timeout 3
 rc=$?
 grep -E "passed|failed|error" $O/pytest.log | tail -3
 [ $rc -ne 0 ] && { grep -E "FAILED|Error|assert" $O/pytest.log | head -30; exit $rc; }
-Q="--no-cpu --pso-steps 0 --predict-points 0 --no-hull --psurf-rows 0 --no-secondary"
+Q="--no-cpu --pso-steps 0 --predict-points 0 --no-hull --no-kmeans --psurf-rows 0 --no-secondary"
 for r in 1 2; do
   for v in 1 0; do
     GPF_PERSIST=$v timeout -k 10 300 python bench.py --steps ${STEPS:-40} --warmup 2 $Q > $O/C_${v}_${r}.log 2>&1 || exit 4

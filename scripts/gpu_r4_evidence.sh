@@ -23,12 +23,12 @@ p = d["predict"]
 print("predict", round(p["ms"], 3), "factor", round(p["factor_ms"], 3), "vsq", round(p["k_predict_vsq_ms"], 3))
 PY
 else
-  B="python bench.py --steps 3 --warmup 1 --pso-steps 0 --no-cpu --predict-points 0 --no-hull --psurf-rows 0 --no-secondary"
+  B="python bench.py --steps 3 --warmup 1 --pso-steps 0 --no-cpu --predict-points 0 --no-hull --no-kmeans --psurf-rows 0 --no-secondary"
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- $B > $O/prof.log 2>&1 || exit 4
   f=$(find $O/prof -name "*kernel_trace.csv" | head -1)
   python scripts/kernel_union.py $f 4096 64 3 > $O/kernel_union.txt 2>&1 || true
   python scripts/step_timeline.py $f 4096 > $O/timeline.txt 2>&1 || true
-  B2="python bench.py --steps 2 --warmup 1 --pso-steps 0 --no-profile --no-cpu --predict-points 0 --no-hull --psurf-rows 0 --no-secondary"
+  B2="python bench.py --steps 2 --warmup 1 --pso-steps 0 --no-profile --no-cpu --predict-points 0 --no-hull --no-kmeans --psurf-rows 0 --no-secondary"
   timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o f --output-format csv -- $B2 > $O/pmc_fetch.log 2>&1 || exit 5
   timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o w --output-format csv -- $B2 > $O/pmc_write.log 2>&1 || exit 5
   timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_mfma -o m --output-format csv -- $B2 > $O/pmc_mfma.log 2>&1 || exit 5

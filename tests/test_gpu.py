@@ -226,6 +226,41 @@ def test_pso_on_gpu_end_to_end(ctx, f4, k, capsys):
         assert pull_at_threshold(best, x, y, e, s), (ref_at_best, got_score)
 
 
+@pytest.mark.parametrize("n,d,k,dup", [(1024, 3, 100, 0), (4096, 3, 100, 0), (16384, 4, 100, 0), (600, 2, 100, 400),
+                                       (3000, 5, 37, 0)])
+def test_kmeans_fit_on_gpu_matches_sklearn(ctx, n, d, k, dup):
+    """The KMeans subsample's fit with the Lloyd E/M-steps on the GPU (gpf_kmeans_step,
+    gpfit.kmeans): labels equal to sklearn's KMeans(k, n_init='auto', random_state=0).fit (the
+    reference's call, find_len_scales.py:27-31), centres within 1e-12; duplicate points (empty
+    clusters relocated) included."""
+    from sklearn.cluster import KMeans
+    from gpfit.kmeans import kmeans_fit
+    rng = np.random.default_rng(n + d + k + dup)
+    X = rng.uniform(size=(n, d))
+    if dup:
+        X[-dup:] = X[:8][rng.integers(0, 8, size=dup)]
+    with _blas_threads():
+        km = KMeans(n_clusters=k, n_init="auto", random_state=0).fit(X)
+    labels, centres = kmeans_fit(ctx, X, k)
+    assert np.array_equal(labels, km.labels_)
+    np.testing.assert_allclose(centres, km.cluster_centers_, rtol=0, atol=1e-12)
+
+
+def test_kmeans_subsample_on_gpu_keeps_reference_points(ctx):
+    """F10 (the points the reference's len_scale_opt keeps at N = 300..4096, d = 2..4) through
+    prepare() with a GPU context, the product path of the drop-in's len_scale_opt: the same points
+    in the same order, and the same search box."""
+    from conftest import fixture_data, load_golden
+    from gpfit.swarm import prepare
+    f = load_golden("f10_kmeans.npz")
+    for i in range(int(f["ncases"])):
+        x, y, e = fixture_data(f[f"c{i}_meta"], f[f"c{i}_data_sha256"])
+        xs, ys, es, lo, hi, _, _ = prepare(np.asfortranarray(x), y, e, max_points=100, verbose=False, ctx=ctx)
+        idx = f[f"c{i}_idx"]
+        assert np.array_equal(xs, x[:, idx]) and np.array_equal(ys, y[idx]) and np.array_equal(es, e[idx])
+        assert np.array_equal(lo, f[f"c{i}_lo"]) and np.array_equal(hi, f[f"c{i}_hi"])
+
+
 def test_not_positive_definite_raises_like_numpy(ctx):
     x = np.array([[0.0, 1.0, 1.0, 2.0]])  # duplicate point, zero noise: K singular exactly
     y, e = np.array([0.1, 0.2, 0.2, 0.3]), np.zeros(4)

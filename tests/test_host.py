@@ -93,3 +93,57 @@ def test_kmeans_path_taken_above_max_points(capsys):
     particle_swarm(x, y, e, False, num_particles=4, max_iter=2, max_points=100, seed=0, evaluator=ev)
     assert "Subsampling to 100" in capsys.readouterr().out
     assert set(seen) == {100}
+
+
+class _NumpyKMeansSteps:
+    """Test stand-in for Context.kmeans_step (csrc/gpf_kmeans.hip's arithmetic in NumPy): lets the
+    host half of gpfit.kmeans — sklearn's Lloyd loop around the device steps — run without a GPU."""
+
+    def kmeans_set(self, X):
+        self.X = np.array(X, dtype=np.float64)
+
+    def kmeans_step(self, centers, update=True, want_dist=False):
+        X, C = self.X, np.asarray(centers, dtype=np.float64)
+        d2 = np.einsum("ij,ij->i", C, C)[None, :] + (-2.0 * (X @ C.T))
+        labels = np.argmin(d2, axis=1).astype(np.int32)
+        sums = counts = dist = None
+        if update:
+            k = C.shape[0]
+            sums = np.zeros_like(C)
+            np.add.at(sums, labels, X)
+            counts = np.bincount(labels, minlength=k).astype(np.float64)
+        if want_dist:
+            dist = np.sum((X - C[labels]) ** 2, axis=1)
+        return labels, sums, counts, dist
+
+
+@pytest.mark.parametrize("n,d,k,dup", [(300, 2, 100, 0), (1024, 3, 100, 0), (2000, 4, 50, 0), (500, 2, 100, 300),
+                                       (4096, 3, 100, 0)])
+def test_kmeans_fit_loop_matches_sklearn(n, d, k, dup):
+    """gpfit.kmeans.kmeans_fit (sklearn's seeding and Lloyd loop, the E/M-steps delegated — here to
+    a NumPy stand-in of the device steps): labels equal to sklearn's KMeans(k, n_init='auto',
+    random_state=0).fit, centres to rounding; with many duplicate points too (empty clusters get
+    relocated as sklearn's _relocate_empty_clusters_dense does)."""
+    from sklearn.cluster import KMeans
+    from gpfit.kmeans import kmeans_fit
+    rng = np.random.default_rng(n + d + k + dup)
+    X = rng.uniform(size=(n, d))
+    if dup:
+        X[-dup:] = X[:8][rng.integers(0, 8, size=dup)]
+    km = KMeans(n_clusters=k, n_init="auto", random_state=0).fit(X)
+    labels, centres = kmeans_fit(_NumpyKMeansSteps(), X, k)
+    assert np.array_equal(labels, km.labels_)
+    np.testing.assert_allclose(centres, km.cluster_centers_, rtol=0, atol=1e-12)
+
+
+def test_kmeans_fit_keeps_the_reference_points_f10():
+    """F10 (the points the reference's len_scale_opt keeps, N = 300..4096) through the GPU path's
+    host loop (NumPy stand-in for the device steps): the same points in the same order."""
+    from conftest import fixture_data, load_golden
+    from gpfit.kmeans import kmeans_representatives_gpu
+    f = load_golden("f10_kmeans.npz")
+    for i in range(int(f["ncases"])):
+        x, y, e = fixture_data(f[f"c{i}_meta"], f[f"c{i}_data_sha256"])
+        xs, ys, es = kmeans_representatives_gpu(_NumpyKMeansSteps(), _fx(x), y, e, 100)
+        idx = f[f"c{i}_idx"]
+        assert np.array_equal(xs, x[:, idx]) and np.array_equal(ys, y[idx]) and np.array_equal(es, e[idx])
