@@ -122,7 +122,7 @@ struct gpf_ctx {
   double *km_x = nullptr, *km_c = nullptr, *km_dist = nullptr, *km_sums = nullptr, *km_cnt = nullptr;
   int* km_lab = nullptr;
   int64_t km_n = 0;
-  int km_d = 0, km_kcap = 0;
+  int km_d = 0, km_kcap = 0, km_cd = 0;  // km_cd: the d the centre buffers were sized for
   // last convex-hull grid (gpf_hull_fill -> gpf_hull_fetch)
   std::vector<double> hull_rows;
   int hull_d = 0;
@@ -1368,7 +1368,7 @@ int gpf_kmeans_step(gpf_ctx* c, const double* centers, int k, int update, int* l
   if (k <= 0 || (int64_t)k * d > gpf::KM_MAXKD || !centers || !labels || (update && (!sums || !counts)))
     return bad_arg(c, "gpf_kmeans_step: bad arguments");
   hipSetDevice(c->device);
-  if (k > c->km_kcap) {
+  if (k > c->km_kcap || d != c->km_cd) {  // the centre buffers are k x d: both sizes matter
     GPF_HIP(c, hipStreamSynchronize(c->stream));
     hipFree(c->km_c); hipFree(c->km_sums); hipFree(c->km_cnt);
     c->km_c = c->km_sums = c->km_cnt = nullptr;
@@ -1377,6 +1377,7 @@ int gpf_kmeans_step(gpf_ctx* c, const double* centers, int k, int update, int* l
     GPF_HIP(c, hipMalloc(&c->km_sums, (size_t)k * d * 8));
     GPF_HIP(c, hipMalloc(&c->km_cnt, (size_t)k * 8));
     c->km_kcap = k;
+    c->km_cd = d;
   }
   const int64_t n = c->km_n;
   GPF_HIP(c, hipMemcpyAsync(c->km_c, centers, (size_t)k * d * 8, hipMemcpyHostToDevice, c->stream));

@@ -246,6 +246,24 @@ def test_kmeans_fit_on_gpu_matches_sklearn(ctx, n, d, k, dup):
     np.testing.assert_allclose(centres, km.cluster_centers_, rtol=0, atol=1e-12)
 
 
+def test_kmeans_step_buffers_follow_k_and_d(ctx):
+    """gpf_kmeans_step keeps its centre buffers between calls: a call with more dimensions at the
+    same or a smaller k, or more clusters, must resize them (a d-only change once overran them)."""
+    rng = np.random.default_rng(5)
+    for n, d, k in ((500, 2, 50), (700, 5, 50), (400, 3, 120), (300, 4, 10)):
+        X = rng.uniform(size=(n, d))
+        C = X[rng.choice(n, k, replace=False)]
+        ctx.kmeans_set(X)
+        labels, sums, counts, dist = ctx.kmeans_step(C, update=True, want_dist=True)
+        d2 = np.einsum("ij,ij->i", C, C)[None, :] - 2.0 * (X @ C.T)
+        assert np.array_equal(labels, np.argmin(d2, axis=1))
+        assert np.array_equal(counts, np.bincount(labels, minlength=k).astype(float))
+        ref = np.zeros((k, d))
+        np.add.at(ref, labels, X)
+        np.testing.assert_allclose(sums, ref, rtol=1e-13, atol=1e-13)
+        np.testing.assert_allclose(dist, np.sum((X - C[labels]) ** 2, axis=1), rtol=1e-13, atol=1e-15)
+
+
 def test_kmeans_subsample_on_gpu_keeps_reference_points(ctx):
     """F10 (the points the reference's len_scale_opt keeps at N = 300..4096, d = 2..4) through
     prepare() with a GPU context, the product path of the drop-in's len_scale_opt: the same points
