@@ -1089,6 +1089,13 @@ __device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, con
 // bitwise these sums with half the levels — measured slower: factor 3.45 -> 3.73 ms, the
 // carrier's three 128 KiB reads per level cost more than the saved hand-offs;
 // profiles/r3s2/ab_split_tree_radix.txt.)
+// GPF_TREE_SC1 (A/B build): the second arriver reads the sibling's node sum with sc1 loads (L1
+// bypassed, served by L2 / memory) instead of an agent-scope acquire (L1 invalidate) before plain
+// loads — MI355X_MICROARCH's sc1 hand-off form: sc1 payload stores drained by every wave, then one
+// lane's sc1 flag store behind a barrier; one lane's sc1 poll, a barrier, then every load sc1.
+#ifndef GPF_TREE_SC1
+#define GPF_TREE_SC1 0
+#endif
 constexpr int SPLIT_TREE = 80;              // tickets per split tile: pair (level l < 5, pair k < 16) at l * 16 + k
 constexpr int SPLIT_CNT = 2 * SPLIT_TREE;   // + the pairs' ready flags at SPLIT_TREE + l * 16 + k
 
@@ -1140,7 +1147,9 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
         __builtin_amdgcn_s_sleep(2);
       }
       if (!late) {
+#if !GPF_TREE_SC1
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
         __hip_atomic_store(rdy, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -1161,7 +1170,8 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           acc.v[mi][ni][r] = acc.v[mi][ni][r] + __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
-                                                                            rs, vo, 8 * ((mi * 16 + 4 * r) * T + ni * 16), 0));
+                                                                            rs, vo, 8 * ((mi * 16 + 4 * r) * T + ni * 16),
+                                                                            GPF_TREE_SC1 ? 16 : 0));
       if (mi & 1) __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -1289,7 +1299,9 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
                                        cnt + ti * SPLIT_CNT, lds, qd, sflag, info + p, spins,
                                        [&](Acc<T>& a) { cov_tile_acc(a, qd, x, lp, d, N, Jn, In, lds); }, J))
       return;
+    GPF_PHASE(0);
     acc.store(qd, lab + la_slot(p, J), T);
+    GPF_PHASE(1);
     return;
   }
 

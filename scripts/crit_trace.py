@@ -31,25 +31,38 @@ y = np.sin(2 * np.pi * x).sum(0) + 0.1 * rng.standard_normal(N)
 e = np.full(N, 0.1)
 
 
-def split_all_chunks(J, w, nt):  # mirrors gpf::split_all_chunks / split_all_pieces / split_all_target
+def split_la_bits(J, nt):  # mirrors split_la_bits (gpfit_api.hip; one group, GPF_SPLIT_LA)
+    if os.environ.get("GPF_SPLIT_LA", "0") == "0" or nt < 4:
+        return 0
+    return (1 if 1 <= J <= nt - 3 else 0) | (2 if 2 <= J <= nt - 2 else 0)
+
+
+def split_all_chunks(J, w, nt, la=0):  # mirrors gpf::split_all_chunks / split_all_pieces / split_all_target
+    if w == nt - 1:
+        return J * 8 if la & 1 else 0
+    if w == 0 and la & 2:
+        return 8
     nL = nt - 1 - J
     return (J if w < nL else J - (w - nL)) * 8
 
 
-def split_all_pieces(J, w, nt, tgt):
-    c = split_all_chunks(J, w, nt)
+def split_all_pieces(J, w, nt, tgt, la=0):
+    if w == 0 and la & 2:
+        return 1
+    c = split_all_chunks(J, w, nt, la)
     return min(32, 1 if c <= 0 else -(-c // tgt))
 
 
-def split_all_target(pc, nt, J):
+def split_all_target(pc, nt, J, la=0):
     budget = max(1, int(os.environ.get("GPF_SPLIT_K_SLOTS", 256)) - pc)
     minch = int(os.environ.get("GPF_SPLIT_K_MINCH", 4))
-    tot = sum(split_all_chunks(J, w, nt) for w in range(nt - 1))
+    wl = nt if la & 1 else nt - 1
+    tot = sum(split_all_chunks(J, w, nt, la) for w in range(wl))
     cap = max(1, J * 8)
     lo, hi = min(cap, max(minch, -(-pc * tot // budget))), cap
     while lo < hi:
         m = (lo + hi) // 2
-        if pc * sum(split_all_pieces(J, w, nt, m) for w in range(nt - 1)) <= budget:
+        if pc * sum(split_all_pieces(J, w, nt, m, la) for w in range(wl)) <= budget:
             hi = m
         else:
             lo = m + 1
@@ -94,8 +107,21 @@ for J in range(nt - 1):
     # 1 .. nt-2 without the all-tile split, P SYRK workgroups (deferred diagonal update)
     ed = P if plan["diag_workgroups"] > 0 else 0
     if mode == "predict":  # balanced all-tile split: tile w = 0's pieces right after the diagonal workgroup
-        np0 = split_all_pieces(J, 0, nt, split_all_target(P, nt, J))
+        la = split_la_bits(J, nt)
+        tgt = split_all_target(P, nt, J, la)
+        np0 = split_all_pieces(J, 0, nt, tgt, la)
         ids = [b for b in range(ed, ed + np0 * P, P) if live[b]]
+        if la & 1:  # the look-ahead pieces (virtual tile w = nt-1) after every real tile
+            o = ed + P * sum(split_all_pieces(J, w, nt, tgt, la) for w in range(nt - 1))
+            lids = [b for b in range(o, o + P * split_all_pieces(J, nt - 1, nt, tgt, la), P) if live[b]]
+            if lids:
+                p0 = ph[J].astype(np.int64)
+                print(f"   la: {len(lids)} pieces, gemm-only max {(max(p0[b, 3] for b in lids) - t0) * 1e-2:6.1f}"
+                      f"  end max {(max(en[b] for b in lids) - t0) * 1e-2:6.1f}  (target {tgt} chunks)")
+                if os.environ.get("LA_DETAIL"):
+                    r = lambda v: (v - t0) * 1e-2 if v >= t0 else float("nan")  # noqa: E731
+                    print("      " + "  ".join(f"[{b}: {r(st[b]):.1f} {r(p0[b, 3]):.1f} {r(p0[b, 0]):.1f} {r(p0[b, 1]):.1f} "
+                                              f"{r(en[b]):.1f} hw{int(tr[J, b, 2]):x}]" for b in lids))
     else:  # critical-tile split (csrc/gpfit_api.hip split_crit, off by default): pieces at b = off + s * P
         off = ed + (P if (plan["syrk_workgroups"] > 0 and 1 <= J <= nt - 2) else 0)
         # r4 reordered dispatch (GPF_REORDER, default on): light U tiles, SYRK, diagonal, then w = 0
