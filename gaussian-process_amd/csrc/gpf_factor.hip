@@ -1093,6 +1093,12 @@ __device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, con
 // bypassed, served by L2 / memory) instead of an agent-scope acquire (L1 invalidate) before plain
 // loads — MI355X_MICROARCH's sc1 hand-off form: sc1 payload stores drained by every wave, then one
 // lane's sc1 flag store behind a barrier; one lane's sc1 poll, a barrier, then every load sc1.
+#ifndef GPF_SEED_CH
+#define GPF_SEED_CH 0  // (A/B build switch) split_part: chunks of GEMM piece 0's covariance seed stands for
+#endif
+#ifndef GPF_TREE_NATIVE
+#define GPF_TREE_NATIVE 0  // (A/B build switch) split_part node sums in a register-native layout, 16-B accesses
+#endif
 #ifndef GPF_TREE_SC1
 #define GPF_TREE_SC1 0
 #endif
@@ -1103,7 +1109,11 @@ template <bool NN, bool NEG, bool SEEDED = false, typename Seed>
 __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int lda, const double* Bp, int ldb, int nch, int S,
                            int s, double* __restrict__ pt, unsigned* __restrict__ ct, double* smem,
                            const Quad<T>& qd, int* flag, int* info, int spins, Seed seed, int J) {
-  const int c0 = s * nch / S, c1 = (s + 1) * nch / S;
+  // piece boundaries over nch + e chunks, the first e of them standing for piece 0's seed (its
+  // covariance tile costs about GPF_SEED_CH chunks of GEMM), so that the seeded piece — the carrier
+  // of every tree level it reaches — ends its GEMM with the others
+  const int e = SEEDED ? GPF_SEED_CH : 0;
+  const int c0 = s == 0 ? 0 : max(0, s * (nch + e) / S - e), c1 = max(0, (s + 1) * (nch + e) / S - e);
   if (SEEDED && s == 0)
     seed(acc);
   else
@@ -1129,7 +1139,29 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
     if (threadIdx.x == 0) *flag = (int)__hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (*flag == 0) {  // first: publish the node sum, then the sibling carries the pair on
+#if GPF_TREE_NATIVE
+      {  // register-native slot layout: 16-B write-through stores, 1 KiB per wave instruction
+        const auto ws = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(pt + (size_t)(c << l) * T * T), 0,
+                                                          T * T * 8, 0x00020000);
+        const int wb = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (Acc<T>::MBR * Acc<T>::MBC * 2048);
+#pragma unroll
+        for (int mi = 0; mi < Acc<T>::MBR; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < Acc<T>::MBC; ++ni)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const double a0 = acc.v[mi][ni][2 * h], a1 = acc.v[mi][ni][2 * h + 1];
+              const unsigned long long u0 = __builtin_bit_cast(unsigned long long, a0),
+                                       u1 = __builtin_bit_cast(unsigned long long, a1);
+              const __attribute__((ext_vector_type(4))) unsigned q4 = {(unsigned)u0, (unsigned)(u0 >> 32),
+                                                                        (unsigned)u1, (unsigned)(u1 >> 32)};
+              __builtin_amdgcn_raw_buffer_store_b128(q4, ws, qd.lane * 16, wb + ((mi * Acc<T>::MBC + ni) * 2 + h) * 1024,
+                                                     16);  // sc1: write-through
+            }
+      }
+#else
       acc.store_wt(qd, pt + (size_t)(c << l) * T * T, T);
+#endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its part of the node sum
       __syncthreads();
       if (threadIdx.x == 0) __hip_atomic_store(rdy, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1162,6 +1194,28 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
     // loop and spilled)
     const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(pt + (size_t)(sib << l) * T * T), 0, T * T * 8,
                                                       0x00020000);
+#if GPF_TREE_NATIVE
+    {
+      const int wb = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (Acc<T>::MBR * Acc<T>::MBC * 2048);
+#pragma unroll
+      for (int mi = 0; mi < Acc<T>::MBR; ++mi) {
+#pragma unroll
+        for (int ni = 0; ni < Acc<T>::MBC; ++ni)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const auto q4 = __builtin_amdgcn_raw_buffer_load_b128(rs, qd.lane * 16,
+                                                                  wb + ((mi * Acc<T>::MBC + ni) * 2 + h) * 1024,
+                                                                  GPF_TREE_SC1 ? 16 : 0);
+            const unsigned long long u0 = (unsigned long long)q4[0] | ((unsigned long long)q4[1] << 32),
+                                     u1 = (unsigned long long)q4[2] | ((unsigned long long)q4[3] << 32);
+            acc.v[mi][ni][2 * h] = acc.v[mi][ni][2 * h] + __builtin_bit_cast(double, u0);
+            acc.v[mi][ni][2 * h + 1] = acc.v[mi][ni][2 * h + 1] + __builtin_bit_cast(double, u1);
+          }
+        if (mi & 1) __builtin_amdgcn_sched_barrier(0);
+      }
+      continue;
+    }
+#endif
     const int vo = 8 * ((qd.rb + (qd.lane >> 4)) * T + qd.cb + (qd.lane & 15));
 #pragma unroll
     for (int mi = 0; mi < Acc<T>::MBR; ++mi) {
