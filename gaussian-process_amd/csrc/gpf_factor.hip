@@ -861,26 +861,14 @@ enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2, ROLE_DIAG = 3, ROLE_SYRK =
 // pieces per tile (which gave the deepest tiles the longest pieces: the critical tile's GEMM, not
 // the diagonal factor, ended the launch). At most SPLIT_MAXS pieces (the reduction tree's bound).
 constexpr int SPLIT_MAXS = 32;
-// la (r4, the split look-ahead; gpf::step_decode): bit 0 — the launch also runs, as pieces of a
-// virtual tile w = nt-1, the next launch's critical tile (J+1, J+2) over the columns < J; bit 1 —
-// its own critical tile (w = 0) was run that way by the previous launch and is one workgroup over
-// its last block column.
-__host__ __device__ __forceinline__ int split_all_chunks(int J, int w, int nt, int la = 0) {
-  if (w == nt - 1) return (la & 1) ? J * (T / DL_KC) : 0;  // the look-ahead pieces
-  if (w == 0 && (la & 2)) return T / DL_KC;                // the seeded critical tile: one block
+__host__ __device__ __forceinline__ int split_all_chunks(int J, int w, int nt) {
   const int nL = nt - 1 - J;
   return (w < nL ? J : J - (w - nL)) * (T / DL_KC);  // L tile: depth 128J; U tile K: 128(J-K)
 }
-__host__ __device__ __forceinline__ int split_all_pieces(int J, int w, int nt, int tgt, int la = 0) {
-  if (w == 0 && (la & 2)) return 1;
-  const int ch = split_all_chunks(J, w, nt, la);
+__host__ __device__ __forceinline__ int split_all_pieces(int J, int w, int nt, int tgt) {
+  const int ch = split_all_chunks(J, w, nt);
   const int s = ch <= 0 ? 1 : (ch + tgt - 1) / tgt;
   return s > SPLIT_MAXS ? SPLIT_MAXS : s;
-}
-// split-K slot (partials, counters) of tile w of particle p in a launch of P particles: the
-// look-ahead pieces' virtual tile after every real one
-__host__ __device__ __forceinline__ size_t split_tile_slot(int p, int w, int P, int nt) {
-  return w == nt - 1 ? (size_t)P * (nt - 1) + p : (size_t)p * (nt - 1) + w;
 }
 
 // Workgroup b of a k_step<SPLIT> launch (grid: [P diagonal workgroups if ed] + [P SYRK workgroups
@@ -935,7 +923,7 @@ __host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt,
     }
     b -= P;
   }
-  if (SPLIT == SPLIT_NONE && la) {  // (under SPLIT_ALL, la carries the split look-ahead bits)
+  if (la) {
     if (b < P) {
       p = b;
       w = -1;
@@ -943,15 +931,14 @@ __host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt,
     }
     b -= P;
   }
-  if (SPLIT == SPLIT_ALL) {  // S: chunks per piece; la: the split look-ahead bits (split_all_chunks)
+  if (SPLIT == SPLIT_ALL) {  // S: chunks per piece
     int np = 1;
-    const int wl = (la & 1) ? nt - 1 : nt - 2;  // the last tile (nt-1: the look-ahead pieces)
-    for (w = 0; w < wl; ++w) {
-      np = split_all_pieces(J, w, nt, S, la);
+    for (w = 0; w < nt - 2; ++w) {
+      np = split_all_pieces(J, w, nt, S);
       if (b < P * np) break;
       b -= P * np;
     }
-    if (w == wl) np = split_all_pieces(J, w, nt, S, la);
+    if (w == nt - 2) np = split_all_pieces(J, w, nt, S);
     p = b % P;
     sidx = b / P;  // (< np for every dispatched workgroup: gpf_plan_check)
     return np > 1 ? ROLE_PIECE : ROLE_WHOLE;
@@ -1325,7 +1312,7 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
                                           const double* __restrict__ ls, int d, int S, int S2, int sidx,
                                           double* __restrict__ part, unsigned* __restrict__ cnt, int* sflag,
                                           const int* __restrict__ dflag, const int* __restrict__ yflag, int defer,
-                                          int spins, int la, double* __restrict__ lab, double* lds, int P) {
+                                          int spins, int la, const double* __restrict__ lab, double* lds) {
   const int tid = threadIdx.x;
   const int nL = nt - 1 - J;
   const size_t ld = (size_t)Npad;
@@ -1337,27 +1324,6 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
   const int g = qd.lane >> 4, cl = qd.lane & 15;
   const double* Ujj = Up + (size_t)J * T * ld + (size_t)J * T;
   double* zj = lds + STEP_ZJ;  // z_J (128), written by the diagonal factor of block J
-
-  if (SPLIT == SPLIT_ALL && (la & 1) && w == nt - 1) {
-    // (r4) split look-ahead: a piece of the next launch's critical tile (J+1, J+2) over the columns
-    // < J (final before this launch), the covariance seed in piece 0, the pieces' own reduction tree
-    // here, off the next launch's chain; the tree's last workgroup leaves the sum in slot J & 1 of
-    // the particle (plain stores: read after the launch boundary), which the next launch's critical
-    // tile loads and finishes with its last 128-deep block
-    const int Jn = J + 1, In = J + 2;
-    const double* lp = ls + (size_t)p * d;
-    const size_t ti = split_tile_slot(p, w, P, nt);
-    Acc<T> acc;
-    if (!split_part<false, true, true>(acc, Lp + (size_t)Jn * T * ld, Npad, Lp + (size_t)In * T * ld, Npad,
-                                       J * T / DL_KC, split_all_pieces(J, w, nt, S, la), sidx, part + ti * S2 * T * T,
-                                       cnt + ti * SPLIT_CNT, lds, qd, sflag, info + p, spins,
-                                       [&](Acc<T>& a) { cov_tile_acc(a, qd, x, lp, d, N, Jn, In, lds); }, J))
-      return;
-    GPF_PHASE(0);
-    acc.store(qd, lab + la_slot(p, J), T);
-    GPF_PHASE(1);
-    return;
-  }
 
   if (w < nL) {
     const int I = J + 1 + w;
@@ -1372,18 +1338,12 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
       // its partial with the covariance tile (the unsplit path's accumulator seed)
       // (S2 partial slots per tile; the all-tile split's pieces per tile from the chunk target S)
       double* pt = part + (size_t)(p * (nt - 1) + w) * S2 * T * T;
-      const int Sx = SPLIT == SPLIT_ALL ? split_all_pieces(J, w, nt, S, la & 3) : S;
+      const int Sx = SPLIT == SPLIT_ALL ? split_all_pieces(J, w, nt, S) : S;
       if (!split_part<false, true, true>(acc, Lp + (size_t)J * T * ld, Npad, Lp + (size_t)I * T * ld, Npad,
                                          J * T / DL_KC, Sx, sidx, pt, cnt + (size_t)(p * (nt - 1) + w) * SPLIT_CNT, lds,
                                          qd, sflag, info + p, spins,
                                          [&](Acc<T>& a) { cov_tile_acc(a, qd, x, lp, d, N, J, I, lds); }, J))
         return;  // (the finisher's accumulators hold D)
-    } else if (SPLIT == SPLIT_ALL && (la & 2) && I == J + 1) {
-      // (r4) split look-ahead seed: launch J-1's pieces left this tile's GEMM over the columns < J-1
-      // (covariance seed included, reduced by their tree); the last block column follows
-      acc.load(qd, lab + la_slot(p, J - 1), T);
-      gemm_stream_dl<false, true>(acc, Lp + (size_t)J * T * ld + (size_t)(J - 1) * T, Npad,
-                                  Lp + (size_t)I * T * ld + (size_t)(J - 1) * T, Npad, T, lds, qd);
     } else if (SPLIT == SPLIT_NONE && ED && (la & 2) && I == J + 1) {
       // look-ahead seed: launch J-1 left this tile's GEMM over its first la_chunks(J-1) chunks (cov
       // seed included); the rest follows — the same MFMAs in the same order
@@ -1454,7 +1414,7 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
     // W = L_J,[K,J) U_[K,J),K (U_KK is lower triangular: the wave's first chunks add zeros)
     if (SPLIT == SPLIT_ALL && role == ROLE_PIECE) {  // split-K (the triangular first block runs dense: its upper part holds zeros)
       double* pt = part + (size_t)(p * (nt - 1) + w) * S2 * T * T;
-      const int Sx = split_all_pieces(J, w, nt, S, la & 3);
+      const int Sx = split_all_pieces(J, w, nt, S);
       if (!split_part<true, false, false>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
                                           Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T / DL_KC, Sx, sidx,
                                           pt, cnt + (size_t)(p * (nt - 1) + w) * SPLIT_CNT, lds, qd, sflag, info + p,
@@ -1547,8 +1507,8 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
   if (la & 8) __builtin_amdgcn_s_setprio(2);
   int p, w, sidx;
   const int role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, SPLIT != SPLIT_ALL && sy,
-                                      SPLIT == SPLIT_ALL ? (la & 3) : (SPLIT == SPLIT_NONE && ED && (la & 1) && !sy),
-                                      p, w, sidx, SPLIT == SPLIT_NONE && ED && (la & 32) != 0);
+                                      SPLIT == SPLIT_NONE && ED && (la & 1) && !sy, p, w, sidx,
+                                      SPLIT == SPLIT_NONE && ED && (la & 32) != 0);
 #ifdef GPF_CHECK
   // diagnostic build (-DGPF_CHECK): every index the workgroup derives its addresses from, checked
   // against the launch's extents before any access (an out-of-range role prints and does nothing)
@@ -1558,10 +1518,9 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
     else if (role == ROLE_LA) ok = ok && w == -1 && J >= 1 && J + 2 < nt && lab != nullptr;
     else if (role == ROLE_DIAG) ok = ok && w == -1 && ED && dflag != nullptr;
     else if (role != ROLE_IDLE) ok = ok && w >= 0 && w < nt - 1 && sidx >= 0 &&
-                                     sidx < (SPLIT == SPLIT_ALL ? split_all_pieces(J, w, nt, S, la & 3) : S) && sidx < S2 &&
+                                     sidx < (SPLIT == SPLIT_ALL ? split_all_pieces(J, w, nt, S) : S) && sidx < S2 &&
                                      (role != ROLE_PIECE || (part != nullptr && cnt != nullptr && S > 1)) &&
-                                     (w >= nt - 1 - J || J + 1 + w < nt) &&
-                                     (w < nt - 1 - J || w - (nt - 1 - J) < J || (SPLIT == SPLIT_ALL && (la & 1) && w == nt - 1));
+                                     (w >= nt - 1 - J || J + 1 + w < nt) && (w < nt - 1 - J || w - (nt - 1 - J) < J);
     if (!ok) {
       if (tid == 0)
         printf("k_step check: J=%d block %d role %d p=%d w=%d sidx=%d (P=%d nt=%d S=%d)\n", J, (int)blockIdx.x, role,
@@ -1597,7 +1556,7 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
                     carve_diag(lds, lds + DIAG_BASE), J * T + H >= N, dflag + p, J);
   } else {
     step_item<SPLIT, ED>(role, J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, S2, sidx, part, cnt, &sflag,
-                         dflag, yflag, defer, spins, la, lab, lds, P);
+                         dflag, yflag, defer, spins, la, lab, lds);
   }
   span.stop(clk);
 #ifdef GPF_WG_TRACE

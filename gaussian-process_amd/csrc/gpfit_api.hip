@@ -376,31 +376,17 @@ static int split_k(int tiles, int nt) {
 // the same piece count, so the deepest tiles — the critical tile I = J+1 among them — had the
 // longest pieces and, from J ~ 10 on, ended the launch after the diagonal factor.
 // GPF_SPLIT_K_SLOTS overrides the workgroup budget (256).
-// Split look-ahead (r4; gpf::split_all_chunks la bits) of launch J of a one-group all-tile-split
-// factorisation (the single-particle prediction): launch J (1 <= J <= nt-3) also runs the next
-// critical tile over the columns < J as pieces with their own reduction tree, and launch J
-// (2 <= J <= nt-2) finishes its critical tile from that sum with one 128-deep block — the
-// critical tile's pieces and tree leave the launch's chain (profiles/r4/crit_predict_r4.txt: from
-// J ~ 4 the launch waited for them). GPF_SPLIT_LA = 1 turns it on (opt-in until measured).
-static int split_la_bits(int J, int nt, int ng) {
-  bool on = false;
-  if (const char* e = getenv("GPF_SPLIT_LA")) on = atoi(e) != 0;
-  if (!on || ng != 1 || nt < 4) return 0;
-  return ((J >= 1 && J <= nt - 3) ? 1 : 0) | ((J >= 2 && J <= nt - 2) ? 2 : 0);
-}
-
-static int split_all_target(int pc, int nt, int J, int la = 0) {
+static int split_all_target(int pc, int nt, int J) {
   int slots = 256, minch = 4;
   if (const char* e = getenv("GPF_SPLIT_K_SLOTS")) slots = std::max(1, atoi(e));
   if (const char* e = getenv("GPF_SPLIT_K_MINCH")) minch = std::max(1, atoi(e));
   const int budget = std::max(1, slots - pc);
-  const int wl = (la & 1) ? nt : nt - 1;  // tiles, the look-ahead pieces' virtual tile included
   long long tot = 0;
-  for (int w = 0; w < wl; ++w) tot += gpf::split_all_chunks(J, w, nt, la);
+  for (int w = 0; w < nt - 1; ++w) tot += gpf::split_all_chunks(J, w, nt);
   const int cap = std::max(1, J * T / gpf::DL_KC);  // every tile in one piece from here on
   auto wgs = [&](int tgt) {
     long long n = 0;
-    for (int w = 0; w < wl; ++w) n += gpf::split_all_pieces(J, w, nt, tgt, la);
+    for (int w = 0; w < nt - 1; ++w) n += gpf::split_all_pieces(J, w, nt, tgt);
     return pc * n;
   };
   // smallest target >= the even share whose pieces fit the budget (the count falls with tgt)
@@ -532,9 +518,8 @@ static void split_sizes(int pc, int nt, int& S, int& Smax) {
     for (int g = 0; g < ng; ++g) {  // (the target depends on the group's particle count)
       const int gc = (int)((long long)pc * (g + 1) / ng) - (int)((long long)pc * g / ng);
       for (int J = 1; J < nt; ++J) {
-        const int la = split_la_bits(J, nt, ng);
-        const int tgt = split_all_target(gc, nt, J, la);
-        for (int w = 0; w < ((la & 1) ? nt : nt - 1); ++w) Smax = std::max(Smax, gpf::split_all_pieces(J, w, nt, tgt, la));
+        const int tgt = split_all_target(gc, nt, J);
+        for (int w = 0; w < nt - 1; ++w) Smax = std::max(Smax, gpf::split_all_pieces(J, w, nt, tgt));
       }
     }
     Smax = std::max(Smax, 2);
@@ -544,9 +529,7 @@ static void split_sizes(int pc, int nt, int& S, int& Smax) {
 
 static int split_plan(gpf_ctx* c, int pc, int& S, int& Smax) {
   split_sizes(pc, c->nt, S, Smax);
-  // (the split look-ahead's virtual tile: one more slot set per particle, gpf::split_tile_slot)
-  const bool sla = S > 1 && split_la_bits(1, c->nt, num_groups(pc, c->nt)) != 0;
-  return Smax > 1 ? ensure_split(c, pc * (c->nt - 1) + (sla ? pc : 0), Smax) : GPF_OK;
+  return Smax > 1 ? ensure_split(c, pc * (c->nt - 1), Smax) : GPF_OK;
 }
 
 // One k_step launch of a factorisation: block column J of particle group g (particles
@@ -588,19 +571,13 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
       const bool prev_none = J >= 1 && (S > 1 ? false : split_crit(pc, nt, J - 1, l.grp, S) <= 1);
       const bool next_none = S > 1 ? false : split_crit(pc, nt, J + 1, l.grp, S) <= 1;
       l.la = ((la_ok && next_none && J >= 1 && J <= nt - 3) ? 1 : 0) | ((la_ok && prev_none && J >= 2 && J <= nt - 2) ? 2 : 0);
-      if (S > 1) {  // the split look-ahead (split_la_bits) under the all-tile split
-        l.la = split_la_bits(J, nt, ng);
-        l.S = split_all_target(l.gc, nt, J, l.la);
-      }
       // reordered dispatch: only where the first 3 gc workgroups (the light U tiles, which wait for
       // the diagonal workgroups behind them, and the SYRK workgroups) fit the chip's CUs at once
       l.ro = (reorder_on() && l.ed && l.sy && l.split == gpf::SPLIT_NONE && l.grp == 0 && J >= 1 && 3 * l.gc <= 256) ? 1 : 0;
       int nall = 0;
-      for (int w = 0; S > 1 && w < ((l.la & 1) ? nt : nt - 1); ++w) nall += gpf::split_all_pieces(J, w, nt, l.S, l.la);
+      for (int w = 0; S > 1 && w < nt - 1; ++w) nall += gpf::split_all_pieces(J, w, nt, l.S);
       l.grid = (S > 1 ? l.gc * nall : l.gc * (nt - 1) + l.gc * (Sc - 1)) + (l.ed ? l.gc : 0) + (l.sy ? l.gc : 0) +
-               ((l.la & 1) && !l.sy && l.split == gpf::SPLIT_NONE ? l.gc : 0);  // (with SYRK workgroups the
-                                                                                // look-ahead rides on them; under
-                                                                                // the all-tile split it is pieces)
+               ((l.la & 1) && !l.sy ? l.gc : 0);  // (with SYRK workgroups the look-ahead rides on them)
       // one set of partial slots per group: groups run concurrently
       l.part_off = (size_t)l.p0 * (nt - 1) * Smax * T * T;
       l.cnt_off = (size_t)l.p0 * (nt - 1) * gpf::SPLIT_CNT;
@@ -648,10 +625,7 @@ static int run_factor(gpf_ctx* c, int pc, hipEvent_t* after = nullptr) {
   // finishing pieces re-zero what they used, but a hand-off that timed out (info bit 2) leaves its
   // pair's ticket and flag set, and the next tree would elect the wrong finisher;
   // ~20 KB at N=4096 for one particle, on c->stream ahead of the fork
-  if (Smax > 1)
-    GPF_HIP(c, hipMemsetAsync(c->d_cnt, 0,
-                              (size_t)(pc * (nt - 1) + (S > 1 && split_la_bits(1, nt, ng) ? pc : 0)) * gpf::SPLIT_CNT * 4,
-                              c->stream));
+  if (Smax > 1) GPF_HIP(c, hipMemsetAsync(c->d_cnt, 0, (size_t)pc * (nt - 1) * gpf::SPLIT_CNT * 4, c->stream));
   hipEvent_t wa = nullptr, wb = nullptr;
   if (c->prof) {
     wa = take_event(c);
@@ -1571,10 +1545,8 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
   std::vector<StepLaunch> plan;
   step_plan(pc, nt, S, Smax, plan);
   const int ntl = nt - 1, ng = num_groups(pc, nt);
-  // (split_plan's buffers: one more slot set per particle for the split look-ahead's virtual tile)
-  const size_t slot_sets = (size_t)pc * ntl + ((S > 1 && split_la_bits(1, nt, ng)) ? pc : 0);
-  const size_t part_cap = Smax > 1 ? slot_sets * Smax * T * T : 0;
-  const size_t cnt_cap = Smax > 1 ? slot_sets * gpf::SPLIT_CNT : 0;
+  const size_t part_cap = Smax > 1 ? (size_t)pc * ntl * Smax * T * T : 0;
+  const size_t cnt_cap = Smax > 1 ? (size_t)pc * ntl * gpf::SPLIT_CNT : 0;
   // partial-slot and counter ranges each group touches: groups run concurrently, so they must
   // be disjoint (within a group the launches are ordered on its stream)
   std::vector<size_t> plo(MAX_GROUPS, SIZE_MAX), phi(MAX_GROUPS, 0), clo(MAX_GROUPS, SIZE_MAX), chi(MAX_GROUPS, 0);
@@ -1596,13 +1568,11 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     if ((l.la & 2) && (l.la & 1) && gpf::la_slot(0, l.J - 1) == gpf::la_slot(0, l.J))
       return plan_fail(msg, msg_len, "J=%d g=%d: look-ahead reads and writes the same slot", l.J, l.g);
     const int tiles = l.gc * ntl;
-    const int sla = l.split == gpf::SPLIT_ALL ? (l.la & 3) : 0;  // the split look-ahead bits
-    const int ntw = ntl + ((sla & 1) ? 1 : 0);                    // tiles per particle, its virtual tile included
-    auto pieces_of = [&](int w) { return l.split == gpf::SPLIT_ALL ? gpf::split_all_pieces(l.J, w, nt, l.S, sla) : l.S; };
-    for (int w = 0; w < ntw; ++w)
+    auto pieces_of = [&](int w) { return l.split == gpf::SPLIT_ALL ? gpf::split_all_pieces(l.J, w, nt, l.S) : l.S; };
+    for (int w = 0; w < ntl; ++w)
       if (pieces_of(w) > l.S2) return plan_fail(msg, msg_len, "J=%d tile %d: %d pieces but %d slots", l.J, w, pieces_of(w), l.S2);
-    whole.assign((size_t)tiles + l.gc, 0);
-    piece.assign(((size_t)tiles + l.gc) * l.S2, 0);
+    whole.assign((size_t)tiles, 0);
+    piece.assign((size_t)tiles * l.S2, 0);
     diag.assign((size_t)l.gc, 0);
     syrk.assign((size_t)l.gc, 0);
     if (l.sy && (!l.defer || l.J < 1 || l.J > nt - 2 || l.split == gpf::SPLIT_ALL))
@@ -1611,9 +1581,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
       return plan_fail(msg, msg_len, "J=%d: deferred diagonal update under the all-tile split", l.J);
     // look-ahead: LA workgroups only where a next critical tile exists, no split, early diagonal
     // factor; a seeded launch follows a launch of the same group that ran them
-    // (the all-tile split: its own look-ahead, pieces of the next critical tile, one group only)
-    if (l.la && ((l.split != gpf::SPLIT_NONE && !(l.split == gpf::SPLIT_ALL && ng == 1)) ||
-                 (l.split == gpf::SPLIT_NONE && !l.ed) || ((l.la & 1) && (l.J < 1 || l.J > nt - 3)) ||
+    if (l.la && (l.split != gpf::SPLIT_NONE || !l.ed || ((l.la & 1) && (l.J < 1 || l.J > nt - 3)) ||
                  ((l.la & 2) && (l.J < 2 || l.J > nt - 2 || !(la_prev[l.g] & 1)))))
       return plan_fail(msg, msg_len, "J=%d g=%d: look-ahead bits %d out of place", l.J, l.g, l.la);
     if ((la_prev[l.g] & 1) && !(l.la & 2))
@@ -1626,7 +1594,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     for (unsigned b = 0; b < l.grid; ++b) {
       int p = -1, w = -1, sidx = -1;
       const int role =
-          l.split == gpf::SPLIT_ALL    ? gpf::step_decode<gpf::SPLIT_ALL>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, 0, sla, p, w, sidx)
+          l.split == gpf::SPLIT_ALL    ? gpf::step_decode<gpf::SPLIT_ALL>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, 0, 0, p, w, sidx)
           : l.split == gpf::SPLIT_CRIT ? gpf::step_decode<gpf::SPLIT_CRIT>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.sy, 0, p, w, sidx)
                                        : gpf::step_decode<gpf::SPLIT_NONE>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.sy,
                                                                            (l.la & 1) && !l.sy, p, w, sidx, l.ro);
@@ -1638,8 +1606,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
         continue;
       }
       if (role == gpf::ROLE_LA) {  // one per particle, right behind the diagonal and SYRK workgroups
-        if (!(l.la & 1) || l.sy || l.split != gpf::SPLIT_NONE || p < 0 || p >= l.gc ||
-            (unsigned)p + (l.ed ? l.gc : 0) != b || lawg[p]++)
+        if (!(l.la & 1) || l.sy || p < 0 || p >= l.gc || (unsigned)p + (l.ed ? l.gc : 0) != b || lawg[p]++)
           return plan_fail(msg, msg_len, "J=%d block %u: misplaced or duplicate look-ahead workgroup (p=%d)", l.J, b, p);
         ++wgs;
         continue;
@@ -1650,9 +1617,9 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
         ++wgs;
         continue;
       }
-      if (p < 0 || p >= l.gc || w < 0 || w >= ntw || sidx < 0 || sidx >= pieces_of(w))
+      if (p < 0 || p >= l.gc || w < 0 || w >= ntl || sidx < 0 || sidx >= pieces_of(w))
         return plan_fail(msg, msg_len, "J=%d block %u decodes out of range (p=%d w=%d)", l.J, b, p, w);
-      const int t = (int)gpf::split_tile_slot(p, w, l.gc, nt);  // (the virtual tile: after every real one)
+      const int t = p * ntl + w;
       if (role == gpf::ROLE_WHOLE) {
         ++whole[t];
       } else if (role == gpf::ROLE_PIECE) {
@@ -1680,7 +1647,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
       if (diag[q] != l.ed) return plan_fail(msg, msg_len, "J=%d particle %d: %d diagonal workgroups", l.J, q, diag[q]);
       diag_wgs += diag[q];
       if (syrk[q] != l.sy) return plan_fail(msg, msg_len, "J=%d particle %d: %d SYRK workgroups", l.J, q, syrk[q]);
-      if (lawg[q] != ((l.la & 1) && !l.sy && l.split == gpf::SPLIT_NONE ? 1 : 0))
+      if (lawg[q] != ((l.la & 1) && !l.sy ? 1 : 0))
         return plan_fail(msg, msg_len, "J=%d particle %d: %d look-ahead workgroups", l.J, q, lawg[q]);
       syrk_wgs += syrk[q];
     }
@@ -1693,14 +1660,6 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
       if (whole[t] == 1 && np == 0) ++whole_tiles;
       else if (whole[t] == 0 && np == pieces_of(t % ntl)) ++split_tiles;  // S arrivals on a zeroed counter: one finisher
       else return plan_fail(msg, msg_len, "J=%d tile %d: %d whole runs and %d pieces", l.J, t, whole[t], np);
-    }
-    for (int q = 0; (sla & 1) && q < l.gc; ++q) {  // the look-ahead pieces: all of them, once (or one whole)
-      const int t = tiles + q;
-      int np = 0;
-      for (int s = 0; s < l.S2; ++s) np += piece[(size_t)t * l.S2 + s] == 1 ? 1 : (piece[(size_t)t * l.S2 + s] ? 99 : 0);
-      if (!((whole[t] == 1 && np == 0) || (whole[t] == 0 && np == pieces_of(ntl))))
-        return plan_fail(msg, msg_len, "J=%d particle %d: look-ahead pieces %d whole %d (want %d)", l.J, q, np, whole[t],
-                         pieces_of(ntl));
     }
   }
   for (int a = 0; a < ng; ++a)

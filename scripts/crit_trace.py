@@ -31,7 +31,7 @@ y = np.sin(2 * np.pi * x).sum(0) + 0.1 * rng.standard_normal(N)
 e = np.full(N, 0.1)
 
 
-def split_la_bits(J, nt):  # mirrors split_la_bits (gpfit_api.hip; one group, GPF_SPLIT_LA)
+def split_la_bits(J, nt):  # the r4 split look-ahead (09b4abc, removed after profiles/r4/ab_split_la.txt)
     if os.environ.get("GPF_SPLIT_LA", "0") == "0" or nt < 4:
         return 0
     return (1 if 1 <= J <= nt - 3 else 0) | (2 if 2 <= J <= nt - 2 else 0)

@@ -358,34 +358,6 @@ def test_predict_pipeline_bitwise(ctx, monkeypatch, N, d, M, vcu):
     assert _rel(a[0][k], m0) < RTOL_MU_SD and _rel(a[1][k], s0) < RTOL_MU_SD
 
 
-@pytest.mark.parametrize("N,d,M", [(4096, 3, 2000), (1700, 2, 500), (700, 4, 300)])
-def test_split_lookahead_prediction(ctx, monkeypatch, N, d, M):
-    """The split look-ahead (r4, GPF_SPLIT_LA: launch J of the single-particle factorisation runs
-    the next critical tile over the columns < J as pieces with their own reduction tree, launch J+1
-    finishes it from that sum with one 128-deep block): mean and sd of the prediction within 1e-8
-    of the plain all-tile split (a different summation order of that tile's partials),
-    deterministic, and against the oracle's GP() on a sample of the queries."""
-    rng = np.random.default_rng(N * 3 + M)
-    x = rng.uniform(size=(d, N))
-    y = np.sin(5 * x[0]) * np.cos(2 * x[-1]) + 0.1 * rng.standard_normal(N)
-    e = rng.uniform(0.05, 0.2, size=N)
-    xf = rng.uniform(-0.1, 1.1, size=(d, M))
-    ls = rng.uniform(0.1, 0.4, size=d)
-    ctx.set_data(x, y, e)
-    monkeypatch.setenv("GPF_SPLIT_LA", "0")
-    m0, s0 = ctx.predict(ls, xf)
-    monkeypatch.setenv("GPF_SPLIT_LA", "1")
-    m1, s1 = ctx.predict(ls, xf)
-    m2, s2 = ctx.predict(ls, xf)
-    np.testing.assert_array_equal(m1, m2)
-    np.testing.assert_array_equal(s1, s2)
-    assert _rel(m1, m0) < 1e-8 and _rel(s1, s0) < 1e-8  # (1.4e-10 measured at N=4096)
-    k = np.linspace(0, M - 1, 32).astype(int)
-    with _blas_threads():
-        mo, so = ref_cpu.GP(x, y, e, xf[:, k], ls, batch_size=10000)
-    assert _rel(m1[k], mo) < RTOL_MU_SD and _rel(s1[k], so) < RTOL_MU_SD
-
-
 @pytest.mark.parametrize("keep_mb", [None, "0"])
 def test_predict_buffer_reuse_across_calls(monkeypatch, keep_mb):
     """gpf_predict keeps its query-chunk buffers in the context between calls (grow-only): a

@@ -34,8 +34,6 @@ ENVS = [
     {"GPF_SPLIT_K": "3", "GPF_SPLIT_K_SLOTS": "1000", "GPF_SPLIT_K_MINCH": "1", "GPF_GROUPS": "2"},
     {"GPF_REORDER": "0"}, {"GPF_REORDER": "0", "GPF_EARLY_DIAG": "1"},  # r4: the reordered dispatch off
     {"GPF_EARLY_DIAG": "1", "GPF_GROUPS": "2"},                         # reordered where it fits, two groups
-    {"GPF_SPLIT_LA": "1"}, {"GPF_SPLIT_LA": "1", "GPF_SPLIT_K_MINCH": "1"},  # r4: the split look-ahead
-    {"GPF_SPLIT_LA": "1", "GPF_SPLIT_K": "7", "GPF_GROUPS": "2"},         # (one group only: off with two)
 ]
 
 
@@ -43,8 +41,7 @@ ENVS = [
 def env(monkeypatch):
     def apply(kv):
         for k in ("GPF_GROUPS", "GPF_SPLIT_K", "GPF_SPLIT_CRIT", "GPF_SPLIT_CRIT_MIN", "GPF_STEP_GROUP", "GPF_EARLY_DIAG",
-                  "GPF_DEFER_SYRK", "GPF_SPLIT_K_SLOTS", "GPF_SPLIT_K_MINCH", "GPF_PERSIST", "GPF_REORDER",
-                  "GPF_SPLIT_LA"):
+                  "GPF_DEFER_SYRK", "GPF_SPLIT_K_SLOTS", "GPF_SPLIT_K_MINCH", "GPF_PERSIST", "GPF_REORDER"):
             monkeypatch.delenv(k, raising=False)
         if kv and "GPF_PERSIST" not in kv:  # the launch-plan knobs: on the per-block-column launches
             monkeypatch.setenv("GPF_PERSIST", "0")
