@@ -1070,7 +1070,12 @@ __device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, con
 // timeout info gets bit 2 and the piece gives up, so the host reports the error).
 // seed(acc) (SEEDED: piece 0 only) starts piece 0's accumulator instead of zero: the L tiles seed
 // it with their covariance tile A_IJ, so the finisher does not compute it after the pieces, on
-// the critical path.
+// the critical path; piece 0 takes GPF_SEED_CH fewer chunks for it (r4: the seed cost it ~11 us,
+// and as the carrier of every level it reached, the whole tree waited for it).
+// (r4) Node sums are kept in the accumulators' own layout (wave, register pair, lane: 16-B
+// accesses, 1 KiB per wave instruction) instead of the row-major tile (8-B accesses): nothing but
+// the tree reads the slots. Prediction factor 2.99 -> 2.78-2.83 ms with both
+// (profiles/r4/ab_split_tree.txt).
 // ----------------------------------------------------------------------------
 // (A radix-4 tree — groups of up to 4 nodes, the last arriver forming ((n0 + n1) + (n2 + n3)),
 // bitwise these sums with half the levels — measured slower: factor 3.45 -> 3.73 ms, the
@@ -1081,10 +1086,10 @@ __device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, con
 // loads — MI355X_MICROARCH's sc1 hand-off form: sc1 payload stores drained by every wave, then one
 // lane's sc1 flag store behind a barrier; one lane's sc1 poll, a barrier, then every load sc1.
 #ifndef GPF_SEED_CH
-#define GPF_SEED_CH 0  // (A/B build switch) split_part: chunks of GEMM piece 0's covariance seed stands for
+#define GPF_SEED_CH 4  // split_part: chunks of GEMM piece 0's covariance seed stands for (profiles/r4/ab_split_tree.txt)
 #endif
 #ifndef GPF_TREE_NATIVE
-#define GPF_TREE_NATIVE 0  // (A/B build switch) split_part node sums in a register-native layout, 16-B accesses
+#define GPF_TREE_NATIVE 1  // split_part node sums in a register-native layout, 16-B accesses (0: row-major tile)
 #endif
 #ifndef GPF_TREE_SC1
 #define GPF_TREE_SC1 0
