@@ -1091,6 +1091,9 @@ __device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, con
 #ifndef GPF_TREE_NATIVE
 #define GPF_TREE_NATIVE 1  // split_part node sums in a register-native layout, 16-B accesses (0: row-major tile)
 #endif
+#ifndef GPF_TREE_BATCH
+#define GPF_TREE_BATCH 2  // row blocks of the sibling's node sum read per scheduling group (4 x 16 B per lane each)
+#endif
 #ifndef GPF_TREE_SC1
 #define GPF_TREE_SC1 0
 #endif
@@ -1203,7 +1206,7 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
             acc.v[mi][ni][2 * h] = acc.v[mi][ni][2 * h] + __builtin_bit_cast(double, u0);
             acc.v[mi][ni][2 * h + 1] = acc.v[mi][ni][2 * h + 1] + __builtin_bit_cast(double, u1);
           }
-        if (mi & 1) __builtin_amdgcn_sched_barrier(0);
+        if ((mi % GPF_TREE_BATCH) == GPF_TREE_BATCH - 1) __builtin_amdgcn_sched_barrier(0);
       }
       continue;
     }
