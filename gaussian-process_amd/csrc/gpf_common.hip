@@ -35,11 +35,8 @@ __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
 // WR x WC; each wave holds a (TM/WR) x (TM/WC) sub-tile as MBR x MBC MFMA blocks
 // of 16x16 (accumulators: 4 doubles per lane per block).
 template <int TM> struct TileCfg;
-#ifndef GPF_STEP_KC
-#define GPF_STEP_KC 16  // K depth per LDS stage of the 128-tile GEMMs (build-time tuning knob)
-#endif
 template <> struct TileCfg<128> {  // the factorisation / prediction GEMMs: 8 waves, 128x16 per wave
-  static constexpr int KC = GPF_STEP_KC, NW = 8, WR = 1, WC = 8;
+  static constexpr int KC = 16, NW = 8, WR = 1, WC = 8;
 };
 template <> struct TileCfg<64> {   // LDS-resident 64x64 products inside the diagonal factor: 8 waves, 32x16 each
   static constexpr int KC = 32, NW = 8, WR = 2, WC = 4;
@@ -65,9 +62,6 @@ template <int TM> struct Geo {
 //     blocks per SIMD for every s);
 //   64-tiles (WR = 2, WC = 4): the column slabs of the second row half are mirrored.
 // Any map is a permutation of the same per-element work: results are bitwise unchanged.
-#ifndef GPF_BAL
-#define GPF_BAL 1
-#endif
 template <int TM> struct Quad {
   int lane, rb, cb;
   __device__ Quad() {
@@ -76,11 +70,11 @@ template <int TM> struct Quad {
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar) tile origin
     if constexpr (Geo<TM>::WR == 1) {
       rb = 0;
-      cb = ((GPF_BAL && w >= 4) ? 11 - w : w) * (TM / Geo<TM>::WC);
+      cb = (w >= 4 ? 11 - w : w) * (TM / Geo<TM>::WC);
     } else {
       const int wr = w / Geo<TM>::WC, wc = w % Geo<TM>::WC;
       rb = wr * (TM / Geo<TM>::WR);
-      cb = ((GPF_BAL && (wr & 1)) ? (Geo<TM>::WC - 1 - wc) : wc) * (TM / Geo<TM>::WC);
+      cb = ((wr & 1) ? (Geo<TM>::WC - 1 - wc) : wc) * (TM / Geo<TM>::WC);
     }
   }
   __device__ __forceinline__ int row(int mi, int r) const { return rb + mi * 16 + (lane >> 4) + 4 * r; }
@@ -219,16 +213,9 @@ __device__ __forceinline__ d4 mfma_neg_a(double a, double b, d4 c) {
 // since it cannot tell which LDS bytes the transfer writes). That wait drained the next chunk's
 // prefetch before the current chunk's MFMAs could start. Every pipeline that uses dl_load waits
 // for its own transfers itself (s_waitcnt vmcnt before the barrier that publishes a chunk).
-#ifndef GPF_DL_ASM
-#define GPF_DL_ASM 1  // build-time A/B knob
-#endif
 __device__ __forceinline__ void dl_load(const double* g, double* l) {
-#if GPF_DL_ASM
   const uint32_t m = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)l;
   asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m) : "memory");
-#else
-  __builtin_amdgcn_global_load_lds((const void*)g, (__attribute__((address_space(3))) void*)l, 16, 0, 0);
-#endif
 }
 // The same transfer in the saddr form: a wave-uniform 64-bit base in SGPRs plus a 32-bit per-lane
 // byte offset, so the streamed GEMMs keep one VGPR per transfer stream instead of forming a 64-bit
@@ -243,10 +230,7 @@ __device__ __forceinline__ void dl_load_s(const void* base, uint32_t off, double
 // with sw = r & 7, while sw = (r >> 1) & 7 gives the 16 rows 16 distinct bank pairs (even and
 // odd rows sit 16 banks apart). Row offsets of operand blocks are multiples of 16, so the
 // swizzle of a read depends on the lane only and block displacements stay immediates.
-#ifndef GPF_DL_SW
-#define GPF_DL_SW 1
-#endif
-__device__ __forceinline__ int dl_sw(int r) { return GPF_DL_SW ? ((r >> 1) & 7) : (r & 7); }
+__device__ __forceinline__ int dl_sw(int r) { return (r >> 1) & 7; }
 
 // A wave-uniform pointer forced into SGPRs (v_readfirstlane of each half): the saddr transfers
 // need their base there, and the divergence analysis cannot always prove a base uniform (e.g.
@@ -323,27 +307,20 @@ struct DenseRun {
     b = NN ? *(const double*)(sb + lb[0] + s * 512 * 8) : *(const double*)(sb + lb[s]);
   }
 
-  // the MFMAs of one chunk for the row blocks mi >= M0 (M0 = MBR: none). GPF_OPBUF = 2 reads the
-  // operands of k-step s+1 into a second register set before the MFMAs of step s; 1 (default)
-  // reuses one set (the 8 x 1 wave layout needs 9 operands per k-step, and the second set would
-  // push the accumulator-resident finishes over the 128-register budget of 4 waves per SIMD).
-#ifndef GPF_OPBUF
-#define GPF_OPBUF 1
-#endif
+  // the MFMAs of one chunk for the row blocks mi >= M0 (M0 = MBR: none); one operand register set
+  // (the 8 x 1 wave layout needs 9 operands per k-step, and a second set, read a k-step ahead,
+  // would push the accumulator-resident finishes over the 128-register budget of 4 waves per SIMD)
   template <int BUF, int M0>
   __device__ __forceinline__ void mma(Acc<128>& acc, const double* smem) const {
     if constexpr (M0 >= MBR) return;
     const char* sb = (const char*)smem + BUF * DL_BUF * 8;
-    constexpr int NB = GPF_OPBUF;
-    double a[NB][MBR], b[NB];
-    reads<M0>(sb, 0, a[0], b[0]);
+    double a[MBR], b;
+    reads<M0>(sb, 0, a, b);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      if (NB == 2 && s < 3) reads<M0>(sb, s + 1, a[(s + 1) % NB], b[(s + 1) % NB]);
 #pragma unroll
-      for (int mi = M0; mi < MBR; ++mi)
-        acc.v[mi][0] = NEG ? mfma_neg_a(a[s % NB][mi], b[s % NB], acc.v[mi][0]) : mfma(a[s % NB][mi], b[s % NB], acc.v[mi][0]);
-      if (NB == 1 && s < 3) reads<M0>(sb, s + 1, a[0], b[0]);
+      for (int mi = M0; mi < MBR; ++mi) acc.v[mi][0] = NEG ? mfma_neg_a(a[mi], b, acc.v[mi][0]) : mfma(a[mi], b, acc.v[mi][0]);
+      if (s < 3) reads<M0>(sb, s + 1, a, b);
     }
   }
 

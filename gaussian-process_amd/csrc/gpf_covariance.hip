@@ -20,7 +20,7 @@ constexpr int BT = 64;  // covariance build tile
 // dims in order, (|a_i|^2 + |a_j|^2) - 2 a_i.a_j, clamp >= 0, exp(-0.5 r2).
 // Also seeds the per-particle RHS workspace with y (padded with zeros).
 // grid: (nb*(nb+1)/2, P) for every lower 64x64 tile, or (3*nt, P) with diag_only: the lower
-// tiles of the 128-wide diagonal blocks only (k_step computes the others itself, GPF_KFUSE).
+// tiles of the 128-wide diagonal blocks only (k_step computes the others itself).
 // ----------------------------------------------------------------------------
 __global__ __launch_bounds__(NTHR) void k_build_cov(int N, int Npad, int d, const double* __restrict__ x,
                                                     const double* __restrict__ y, const double* __restrict__ e,
@@ -113,13 +113,9 @@ __global__ __launch_bounds__(NTHR) void k_build_cov(int N, int Npad, int d, cons
 // segment). Write-bound (8 B per output) once the exponential per output is spread over enough
 // resident waves. D: the dimension as a template constant (1..4; 0 = any d <= DMAX at run time).
 // grid: (ceil(C/256), ceil(R/CC_R)), dynamic LDS cross_cov_lds(d) bytes
-#ifndef GPF_CC_R
-#define GPF_CC_R 32
-#endif
-#ifndef GPF_CC_NT
-#define GPF_CC_NT 1  // non-temporal stores (A/B, profiles/r3/ab_cross_cov.txt: 4.7 -> 4.9 TB/s)
-#endif
-constexpr int CC_R = GPF_CC_R, CC_C = 256;
+// 32 rows x 256 columns per workgroup; non-temporal stores (A/B, profiles/r3/ab_cross_cov.txt:
+// 4.7 -> 4.9 TB/s)
+constexpr int CC_R = 32, CC_C = 256;
 __host__ __device__ constexpr size_t cross_cov_lds(int d) { return (size_t)(d + 1) * (CC_R + CC_C) * 8; }
 template <int D>
 __global__ __launch_bounds__(NTHR) void k_cross_cov(int N1, int N2, int R, int C, int dd,
@@ -180,11 +176,7 @@ __global__ __launch_bounds__(NTHR) void k_cross_cov(int N1, int N2, int R, int C
       r2 = r2 > 0.0 ? r2 : 0.0;
       v = exp(-0.5 * r2);
     }
-#if GPF_CC_NT
     __builtin_nontemporal_store(v, op + (size_t)gi * ldo);
-#else
-    op[(size_t)gi * ldo] = v;
-#endif
   }
 }
 

@@ -1,0 +1,471 @@
+// gpf_diag.hip — the 128x128 diagonal-block factor of the blocked factorisation, blocked by 16
+// over the whole block (r5).
+//
+// Reference op (per particle, one diagonal block of GP_func.py:22,24,38): L = chol(A) (dpotrf),
+// U = L^-1 (what the identity formulation needs of solve(L, K_s)), z = U y (solve(L, y)), and the
+// column partials of colsum(U o U) and U^T z over the block's 128 rows. Replaces round 4's
+// factor128 (two 64x64 factors around 64-level GEMM phases, ~97-113k cycles on the chain of every
+// latency-bound launch, ~48 us).
+//
+// The block is an 8 x 8 grid of 16 x 16 blocks, right-looking, one 16-wide block column ("panel")
+// per step k, everything LDS-resident (the 36 lower blocks, 72 KiB) or in registers:
+//   P_k  wave 0 factors panel k on its own: the rows of blocks k .. k+3 (lane = row, registers
+//        only: pivot by v_readlane, 1/sqrt by v_rsq + Newton, rank-1 updates with the column's
+//        entries by v_readlane), carrying the forward substitution of y (z_k) and the inverse of
+//        the diagonal block X_kk = L_kk^-1 ([A | I] elimination, lane = column) along;
+//   Q_k  (one barrier later, the chain) every wave: the next panel's blocks A(i,k+1) -= L(i,k)
+//        L(k+1,k)^T for the window rows i <= k+4, and the rows below wave 0's 64-row window
+//        (k <= 3) by MFMA: L(i,k)^T = X_kk A(i,k)^T, their y update y_i -= L(i,k) z_k;
+//   and, beside wave 0's next panel (P_{k+1}), on waves 1-3 and 5-7 (not wave 4: FP64 MFMAs and
+//   VALU share a SIMD's FP64 units, and wave 4 shares wave 0's SIMD):
+//        the rest of step k's trailing update A(i,j) -= L(i,k) L(j,k)^T (k+2 <= j <= i);
+//        step k of the inverse, right-looking by block columns: the owner wave of column j of
+//        X = L^-1 (its blocks in registers, the accumulator layout) finalises X_kj = -X_kk S_kj
+//        (j < k; X_kk: the panel's) and adds S_ij += L(i,k) X_kj for i > k, stores X_kj (U_JJ) and
+//        adds its share of the column partials.
+// Two barriers per panel. Every product is a 16x16x16 MFMA product (4 v_mfma_f64_16x16x4) with
+// operands from LDS or from the owner's accumulators (register e of a 16x16 accumulator is the
+// B operand of k-step e: X_kj and L(i,k)^T never move). Fixed assignment of work to waves and a
+// fixed summation order: deterministic (not bitwise round 4's factor128; test_factor128 checks it
+// against LAPACK and the reference fixtures pin every schedule that uses it).
+#pragma once
+#include "gpf_common.hip"
+
+namespace gpf {
+
+constexpr int DB_LD = 17;                   // row stride of a 16x16 block in LDS (doubles)
+constexpr int DB_BLK = 16 * DB_LD;          // doubles per block
+constexpr int DB_NB = 36;                   // lower blocks (i >= j) of the 8 x 8 grid
+constexpr int DB_Y = DB_NB * DB_BLK;        // y -> z, 128 doubles
+constexpr int DB_LDS = DB_Y + T;            // doubles of LDS the factor uses (77.5 KiB)
+
+__host__ __device__ constexpr int db_bid(int i, int j) { return i * (i + 1) / 2 + j; }
+// element (r, c) of a block: row-major, stride 17: the 16 rows x 2 depths of an MFMA operand read
+// per 32 lanes land on 32 distinct bank pairs, and every access is one per-lane base (the lane's
+// row or column) plus immediate offsets (an XOR swizzle kept ~16 per-lane offsets live per access
+// pattern across the whole factor)
+__device__ __forceinline__ int db_off(int r, int c) { return r * DB_LD + c; }
+
+// ---- one-wave 16x16 block helpers (lane l: g = l >> 4, c = l & 15) ----
+// A operand of k-step s from block M: A(r, k) = M(r, k), r = l & 15, k = 4 s + g. Also the B
+// operand of M^T: B(k, c) = M^T(k, c) = M(c, k).
+__device__ __forceinline__ void db_opa(const double* M, double (&a)[4]) {
+  const int l = threadIdx.x & 63, r = l & 15, g = l >> 4;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) a[s] = M[db_off(r, 4 * s + g)];
+}
+// accumulator layout: register e = element (4 e + g, c) (= the B operand of k-step e)
+__device__ __forceinline__ d4 db_ld(const double* M) {
+  const int l = threadIdx.x & 63, c = l & 15, g = l >> 4;
+  d4 v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = M[db_off(4 * e + g, c)];
+  return v;
+}
+__device__ __forceinline__ void db_st(double* M, const d4& v) {
+  const int l = threadIdx.x & 63, c = l & 15, g = l >> 4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) M[db_off(4 * e + g, c)] = v[e];
+}
+// transposed: register e = element (c, 4 e + g) of M, i.e. (4 e + g, c) of M^T
+__device__ __forceinline__ d4 db_ld_t(const double* M) {
+  const int l = threadIdx.x & 63, c = l & 15, g = l >> 4;
+  d4 v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = M[db_off(c, 4 * e + g)];
+  return v;
+}
+__device__ __forceinline__ void db_st_t(double* M, const d4& v) {
+  const int l = threadIdx.x & 63, c = l & 15, g = l >> 4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) M[db_off(c, 4 * e + g)] = v[e];
+}
+// C -= A B^T, A and B blocks in LDS (rows as A operands)
+__device__ __forceinline__ d4 db_sub_abt(d4 acc, const double* A, const double* B) {
+  double a[4], b[4];
+  db_opa(A, a);
+  db_opa(B, b);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = mfma_neg_a(a[s], b[s], acc);
+  return acc;
+}
+// acc (+/-)= A X with A in LDS and X in the accumulator layout (its registers are the B operands)
+template <bool NEG>
+__device__ __forceinline__ d4 db_mul_ax(d4 acc, const double* A, const d4& X) {
+  double a[4];
+  db_opa(A, a);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = NEG ? mfma_neg_a(a[s], X[s], acc) : mfma(a[s], X[s], acc);
+  return acc;
+}
+
+// ---- static work assignment (compile-time k, block indices; runtime wave) ----
+// owner wave of column j of X (SIMD s holds waves s and s + 4): columns 0, 3, 6 on SIMD 1, 1, 4, 7
+// on SIMD 2, 2, 5 on SIMD 3, so that each step's active columns spread over the three SIMDs
+__host__ __device__ constexpr int db_col_wave(int j) {
+  return j == 0 ? 1 : j == 1 ? 2 : j == 2 ? 3 : j == 3 ? 5 : j == 4 ? 6 : j == 5 ? 7 : j == 6 ? 5 : 6;
+}
+// products the owner of column j does in step t of the inverse (finalise + contributions)
+__host__ __device__ constexpr int db_x_work(int t, int j) { return j > t ? 0 : (j < t ? 1 : 0) + (7 - t); }
+// the trailing-update blocks of step k beside panel k+1: (i, j) with k+2 <= j <= i, and the blocks
+// (i, k+1) below panel k+1's window (i >= k+5; the window's blocks are Q_k's)
+__host__ __device__ constexpr bool db_in_bulk(int k, int i, int j) { return j >= k + 1 && i >= j && i < 8 && (j >= k + 2 || i >= k + 5); }
+// owner wave of the trailing-update block (i, j) of step k: greedy in a fixed block order onto the
+// least-loaded SIMD (1-3) counting step k's inverse work, then its less-loaded wave
+__host__ __device__ constexpr int db_bulk_wave(int k, int bi, int bj) {
+  int wl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j = 0; j <= k && j < 8; ++j) wl[db_col_wave(j)] += db_x_work(k, j);
+  for (int i = k + 1; i < 8; ++i)
+    for (int j = k + 1; j <= i; ++j) {
+      if (!db_in_bulk(k, i, j)) continue;
+      int best = 1;
+      for (int s = 2; s <= 3; ++s)
+        if (wl[s] + wl[s + 4] < wl[best] + wl[best + 4]) best = s;
+      const int w = wl[best + 4] < wl[best] ? best + 4 : best;
+      if (i == bi && j == bj) return w;
+      wl[w] += 1;
+    }
+  return -1;
+}
+// Q_k items: m = 0: rows k+4 (TRSM + the next panel's update; k <= 3); m = 1..3: the next panel's
+// blocks i = k + m (i <= 7); m = 4..6: rows i = k + 1 + m below the window (TRSM only; i <= 7).
+// Item m runs on wave db_q_wave(m): the first four on four different SIMDs.
+__host__ __device__ constexpr int db_q_wave(int m) {
+  return m == 0 ? 1 : m == 1 ? 2 : m == 2 ? 3 : m == 3 ? 0 : m == 4 ? 5 : m == 5 ? 6 : 7;
+}
+
+// ---- the panel: wave 0 ----
+// Rows R = 16 k + r of blocks k .. k+3 (lane r < 64, R < 128): columns 16k .. 16k+15. Lane q holds
+// row 16 k + q of the diagonal block; its pivot reaches every lane by v_readlane. The rank-1
+// update of column q takes L(s, q) (s > q) from lane s by v_readlane, one fma per entry; the same
+// scalars finish X_kk's rows (lane c < 16 holds column c) and the forward substitution of y.
+// Writes L to LDS (blocks i > k) and global (rows R), X_kk to LDS (the diagonal slot) and global
+// (U), z_k / the reduced y of the window to LDS. Returns whether a pivot was not > 0.
+template <bool WT>
+__device__ __forceinline__ bool db_panel(double* lds, int k, double* __restrict__ Lt, double* __restrict__ Ut, size_t ld) {
+  const int r = threadIdx.x & 63;
+  const int R = 16 * k + r;
+  const bool live = R < T;
+  const int rr = r & 15;
+  double* blk = lds + db_bid(live ? k + (r >> 4) : k, k) * DB_BLK;
+  double a[16], w[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) a[c] = (live && (r >= 16 || c <= rr)) ? blk[db_off(rr, c)] : 0.0;
+  double yr = live ? lds[DB_Y + R] : 0.0;
+  int ro = r;
+  asm volatile("" : "+v"(ro));  // (an opaque lane index: the identity below is not kept live across panels)
+#pragma unroll
+  for (int s = 0; s < 16; ++s) w[s] = (s == ro) ? 1.0 : 0.0;
+  bool bad = false;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const double p = readlane_f64(a[q], q);
+    bad = bad | !(p > 0.0);
+    const double inv = rsqrt_nr(p);
+    // lanes r < q hold exact zeros in column q (the diagonal block's upper triangle was zeroed and
+    // every update of it is by a zero multiplier), lane q its pivot: no selects
+    const double l = a[q] * inv;
+    a[q] = l;
+    const double zq = readlane_f64(yr, q) * inv;
+    yr = (r == q) ? zq : fma(-l, zq, yr);
+    const double wq = w[q] * inv;
+    w[q] = wq;
+    asm volatile("" : "+v"(w[q]));  // (w is stored only by lanes < 16: keep its updates from sinking there)
+#pragma unroll
+    for (int s = q + 1; s < 16; ++s) {
+      const double lsq = readlane_f64(l, s);
+      a[s] = fma(-l, lsq, a[s]);
+      w[s] = fma(-lsq, wq, w[s]);
+      asm volatile("" : "+v"(w[s]));
+      if (((s - q) & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (live) {
+    if (r >= 16) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) blk[db_off(rr, c)] = a[c];
+    }
+    double* gl = Lt + (size_t)R * ld + 16 * k;
+#pragma unroll
+    for (int c = 0; c < 16; c += 2) *reinterpret_cast<d2*>(gl + c) = d2{a[c], a[c + 1]};
+    lds[DB_Y + R] = yr;
+  }
+  if (r < 16) {  // X_kk: lane r holds column r
+    double* xs = lds + db_bid(k, k) * DB_BLK;
+    double* gu = Ut + (size_t)(16 * k) * ld + 16 * k + r;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      xs[db_off(s, r)] = w[s];
+      gst<WT>(gu + (size_t)s * ld, w[s]);
+    }
+  }
+  return bad;
+}
+
+// Q_k item m on this wave (see db_q_wave): the chain between panels k and k+1
+template <bool WT>
+__device__ __forceinline__ void db_q_item(double* lds, int k, int m, double* __restrict__ Lt, size_t ld) {
+  const int l = threadIdx.x & 63, c = l & 15, g = l >> 4;
+  auto B = [&](int i, int j) { return lds + db_bid(i, j) * DB_BLK; };
+  if (m >= 1 && m <= 3) {  // the next panel's block (k + m, k + 1), L(k + m, k) from wave 0
+    const int i = k + m;
+    double* C = B(i, k + 1);
+    db_st(C, db_sub_abt(db_ld(C), B(i, k), B(k + 1, k)));
+    return;
+  }
+  // rows below wave 0's window: L(i,k)^T = X_kk A(i,k)^T (B operand A(i,k)^T: the A-operand read of A(i,k))
+  const int i = m == 0 ? k + 4 : k + 1 + m;
+  double* Aik = B(i, k);
+  double xa[4], ab[4];
+  db_opa(B(k, k), xa);
+  db_opa(Aik, ab);
+  d4 lt = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s = 0; s < 4; ++s) lt = mfma(xa[s], ab[s], lt);
+  // y_i -= L(i,k) z_k: lane (g, c) holds L(i,k)(c, 4e + g)
+  double yp = 0.0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) yp = fma(lt[e], lds[DB_Y + 16 * k + 4 * e + g], yp);
+  yp = sum_lane_groups(yp);
+  if (m == 0) {  // the next panel's block (k+4, k+1)^T -= L(k+1,k) L(k+4,k)^T (lt: the B operands)
+    double* C = B(i, k + 1);
+    db_st_t(C, db_mul_ax<true>(db_ld_t(C), B(k + 1, k), lt));
+  }
+  db_st_t(Aik, lt);  // L(i,k) for the trailing updates and the inverse
+  double* gl = Lt + (size_t)(16 * i + c) * ld + 16 * k + g;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) gl[4 * e] = lt[e];
+  if (g == 0) lds[DB_Y + 16 * i + c] = lds[DB_Y + 16 * i + c] - yp;
+}
+
+// Column j of X = L^-1 on its owner wave: S_ij (i > t) and the current X_tj in registers
+// (accumulator layout), the column partials (colsum(X o X), X^T z) per lane.
+struct DbCol {
+  d4 x[8];        // block i of column j: S_ij until step i finalises it, then X_ij
+  double s2, sz;  // lane (g, c): partial sums over the rows 4 e + g of column c's finalised blocks
+};
+
+// Step t of the inverse for column j (compile-time t, j; j <= t): finalise X_tj, store it, add its
+// partials, and the contributions S_ij += L(i,t) X_tj (i > t)
+template <bool WT, int t, int j>
+__device__ __forceinline__ void db_x_step(DbCol& col, double* lds, double* __restrict__ Ut, size_t ld) {
+  const int l = threadIdx.x & 63, c = l & 15, g = l >> 4;
+  auto B = [&](int i, int jj) { return lds + db_bid(i, jj) * DB_BLK; };
+  if constexpr (j == t) {  // the column's first step: X_tt from the panel, empty sums
+    col.x[t] = db_ld(B(t, t));
+#pragma unroll
+    for (int i = t + 1; i < 8; ++i) col.x[i] = d4{0.0, 0.0, 0.0, 0.0};
+    col.s2 = 0.0;
+    col.sz = 0.0;
+  } else {
+    col.x[t] = db_mul_ax<true>(d4{0.0, 0.0, 0.0, 0.0}, B(t, t), col.x[t]);  // X_tj = -X_tt S_tj
+    double* gu = Ut + (size_t)(16 * t + g) * ld + 16 * j + c;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) gst<WT>(gu + (size_t)(4 * e) * ld, col.x[t][e]);
+  }
+  // (one product at a time: the scheduler would otherwise hoist every product's operand reads
+  // ahead of the MFMAs and spill the column's accumulators; the SIMD's other wave fills the gaps)
+#pragma unroll
+  for (int i = t + 1; i < 8; ++i) {
+    col.x[i] = db_mul_ax<false>(col.x[i], B(i, t), col.x[t]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // the column partials of X_tj (after the contributions: fewer registers live)
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const double v = col.x[t][e];
+    col.s2 = fma(v, v, col.s2);
+    col.sz = fma(v, lds[DB_Y + 16 * t + 4 * e + g], col.sz);
+  }
+  // (formed here: sunk to the end, the sums kept every finalised block of the column live)
+  asm volatile("" : "+v"(col.s2), "+v"(col.sz));
+}
+
+// the columns of X wave W owns: at most two (db_col_wave)
+__host__ __device__ constexpr int db_col_of(int W, int n) {
+  int m = 0;
+  for (int j = 0; j < 8; ++j)
+    if (db_col_wave(j) == W) {
+      if (m == n) return j;
+      ++m;
+    }
+  return -1;
+}
+
+// the trailing update of step k beside panel k+1 (db_in_bulk): the blocks wave W owns
+template <int k, int W>
+__device__ __forceinline__ void db_bulk(double* lds) {
+  auto B = [&](int i, int j) { return lds + db_bid(i, j) * DB_BLK; };
+#pragma unroll
+  for (int i = k + 1; i < 8; ++i)
+#pragma unroll
+    for (int j = k + 1; j <= i; ++j)
+      if constexpr (true) {
+        if (db_in_bulk(k, i, j) && db_bulk_wave(k, i, j) == W) {
+          double* C = B(i, j);
+          db_st(C, db_sub_abt(db_ld(C), B(i, k), B(j, k)));
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+}
+
+template <bool WT, int k, int W>
+__device__ __forceinline__ void db_q(double* lds, double* __restrict__ Lt, size_t ld) {
+#pragma unroll
+  for (int m = 0; m < 7; ++m) {
+    const bool valid = m == 0 ? k <= 3 : (m <= 3 ? k + m <= 7 : k + 1 + m <= 7);
+    if (valid && db_q_wave(m) == W) db_q_item<WT>(lds, k, m, Lt, ld);
+  }
+}
+
+// Each wave runs its own path (a compile-time wave: every ownership decision is static, so no
+// column's registers are merged across other waves' branches); all paths pass the same barriers:
+// one after the load, two per step (one after the last panel), and the publish's.
+template <bool WT>
+__device__ __forceinline__ void db_publish(double* __restrict__ yseg, const double* lds, int* pub, int pub_val) {
+  if (threadIdx.x < T) gst<WT>(&yseg[threadIdx.x], lds[DB_Y + threadIdx.x]);  // z (final since the last panel)
+  if (pub) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's U and z stores drained
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(pub, pub_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <bool WT, int k>
+__device__ __forceinline__ void db_step_panel(double* lds, bool& bad, double* __restrict__ Lt, double* __restrict__ Ut,
+                                              size_t ld) {
+  bad = db_panel<WT>(lds, k, Lt, Ut, ld) | bad;
+  lsync();
+  if constexpr (k < 7) {
+    db_q<WT, k, 0>(lds, Lt, ld);
+    lsync();
+  }
+}
+
+template <bool WT>
+__device__ __forceinline__ void db_path_panel(double* lds, double* __restrict__ Lt, double* __restrict__ Ut, size_t ld,
+                                              double* __restrict__ yseg, int* __restrict__ info, int* pub, int pub_val) {
+  bool bad = false;
+  db_step_panel<WT, 0>(lds, bad, Lt, Ut, ld);
+  db_step_panel<WT, 1>(lds, bad, Lt, Ut, ld);
+  db_step_panel<WT, 2>(lds, bad, Lt, Ut, ld);
+  db_step_panel<WT, 3>(lds, bad, Lt, Ut, ld);
+  db_step_panel<WT, 4>(lds, bad, Lt, Ut, ld);
+  db_step_panel<WT, 5>(lds, bad, Lt, Ut, ld);
+  db_step_panel<WT, 6>(lds, bad, Lt, Ut, ld);
+  db_step_panel<WT, 7>(lds, bad, Lt, Ut, ld);
+  db_publish<WT>(yseg, lds, pub, pub_val);
+  if (bad && threadIdx.x == 0 && *info == 0) *info = 1;  // (the pivots are wave-uniform)
+}
+
+template <bool WT, int k, int W>
+__device__ __forceinline__ void db_step_other(double* lds, DbCol& c0, DbCol& c1, double* __restrict__ Lt,
+                                              double* __restrict__ Ut, size_t ld) {
+  constexpr int J0 = db_col_of(W, 0), J1 = db_col_of(W, 1);
+  if constexpr (k >= 1 && W != 4) {
+    db_bulk<k - 1, W>(lds);
+    if constexpr (J0 >= 0 && J0 <= k - 1) db_x_step<WT, k - 1, J0>(c0, lds, Ut, ld);
+    if constexpr (J1 >= 0 && J1 <= k - 1) db_x_step<WT, k - 1, J1>(c1, lds, Ut, ld);
+  }
+  lsync();
+  if constexpr (k < 7) {
+    db_q<WT, k, W>(lds, Lt, ld);
+    lsync();
+  }
+}
+
+template <bool WT, int W>
+__device__ __forceinline__ void db_path_other(double* lds, double* __restrict__ Lt, double* __restrict__ Ut, size_t ld,
+                                              double* __restrict__ yseg, double* __restrict__ s2o,
+                                              double* __restrict__ szo, int* pub, int pub_val) {
+  constexpr int J0 = db_col_of(W, 0), J1 = db_col_of(W, 1);
+  DbCol c0, c1;
+  db_step_other<WT, 0, W>(lds, c0, c1, Lt, Ut, ld);
+  db_step_other<WT, 1, W>(lds, c0, c1, Lt, Ut, ld);
+  db_step_other<WT, 2, W>(lds, c0, c1, Lt, Ut, ld);
+  db_step_other<WT, 3, W>(lds, c0, c1, Lt, Ut, ld);
+  db_step_other<WT, 4, W>(lds, c0, c1, Lt, Ut, ld);
+  db_step_other<WT, 5, W>(lds, c0, c1, Lt, Ut, ld);
+  db_step_other<WT, 6, W>(lds, c0, c1, Lt, Ut, ld);
+  db_step_other<WT, 7, W>(lds, c0, c1, Lt, Ut, ld);
+  // the last inverse step (X_7j = -X_77 S_7j)
+  if constexpr (J0 >= 0) db_x_step<WT, 7, J0>(c0, lds, Ut, ld);
+  if constexpr (J1 >= 0) db_x_step<WT, 7, J1>(c1, lds, Ut, ld);
+  db_publish<WT>(yseg, lds, pub, pub_val);
+  // column partials (after the publish: the launch's tiles do not read them): lane (g, c) holds
+  // rows 4 e + g of every block of the column
+  const int lane = threadIdx.x & 63;
+  if constexpr (J0 >= 0) {
+    const double a2 = sum_lane_groups(c0.s2), az = sum_lane_groups(c0.sz);
+    if (lane < 16) {
+      s2o[16 * J0 + lane] = a2;
+      szo[16 * J0 + lane] = az;
+    }
+  }
+  if constexpr (J1 >= 0) {
+    const double a2 = sum_lane_groups(c1.s2), az = sum_lane_groups(c1.sz);
+    if (lane < 16) {
+      s2o[16 * J1 + lane] = a2;
+      szo[16 * J1 + lane] = az;
+    }
+  }
+}
+
+// The diagonal block at Lt / Ut (row stride ld): in: Lt's lower 128 x 128 (A, fully reduced),
+// yseg (y, fully reduced); out: Lt = L (zeros above the diagonal), Ut = L^-1 (likewise), yseg = z,
+// s2o / szo = the column partials. lds: DB_LDS doubles. WT: write-through U and z (read by other
+// workgroups of the launch after pub). pub (nullable): set to pub_val once U and z are stored and
+// drained, before the partials. info gets 1 on a pivot that is not > 0.
+template <bool WT = false>
+__device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __restrict__ Ut, size_t ld,
+                                          double* __restrict__ yseg, double* __restrict__ s2o, double* __restrict__ szo,
+                                          int* __restrict__ info, double* lds, int* pub = nullptr, int pub_val = 0) {
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // A's 36 lower blocks -> LDS (16 B per lane from memory), y -> LDS
+  {
+    const double* A = launder(Lt);
+#pragma unroll
+    for (int u = 0; u < (DB_NB * 16 * 8) / DNTH; ++u) {
+      const int q = tid + DNTH * u, row = q >> 3, cp = q & 7;  // block row `row` (0..575), pair cp
+      int bi = 0, rem = row;
+#pragma unroll
+      for (int t = 1; t < 8; ++t)
+        if (rem >= 16 * t) {
+          rem -= 16 * t;
+          bi = t;
+        }
+      const int bj = rem >> 4, rr = rem & 15;
+      const d2 v = *reinterpret_cast<const d2*>(A + (size_t)(16 * bi + rr) * ld + 16 * bj + 2 * cp);
+      double* s = lds + db_bid(bi, bj) * DB_BLK + db_off(rr, 2 * cp);
+      s[0] = v.x;
+      s[1] = v.y;
+    }
+    if (tid < T) lds[DB_Y + tid] = yseg[tid];
+  }
+  // zeros above the diagonal blocks of L and U (wave 4: idle otherwise; nothing reads them here)
+  if (wave == 4) {
+    const int lane = tid & 63;
+    for (int t = 0; t < 7; ++t)
+      for (int q = lane; q < 16 * 8 * (7 - t); q += 64) {  // rows 16t.., columns 16(t+1)..127, pairs
+        const int rr = q / (8 * (7 - t)), cp = q % (8 * (7 - t));
+        const size_t o = (size_t)(16 * t + rr) * ld + 16 * (t + 1) + 2 * cp;
+        *reinterpret_cast<d2*>(Lt + o) = d2{0.0, 0.0};
+        gst<WT>(Ut + o, 0.0);
+        gst<WT>(Ut + o + 1, 0.0);
+      }
+  }
+  lsync();
+  switch (wave) {
+    case 0: db_path_panel<WT>(lds, Lt, Ut, ld, yseg, info, pub, pub_val); break;
+    case 1: db_path_other<WT, 1>(lds, Lt, Ut, ld, yseg, s2o, szo, pub, pub_val); break;
+    case 2: db_path_other<WT, 2>(lds, Lt, Ut, ld, yseg, s2o, szo, pub, pub_val); break;
+    case 3: db_path_other<WT, 3>(lds, Lt, Ut, ld, yseg, s2o, szo, pub, pub_val); break;
+    case 4: db_path_other<WT, 4>(lds, Lt, Ut, ld, yseg, s2o, szo, pub, pub_val); break;
+    case 5: db_path_other<WT, 5>(lds, Lt, Ut, ld, yseg, s2o, szo, pub, pub_val); break;
+    case 6: db_path_other<WT, 6>(lds, Lt, Ut, ld, yseg, s2o, szo, pub, pub_val); break;
+    default: db_path_other<WT, 7>(lds, Lt, Ut, ld, yseg, s2o, szo, pub, pub_val); break;
+  }
+}
+
+}  // namespace gpf

@@ -61,30 +61,6 @@ __device__ unsigned long long g_diag_stamps[DIAG_NSTAMPS];
 // The diagonal-block routines below run on all DNTH (= 512) threads of the
 // factorisation workgroups (k_diag and, fused, k_step).
 
-// ----------------------------------------------------------------------------
-// 64x64 Cholesky with the inverse riding along ([A | I] -> [L | L^-1]), in
-// panels of 4 columns with a one-panel look-ahead: one barrier per panel.
-// Thread (r = tid>>3, g = tid&7) keeps row r, columns s = g + 8m, of the
-// trailing A and of X in registers (8 + 8 doubles). Iteration k (panel
-// cb = 4k, its factor already in pout[k&1]):
-//   waves 1..7 (and wave 0 while it still owns live rows): apply panel k
-//     a[r][s] -= L[r][cb+q] L[s][cb+q]  (s > cb+3, s <= r)
-//     x[r][s] -= L[r][cb+q] X[cb+q][s]  (s <= cb+3 < r)
-//   one q at a time in ascending order, take finished X rows of panel k, and
-//   hand strip k+2 (A columns cb+8.., X rows cb+8..) to the panel wave;
-//   wave 0 (lane = row for A, lane = column for X, no barrier): take strip k+1
-//   (through panel k-1), apply panel k to it from its own registers (multipliers
-//   by readlane), factor it (pivot, sqrt, reciprocal per column) and finish its
-//   4 X rows (their diagonal block is still the identity); L -> sA,
-//   pout[(k+1)&1][l][q] = L[l][cb'+q] (l > cb'+3) or X[cb'+q][l] (l <= cb'+3).
-// Every element sees exactly the operations of the column-by-column
-// elimination, in the same order (mul, then sub: -ffp-contract=off), so the
-// result is bitwise that of an unblocked right-looking Cholesky.
-//   in : sA[r*la + s] lower triangle of the tile
-//   out: sA = L (zeros above the diagonal), sX = L^-1; returns true (in thread 0)
-//        if a pivot was not > 0 (numpy: LinAlgError, GP_func.py:22)
-// buf: >= 1024 doubles of LDS scratch.
-// ----------------------------------------------------------------------------
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const long long i = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readlane((int)i, lane);
@@ -96,98 +72,28 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 // operations retired, then s_barrier (the asm's memory clobber keeps the compiler from moving
 // memory operations across it). Unlike __syncthreads() (a workgroup-scope release fence) it does
 // not wait for the wave's outstanding global stores, so the L/U tile stores of the factor drain
-// behind its LDS phases instead of stalling every barrier. GPF_LSYNC=0: __syncthreads().
-#ifndef GPF_LSYNC
-#define GPF_LSYNC 1
-#endif
-__device__ __forceinline__ void lsync() {
-#if GPF_LSYNC
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#else
-  __syncthreads();
-#endif
-}
+// behind its LDS phases instead of stalling every barrier.
+__device__ __forceinline__ void lsync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// 1/sqrt(p) for the pivots of the diagonal factor: v_rsq_f64 and GPF_RSQ_NEWTON Newton steps
+// 1/sqrt(p) for the pivots of the diagonal factor: v_rsq_f64 and two Newton steps
 // (y += y (1/2 - p/2 y^2)), a short dependent chain instead of the ~25 ops of a correctly
 // rounded sqrt followed by a division; within a few ulp of 1/sqrt(p).
-#ifndef GPF_RSQ_NEWTON
-#define GPF_RSQ_NEWTON 2
-#endif
 __device__ __forceinline__ double rsqrt_nr(double p) {
   double y = __builtin_amdgcn_rsq(p);
   const double h = 0.5 * p;
 #pragma unroll
-  for (int it = 0; it < GPF_RSQ_NEWTON; ++it) {
+  for (int it = 0; it < 2; ++it) {
     const double t = fma(-(h * y), y, 0.5);
     y = fma(y, t, y);
   }
   return y;
 }
 
-constexpr int F64_PW = 4;            // panel width
-constexpr int F64_BUF = 4 * 64 * 4;  // LDS scratch of factor64: 2 strip + 2 panel buffers of [64][4]
-
-// Panel wave: factor the 4 columns held as v[q] = A[l][cb+q] (l >= cb) and finish
-// the 4 X rows held as w[q] = X[cb+q][l]; writes L to sA and the panel to pout.
-// The 4x4 diagonal block is broadcast once (10 readlanes) and factored redundantly
-// by every lane, so each lane's row needs no further cross-lane traffic. The
-// operations and their order are those of the column-by-column elimination.
-__device__ __forceinline__ void f64_factor_panel(double (&v)[F64_PW], double (&w)[F64_PW], int l, int cb,
-                                                 double* sA, int la, double* pout, bool& bad) {
-  constexpr int PW = F64_PW;
-  double d[PW][PW];  // d[i][j] = A[cb+i][cb+j], j <= i (then L of the block)
-#pragma unroll
-  for (int i = 0; i < PW; ++i)
-#pragma unroll
-    for (int j = 0; j <= i; ++j) d[i][j] = readlane_f64(v[j], cb + i);
-  double dg[PW], inv[PW];
-#pragma unroll
-  for (int q = 0; q < PW; ++q) {
-    const double p = d[q][q];
-    bad = bad | !(p > 0.0);
-    inv[q] = rsqrt_nr(p);
-    dg[q] = p * inv[q];
-#pragma unroll
-    for (int i = q + 1; i < PW; ++i) d[i][q] = d[i][q] * inv[q];  // L[cb+i][cb+q]
-#pragma unroll
-    for (int i = q + 1; i < PW; ++i)
-#pragma unroll
-      for (int j = q + 1; j <= i; ++j) d[i][j] = d[i][j] - d[i][q] * d[j][q];
-  }
-#pragma unroll
-  for (int q = 0; q < PW; ++q) {
-    const double lq = (l > cb + q) ? v[q] * inv[q] : dg[q];  // L[l][cb+q] (rows below cb+q matter)
-    v[q] = lq;
-    w[q] = w[q] * inv[q];
-#pragma unroll
-    for (int q2 = q + 1; q2 < PW; ++q2) {
-      v[q2] = v[q2] - lq * d[q2][q];
-      w[q2] = w[q2] - d[q2][q] * w[q];
-    }
-  }
-  if (l >= cb) {
-#pragma unroll
-    for (int q = 0; q < PW; ++q) sA[l * la + cb + q] = v[q];
-  }
-  const bool below = l > cb + PW - 1;
-  *reinterpret_cast<d2*>(pout + l * PW) = below ? d2{v[0], v[1]} : d2{w[0], w[1]};
-  *reinterpret_cast<d2*>(pout + l * PW + 2) = below ? d2{v[2], v[3]} : d2{w[2], w[3]};
-}
-
-// Block slots of the MFMA update: the 10 lower 16x16 blocks of A (slot ids 0..9) and
-// of X (10..19), in the order (0,0) (1,0) (1,1) (2,0) (2,1) (2,2) (3,0) .. (3,3);
-// waves 1..7 own ids wave-1, wave-1+7, wave-1+14 (wave 0 is the panel wave).
-__device__ __forceinline__ void f64_block(int id, bool& isx, int& bi, int& bj) {
-  isx = id >= 10;
-  const int t = isx ? id - 10 : id;
-  bi = (t >= 6) ? 3 : (t >= 3) ? 2 : (t >= 1) ? 1 : 0;
-  bj = t - bi * (bi + 1) / 2;
-}
+constexpr int F64_BUF = 1024;  // LDS scratch of the diagonal factor (>= the 512-double reduction scratch)
 
 // ----------------------------------------------------------------------------
-// Blocked 64x64 factor (GPF_F64_BLOCKED = 1, default): 16-wide block columns, right-looking.
-// The 4-wide panels above pass 17 barriers and put the 4x4 pivot chain, the strip hand-off and
+// Blocked 64x64 factor: 16-wide block columns, right-looking.
+// Round 2's 4-wide panels passed 17 barriers and put the 4x4 pivot chain, the strip hand-off and
 // the update waves' serialised operand loads on every 4 columns (~3.4k cycles per panel,
 // profiles/r3/factor64_panel_stamps.txt). Here one wave factors a whole 16-column block column
 // (all rows below the diagonal at once, lane = row, registers only), and everything else is
@@ -202,9 +108,6 @@ __device__ __forceinline__ void f64_block(int id, bool& isx, int& bi, int& bj) {
 // Waves w and w+4 share a SIMD: while wave 0 factors a block column, wave 4 stays idle and the
 // longest side job (the 16x16 inversion) runs on wave 6.
 // ----------------------------------------------------------------------------
-#ifndef GPF_F64_BLOCKED
-#define GPF_F64_BLOCKED 1
-#endif
 
 // D (+)= (NEG ? -1 : 1) A B for 16x16 blocks in LDS: A row-major [r][k] at pa; B as [k][c] at pb
 // (BT = false) or given transposed, Bt[c][k] at pb (BT = true); D row-major at pc (ACC: D is
@@ -375,179 +278,8 @@ __device__ __forceinline__ bool factor64_blocked(double* sA, int la, double* sX,
 }
 
 __device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx, double* buf) {
-#if GPF_F64_BLOCKED
   return factor64_blocked(sA, la, sX, lx, buf);
-#endif
-  constexpr int PW = F64_PW, NS = 3;  // panel width, block slots per update wave
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lr = lane & 15, lk = lane >> 4;  // MFMA operand row/col and depth index; C row base
-  double* strip = buf;                // [2][64][4]: strip k goes to strip[k&1]
-  double* pout = buf + 2 * 64 * PW;   // [2][64][4]: panel k goes to pout[k&1]
-  // update waves: accumulators of the owned blocks, C layout (row lk + 4 reg, col lr)
-  d4 acc[NS];
-#pragma unroll
-  for (int j = 0; j < NS; ++j) {
-    const int id = wave - 1 + 7 * j;
-    acc[j] = d4{0.0, 0.0, 0.0, 0.0};
-    if (wave > 0 && id < 20) {
-      bool isx;
-      int bi, bj;
-      f64_block(id, isx, bi, bj);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = 16 * bi + lk + 4 * e, col = 16 * bj + lr;
-        acc[j][e] = isx ? ((row == col) ? 1.0 : 0.0) : ((col <= row) ? sA[row * la + col] : 0.0);
-      }
-    }
-  }
-  // strips 0 and 1: A[r][0..7] (no X columns left of them)
-  {
-    const int row = tid >> 3, c = tid & 7;
-    strip[(c / PW) * 64 * PW + row * PW + (c % PW)] = (c <= row) ? sA[row * la + c] : 0.0;
-  }
-  bool bad = false;
-  double v[PW], w[PW];  // panel wave: the current panel (L columns by row lane, X rows by column lane)
-  lsync();
-  if (wave == 0) {
-    const int l = lane;
-    const d2 p01 = *reinterpret_cast<const d2*>(strip + l * PW);
-    const d2 p23 = *reinterpret_cast<const d2*>(strip + l * PW + 2);
-    v[0] = p01.x; v[1] = p01.y; v[2] = p23.x; v[3] = p23.y;
-#pragma unroll
-    for (int q = 0; q < PW; ++q) w[q] = (l == q) ? 1.0 : 0.0;
-    f64_factor_panel(v, w, l, 0, sA, la, pout, bad);
-  }
-#pragma unroll 1
-  for (int k = 0; k < 64 / PW; ++k) {
-    const int cb = k * PW, ce = cb + PW, pc = cb / 16;
-    if (k == 4) DIAG_STAMP(10);
-    DIAG_STAMP_T(32 + 16 * k + wave, 64 * wave);
-    lsync();
-    if (k == 4) DIAG_STAMP(11);
-    DIAG_STAMP_T(32 + 16 * k + 8, 0);
-    DIAG_STAMP_T(32 + 16 * k + 14, 64 * DIAG_UW);
-    const double* pk = pout + (k & 1) * 64 * PW;
-    if (wave == 0) {
-      if (ce < 64) {
-        // look-ahead: strip k+1 through panel k, then factor it
-        const int l = lane, cn = ce;
-        const double* sb = strip + ((k + 1) & 1) * 64 * PW;
-        const d2 p01 = *reinterpret_cast<const d2*>(sb + l * PW);
-        const d2 p23 = *reinterpret_cast<const d2*>(sb + l * PW + 2);
-        double vn[PW] = {p01.x, p01.y, p23.x, p23.y};  // A[l][cn+q] for l >= cn; X[cn+q][l] for l < cb
-        double wn[PW];
-#pragma unroll
-        for (int q = 0; q < PW; ++q) wn[q] = (l < cb) ? vn[q] : ((l == cn + q) ? 1.0 : 0.0);
-#pragma unroll
-        for (int q = 0; q < PW; ++q)
-#pragma unroll
-          for (int q2 = 0; q2 < PW; ++q2) {
-            const double ls = readlane_f64(v[q], cn + q2);  // L[cn+q2][cb+q]
-            vn[q2] = vn[q2] - v[q] * ls;
-            wn[q2] = wn[q2] - ls * w[q];
-          }
-#pragma unroll
-        for (int q = 0; q < PW; ++q) {
-          v[q] = vn[q];
-          w[q] = wn[q];
-        }
-        if (k == 4) DIAG_STAMP(12);
-        DIAG_STAMP_T(32 + 16 * k + 9, 0);
-        f64_factor_panel(v, w, l, cn, sA, la, pout + ((k + 1) & 1) * 64 * PW, bad);
-        if (k == 4) DIAG_STAMP(13);
-        DIAG_STAMP_T(32 + 16 * k + 10, 0);
-      }
-    } else {
-      if (k == 4) DIAG_STAMP_T(20, 64);  // update wave 1 after the barrier
-      if (k == 4) DIAG_STAMP_T(24, 448);  // update wave 7 after the barrier
-      // rank-4 updates with one MFMA per owned live block (A operand staged negated); entries of
-      // A left of / above the panel are dead (never read again). (Issuing every slot's loads and
-      // MFMAs together measured slower, with or without the MFMA negate modifier; timing builds
-      // that drop parts of this work: profiles/r3/factor64_update_experiments.txt.)
-      const int c2 = cb + 2 * PW;
-      double* sb = strip + (k & 1) * 64 * PW;
-#pragma unroll
-      for (int j = 0; j < NS; ++j) {
-        const int id = wave - 1 + 7 * j;
-        if (id >= 20) continue;
-        bool isx;
-        int bi, bj;
-        f64_block(id, isx, bi, bj);
-        const int arow = 16 * bi + lr, bcol = 16 * bj + lr;
-        if (!isx) {
-          if (bj >= pc) {  // A(bi,bj), bj >= pc: C -= L[rows][cb..] L[cols][cb..]^T
-            const double av = -pk[arow * PW + lk];
-            const double bv = pk[bcol * PW + lk];
-            acc[j] = mfma(av, bv, acc[j]);
-          }
-          // strip k+2: A columns c2..c2+3 (rows >= c2) for the panel wave
-          if (c2 < 64 && bj == c2 / 16 && bi >= bj) {
-            const int q = lr - c2 % 16;
-            if (q >= 0 && q < PW) {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const int row = 16 * bi + lk + 4 * e;
-                if (row >= c2) sb[row * PW + q] = acc[j][e];
-              }
-            }
-          }
-        } else {
-          if (bi >= pc && bj <= pc) {  // X(bi,bj), bi >= pc >= bj: C -= L[rows > cb+3][cb..] X[cb..][cols <= cb+3]
-            const double av = (arow > cb + PW - 1) ? -pk[arow * PW + lk] : 0.0;
-            const double bv = (bcol <= cb + PW - 1) ? pk[bcol * PW + lk] : 0.0;
-            acc[j] = mfma(av, bv, acc[j]);
-            if (bi == pc) {  // the panel's X rows cb+lk are finished: take them
-              const int e0 = (cb % 16) / 4;
-              const double xf = (bcol <= cb + PW - 1) ? pk[bcol * PW + lk] : 0.0;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) acc[j][e] = (e == e0) ? xf : acc[j][e];
-            }
-          }
-          // strip k+2: X rows c2..c2+3 (columns < ce) for the panel wave
-          if (c2 < 64 && bi == c2 / 16 && bcol < ce) {
-            const int e0 = (c2 % 16) / 4;
-            double xv = acc[j][0];
-#pragma unroll
-            for (int e = 1; e < 4; ++e) xv = (e == e0) ? acc[j][e] : xv;
-            sb[bcol * PW + lk] = xv;
-          }
-        }
-        DIAG_STAMP_T(32 + 16 * k + 11 + j, 64 * DIAG_UW);
-      }
-      if (k == 4) DIAG_STAMP_T(21, 64);
-      if (k == 4) DIAG_STAMP_T(25, 448);
-    }
-  }
-  lsync();
-  // outputs: X blocks from their owners, zeros above the diagonal of X (wave 0) and of L
-#pragma unroll
-  for (int j = 0; j < NS; ++j) {
-    const int id = wave - 1 + 7 * j;
-    if (wave > 0 && id >= 10 && id < 20) {
-      bool isx;
-      int bi, bj;
-      f64_block(id, isx, bi, bj);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) sX[(16 * bi + lk + 4 * e) * lx + 16 * bj + lr] = acc[j][e];
-    }
-  }
-  if (wave == 0) {
-    for (int t = 0; t < 6; ++t) {  // upper blocks (0,1) (0,2) (0,3) (1,2) (1,3) (2,3)
-      const int bi = (t < 3) ? 0 : (t < 5) ? 1 : 2;
-      const int bj = (t < 3) ? t + 1 : (t < 5) ? t - 1 : 3;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) sX[(16 * bi + lk + 4 * e) * lx + 16 * bj + lr] = 0.0;
-    }
-  }
-  for (int i = tid; i < 64 * 64; i += DNTH) {
-    const int row = i >> 6, col = i & 63;
-    if (col > row) sA[row * la + col] = 0.0;
-  }
-  return bad;
 }
-
 
 // Fixed-order sum of the 8 partials scratch[q*64 + i], q = 0..7.
 __device__ __forceinline__ double sum8(const double* scratch, int i) {
@@ -814,9 +546,6 @@ __global__ __launch_bounds__(DNTH) void k_diag(int J, int nt, int N, int Npad, d
 // longest-first over the whole launch; smaller groups keep fewer particles'
 // B panels live in the 4 MB L2 at a time.
 // ----------------------------------------------------------------------------
-#ifndef GPF_KFUSE
-#define GPF_KFUSE 1  // off-diagonal K tiles computed in k_step instead of read from the K build
-#endif
 __host__ __device__ __forceinline__ void step_tile(int b, int P, int ntl, int grp, int& p, int& w) {
   if ((P & 7) != 0 || grp <= 0) {  // particle fastest
     p = b % P;
@@ -952,7 +681,7 @@ __host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt,
   const bool ltile = w < nt - 1 - J;
   if (ltile) {
     // L tiles split their depth-128J GEMM (only with the K tiles fused into k_step)
-    if (GPF_KFUSE && SPLIT == SPLIT_CRIT && w == 0 && J > 0) return ROLE_PIECE;
+    if (SPLIT == SPLIT_CRIT && w == 0 && J > 0) return ROLE_PIECE;
     return (SPLIT != SPLIT_NONE && sidx > 0) ? ROLE_IDLE : ROLE_WHOLE;  // nothing to split at J = 0
   }
   return (SPLIT == SPLIT_CRIT && sidx > 0) ? ROLE_IDLE : ROLE_WHOLE;  // U tiles never split in CRIT
@@ -968,18 +697,7 @@ static_assert(STEP_LDS * 8 <= 80 * 1024, "two k_step workgroups per CU (160 KiB 
 constexpr int STEP_NTH = Geo<T>::NTH;     // 512 threads: 8 waves, 128x16 per wave
 static_assert(STEP_NTH == DNTH, "the fused diagonal runs on the step workgroup");
 
-#ifndef GPF_DIAG_PRIO
-#define GPF_DIAG_PRIO 1
-#endif
-#ifndef GPF_WAVE_PRIO
-#define GPF_WAVE_PRIO 0  // build-time A/B knob
-#endif
-#ifndef GPF_CRIT_PRIO
-#define GPF_CRIT_PRIO 0  // wave priority of the critical tile's workgroups (I = J+1; 0 = off)
-#endif
-#ifndef GPF_STEP_WAVES_PER_SIMD
-#define GPF_STEP_WAVES_PER_SIMD 4  // 2 workgroups of 8 waves per CU
-#endif
+constexpr int STEP_WAVES_PER_SIMD = 4;  // 2 workgroups of 8 waves per CU
 #ifdef GPF_WG_TRACE
 // Diagnostic build only (-DGPF_WG_TRACE): per-workgroup start/end (s_memrealtime, 100 MHz)
 // and hardware placement of every k_step workgroup, per block column J.
@@ -1070,7 +788,7 @@ __device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, con
 // timeout info gets bit 2 and the piece gives up, so the host reports the error).
 // seed(acc) (SEEDED: piece 0 only) starts piece 0's accumulator instead of zero: the L tiles seed
 // it with their covariance tile A_IJ, so the finisher does not compute it after the pieces, on
-// the critical path; piece 0 takes GPF_SEED_CH fewer chunks for it (r4: the seed cost it ~11 us,
+// the critical path; piece 0 takes SEED_CH fewer chunks for it (r4: the seed cost it ~11 us,
 // and as the carrier of every level it reached, the whole tree waited for it).
 // (r4) Node sums are kept in the accumulators' own layout (wave, register pair, lane: 16-B
 // accesses, 1 KiB per wave instruction) instead of the row-major tile (8-B accesses): nothing but
@@ -1081,22 +799,10 @@ __device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, con
 // bitwise these sums with half the levels — measured slower: factor 3.45 -> 3.73 ms, the
 // carrier's three 128 KiB reads per level cost more than the saved hand-offs;
 // profiles/r3s2/ab_split_tree_radix.txt.)
-// GPF_TREE_SC1 (A/B build): the second arriver reads the sibling's node sum with sc1 loads (L1
-// bypassed, served by L2 / memory) instead of an agent-scope acquire (L1 invalidate) before plain
-// loads — MI355X_MICROARCH's sc1 hand-off form: sc1 payload stores drained by every wave, then one
-// lane's sc1 flag store behind a barrier; one lane's sc1 poll, a barrier, then every load sc1.
-#ifndef GPF_SEED_CH
-#define GPF_SEED_CH 4  // split_part: chunks of GEMM piece 0's covariance seed stands for (profiles/r4/ab_split_tree.txt)
-#endif
-#ifndef GPF_TREE_NATIVE
-#define GPF_TREE_NATIVE 1  // split_part node sums in a register-native layout, 16-B accesses (0: row-major tile)
-#endif
-#ifndef GPF_TREE_BATCH
-#define GPF_TREE_BATCH 2  // row blocks of the sibling's node sum read per scheduling group (4 x 16 B per lane each)
-#endif
-#ifndef GPF_TREE_SC1
-#define GPF_TREE_SC1 0
-#endif
+// (sc1 loads of the sibling's node sum in place of the acquire: within noise; 4 or 8 row blocks of
+// it read per scheduling group instead of 2: slower; profiles/r4/ab_split_tree.txt.)
+constexpr int SEED_CH = 4;     // split_part: chunks of GEMM piece 0's covariance seed stands for
+constexpr int TREE_BATCH = 2;  // row blocks of the sibling's node sum read per scheduling group
 constexpr int SPLIT_TREE = 80;              // tickets per split tile: pair (level l < 5, pair k < 16) at l * 16 + k
 constexpr int SPLIT_CNT = 2 * SPLIT_TREE;   // + the pairs' ready flags at SPLIT_TREE + l * 16 + k
 
@@ -1105,9 +811,9 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
                            int s, double* __restrict__ pt, unsigned* __restrict__ ct, double* smem,
                            const Quad<T>& qd, int* flag, int* info, int spins, Seed seed, int J) {
   // piece boundaries over nch + e chunks, the first e of them standing for piece 0's seed (its
-  // covariance tile costs about GPF_SEED_CH chunks of GEMM), so that the seeded piece — the carrier
+  // covariance tile costs about SEED_CH chunks of GEMM), so that the seeded piece — the carrier
   // of every tree level it reaches — ends its GEMM with the others
-  const int e = SEEDED ? GPF_SEED_CH : 0;
+  const int e = SEEDED ? SEED_CH : 0;
   const int c0 = s == 0 ? 0 : max(0, s * (nch + e) / S - e), c1 = max(0, (s + 1) * (nch + e) / S - e);
   if (SEEDED && s == 0)
     seed(acc);
@@ -1134,7 +840,6 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
     if (threadIdx.x == 0) *flag = (int)__hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (*flag == 0) {  // first: publish the node sum, then the sibling carries the pair on
-#if GPF_TREE_NATIVE
       {  // register-native slot layout: 16-B write-through stores, 1 KiB per wave instruction
         const auto ws = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(pt + (size_t)(c << l) * T * T), 0,
                                                           T * T * 8, 0x00020000);
@@ -1154,9 +859,6 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
                                                      16);  // sc1: write-through
             }
       }
-#else
-      acc.store_wt(qd, pt + (size_t)(c << l) * T * T, T);
-#endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its part of the node sum
       __syncthreads();
       if (threadIdx.x == 0) __hip_atomic_store(rdy, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1174,9 +876,7 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
         __builtin_amdgcn_s_sleep(2);
       }
       if (!late) {
-#if !GPF_TREE_SC1
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
         __hip_atomic_store(rdy, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -1189,39 +889,20 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
     // loop and spilled)
     const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(pt + (size_t)(sib << l) * T * T), 0, T * T * 8,
                                                       0x00020000);
-#if GPF_TREE_NATIVE
-    {
-      const int wb = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (Acc<T>::MBR * Acc<T>::MBC * 2048);
-#pragma unroll
-      for (int mi = 0; mi < Acc<T>::MBR; ++mi) {
-#pragma unroll
-        for (int ni = 0; ni < Acc<T>::MBC; ++ni)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const auto q4 = __builtin_amdgcn_raw_buffer_load_b128(rs, qd.lane * 16,
-                                                                  wb + ((mi * Acc<T>::MBC + ni) * 2 + h) * 1024,
-                                                                  GPF_TREE_SC1 ? 16 : 0);
-            const unsigned long long u0 = (unsigned long long)q4[0] | ((unsigned long long)q4[1] << 32),
-                                     u1 = (unsigned long long)q4[2] | ((unsigned long long)q4[3] << 32);
-            acc.v[mi][ni][2 * h] = acc.v[mi][ni][2 * h] + __builtin_bit_cast(double, u0);
-            acc.v[mi][ni][2 * h + 1] = acc.v[mi][ni][2 * h + 1] + __builtin_bit_cast(double, u1);
-          }
-        if ((mi % GPF_TREE_BATCH) == GPF_TREE_BATCH - 1) __builtin_amdgcn_sched_barrier(0);
-      }
-      continue;
-    }
-#endif
-    const int vo = 8 * ((qd.rb + (qd.lane >> 4)) * T + qd.cb + (qd.lane & 15));
+    const int wb = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (Acc<T>::MBR * Acc<T>::MBC * 2048);
 #pragma unroll
     for (int mi = 0; mi < Acc<T>::MBR; ++mi) {
 #pragma unroll
       for (int ni = 0; ni < Acc<T>::MBC; ++ni)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          acc.v[mi][ni][r] = acc.v[mi][ni][r] + __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
-                                                                            rs, vo, 8 * ((mi * 16 + 4 * r) * T + ni * 16),
-                                                                            GPF_TREE_SC1 ? 16 : 0));
-      if (mi & 1) __builtin_amdgcn_sched_barrier(0);
+        for (int h = 0; h < 2; ++h) {
+          const auto q4 = __builtin_amdgcn_raw_buffer_load_b128(rs, qd.lane * 16, wb + ((mi * Acc<T>::MBC + ni) * 2 + h) * 1024, 0);
+          const unsigned long long u0 = (unsigned long long)q4[0] | ((unsigned long long)q4[1] << 32),
+                                   u1 = (unsigned long long)q4[2] | ((unsigned long long)q4[3] << 32);
+          acc.v[mi][ni][2 * h] = acc.v[mi][ni][2 * h] + __builtin_bit_cast(double, u0);
+          acc.v[mi][ni][2 * h + 1] = acc.v[mi][ni][2 * h + 1] + __builtin_bit_cast(double, u1);
+        }
+      if ((mi % TREE_BATCH) == TREE_BATCH - 1) __builtin_amdgcn_sched_barrier(0);
     }
   }
   return true;
@@ -1280,10 +961,7 @@ __device__ __forceinline__ void syrk_item(int J, int p, int Npad, double* __rest
 // lower-triangular update first, so it takes ~7/16 of the depth and the critical tile of launch
 // J+1 continues from there: both then end near the launch's other deep L tiles (a look-ahead
 // over the whole depth made that workgroup the launch's last, profiles/r3s2/ab_lookahead_B.txt).
-#ifndef GPF_LA_FRAC16
-#define GPF_LA_FRAC16 7
-#endif
-__host__ __device__ __forceinline__ int la_chunks(int J) { return GPF_LA_FRAC16 * 8 * J / 16; }
+__host__ __device__ __forceinline__ int la_chunks(int J) { return 7 * 8 * J / 16; }
 
 // The partial of launch J goes to slot J & 1 of its particle (two slots per particle): the
 // critical tile of launch J + 1 reads slot J & 1 while launch J + 1's own look-ahead writes slot
@@ -1409,9 +1087,7 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
     if (!ED && I == J + 1) {  // fused diagonal factor of block J+1 (A_II, y_I fully reduced)
       __syncthreads();
       const size_t poff = ((size_t)p * nt + I) * Npad + (size_t)I * T;
-#if GPF_DIAG_PRIO
       __builtin_amdgcn_s_setprio(3);  // latency-critical: the next launch waits for this block
-#endif
       factor128(Aii, Up + (size_t)I * T * ld + (size_t)I * T, ld, yp + I * T, s2p + poff, szp + poff, info + p,
                 carve_diag(lds, lds + DIAG_BASE), I * T + H >= N);
     }
@@ -1481,7 +1157,7 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
 // first, ahead of the unsplit tiles); SPLIT_NONE carries no split code at all, so its register
 // allocation is that of the plain schedule.
 template <int SPLIT, int ED>
-__global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int J, int nt, int Npad, double* __restrict__ Lb,
+__global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_step(int J, int nt, int Npad, double* __restrict__ Lb,
                                                   double* __restrict__ Ub, double* __restrict__ yb,
                                                   double* __restrict__ s2p, double* __restrict__ szp,
                                                   int* __restrict__ info, int P, int grp, int N,
@@ -1505,14 +1181,6 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
 #endif
   __shared__ __attribute__((aligned(16))) double lds[STEP_LDS];
   __shared__ int sflag;
-#if GPF_WAVE_PRIO
-  // static priority for the second half of the workgroup (waves 4-7 share their SIMDs with waves
-  // 0-3 and lose every arbitration by age otherwise; MI355X_MICROARCH "Two waves per SIMD" item 4)
-  if (__builtin_amdgcn_readfirstlane(tid >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
-  // la bit 8: foreground (gpf_predict's pipelined V runs beside this factorisation on the same
-  // CUs): this launch's waves win issue arbitration against it
-  if (la & 8) __builtin_amdgcn_s_setprio(2);
   int p, w, sidx;
   const int role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, SPLIT != SPLIT_ALL && sy,
                                       SPLIT == SPLIT_NONE && ED && (la & 1) && !sy, p, w, sidx,
@@ -1537,11 +1205,6 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
     }
   }
 #endif
-#if GPF_CRIT_PRIO
-  // the critical tile I = J+1 (its pieces too) ahead of co-resident tiles in issue arbitration:
-  // the next launch waits for it, the other tiles only for the launch boundary
-  if ((role == ROLE_WHOLE || role == ROLE_PIECE) && w == 0 && J + 1 < nt) __builtin_amdgcn_s_setprio(GPF_CRIT_PRIO);
-#endif
   if (SPLIT != SPLIT_ALL && role == ROLE_SYRK) {
     syrk_item(J, p, Npad, Lb, yflag, lds);
     if (SPLIT == SPLIT_NONE && ED && (la & 1)) {  // the look-ahead rides on the SYRK workgroup (after its flag)
@@ -1556,9 +1219,7 @@ __global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_step(int 
     const size_t ld = (size_t)Npad;
     const size_t off = (size_t)p * ld * ld + (size_t)J * T * ld + (size_t)J * T;
     const size_t poff = ((size_t)p * nt + J) * Npad + (size_t)J * T;
-#if GPF_DIAG_PRIO
     __builtin_amdgcn_s_setprio(3);  // the launch's tiles wait for this block
-#endif
     // publishes block J (dflag[p] = J) as soon as U_JJ and z_J are stored, before its partials
     factor128<true>(Lb + off, Ub + off, ld, yb + (size_t)p * Npad + J * T, s2p + poff, szp + poff, info + p,
                     carve_diag(lds, lds + DIAG_BASE), J * T + H >= N, dflag + p, J);
@@ -1615,7 +1276,7 @@ __global__ __launch_bounds__(NTHR) void k_fill_hash(double* __restrict__ p, long
   }
 }
 
-__global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_gemm_bench(int mode, int D, int Npad, int P,
+__global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_gemm_bench(int mode, int D, int Npad, int P,
                                                                                    const double* __restrict__ Lb,
                                                                                    double* __restrict__ C,
                                                                                    unsigned long long* clk) {

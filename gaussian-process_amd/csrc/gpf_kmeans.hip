@@ -16,15 +16,20 @@
 
 namespace gpf {
 
-constexpr int KM_MAXKD = 8192;  // k x d doubles staged in LDS (64 KiB)
+constexpr int KM_MAXKD = 8192;  // k x (d + 1) doubles staged in LDS (centres and their norms: 64 KiB)
 
-// one thread per point; the centres and their squared norms staged in LDS (dynamic: k*d + k doubles)
+// one thread per point; the centres and their squared norms staged in LDS (dynamic: k*d + k doubles).
+// D > 0: the point's coordinates in registers (a compile-time d); D = 0: any d, the coordinates read
+// from memory per centre (a run-time-sized private array would live in scratch). The same operations
+// in the same order either way.
+template <int D>
 __global__ __launch_bounds__(NTHR) void k_km_assign(int64_t n, int d, int k, const double* __restrict__ X,
                                                     const double* __restrict__ C, int* __restrict__ labels,
                                                     double* __restrict__ dist) {
   extern __shared__ double km_lds[];
   double* sc = km_lds;           // [k][d]
   double* cn = km_lds + k * d;   // [k]
+  if (D > 0) d = D;
   for (int t = threadIdx.x; t < k * d; t += NTHR) sc[t] = C[t];
   __syncthreads();
   for (int j = threadIdx.x; j < k; j += NTHR) {
@@ -35,14 +40,23 @@ __global__ __launch_bounds__(NTHR) void k_km_assign(int64_t n, int d, int k, con
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * NTHR + threadIdx.x;
   if (i >= n) return;
-  double x[DMAX];
-#pragma unroll 4
-  for (int f = 0; f < d; ++f) x[f] = X[i * d + f];
+  double x[D > 0 ? D : 1];
+  const double* xi = X + i * d;
+  if (D > 0) {
+#pragma unroll
+    for (int f = 0; f < D; ++f) x[f] = xi[f];
+  }
+  auto coord = [&](int f) { return D > 0 ? x[f] : xi[f]; };
   int best = 0;
   double bv = 0.0;
   for (int j = 0; j < k; ++j) {
     double dot = 0.0;
-    for (int f = 0; f < d; ++f) dot = dot + x[f] * sc[j * d + f];
+    if (D > 0) {
+#pragma unroll
+      for (int f = 0; f < D; ++f) dot = dot + x[f] * sc[j * D + f];
+    } else {
+      for (int f = 0; f < d; ++f) dot = dot + xi[f] * sc[j * d + f];
+    }
     const double v = cn[j] + (-2.0 * dot);
     if (j == 0 || v < bv) {  // strict: the first minimum, as the reference's loop
       bv = v;
@@ -51,11 +65,27 @@ __global__ __launch_bounds__(NTHR) void k_km_assign(int64_t n, int d, int k, con
   }
   double dd = 0.0;
   for (int f = 0; f < d; ++f) {
-    const double t = x[f] - sc[best * d + f];
+    const double t = coord(f) - sc[best * d + f];
     dd = dd + t * t;
   }
   labels[i] = best;
   dist[i] = dd;
+}
+
+inline void launch_km_assign(hipStream_t st, int64_t n, int d, int k, const double* X, const double* C, int* labels,
+                             double* dist) {
+  const dim3 grid((unsigned)((n + NTHR - 1) / NTHR)), block(NTHR);
+  const size_t lds = (size_t)(k * d + k) * 8;
+  switch (d) {
+    case 1: hipLaunchKernelGGL(k_km_assign<1>, grid, block, lds, st, n, d, k, X, C, labels, dist); break;
+    case 2: hipLaunchKernelGGL(k_km_assign<2>, grid, block, lds, st, n, d, k, X, C, labels, dist); break;
+    case 3: hipLaunchKernelGGL(k_km_assign<3>, grid, block, lds, st, n, d, k, X, C, labels, dist); break;
+    case 4: hipLaunchKernelGGL(k_km_assign<4>, grid, block, lds, st, n, d, k, X, C, labels, dist); break;
+    case 5: hipLaunchKernelGGL(k_km_assign<5>, grid, block, lds, st, n, d, k, X, C, labels, dist); break;
+    case 6: hipLaunchKernelGGL(k_km_assign<6>, grid, block, lds, st, n, d, k, X, C, labels, dist); break;
+    case 8: hipLaunchKernelGGL(k_km_assign<8>, grid, block, lds, st, n, d, k, X, C, labels, dist); break;
+    default: hipLaunchKernelGGL(k_km_assign<0>, grid, block, lds, st, n, d, k, X, C, labels, dist); break;
+  }
 }
 
 // one workgroup per cluster: the members' coordinate sums and count, in a fixed order (each thread

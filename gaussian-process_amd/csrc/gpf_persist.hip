@@ -53,9 +53,6 @@
 
 namespace gpf {
 
-#ifndef GPF_PERSIST_WT
-#define GPF_PERSIST_WT 1  // (0: plain tile stores — a timing probe only, NOT coherent across XCDs)
-#endif
 
 struct PState {
   int* lcol;       // [P][nt]
@@ -227,7 +224,7 @@ __device__ __forceinline__ void p_ltile(const PItem& a, const PState& st, int J,
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        gst<GPF_PERSIST_WT>(&lrow[16 * (2 * P + j) + 4 * e], o[j][e]);
+        gst<true>(&lrow[16 * (2 * P + j) + 4 * e], o[j][e]);
         yr = fma(o[j][e], zj[16 * (2 * P + j) + 4 * e + g], yr);
       }
   }
@@ -242,15 +239,11 @@ __device__ __forceinline__ void p_ltile(const PItem& a, const PState& st, int J,
   syrk_tile<false>(Aii, ld, Aij, a.Npad, T, lds, qd);
   __syncthreads();
   const size_t poff = ((size_t)p * nt + I) * a.Npad + (size_t)I * T;
-#if GPF_DIAG_PRIO
   __builtin_amdgcn_s_setprio(3);  // latency-critical: every tile of column I waits for this block
-#endif
   // U_II and z_I are stored write-through and published (ucol[I] = I+1) before the partials
   factor128<true>(Aii, Up + (size_t)I * T * ld + (size_t)I * T, ld, yp + I * T, a.s2p + poff, a.szp + poff, info,
                   carve_diag(lds, lds + DIAG_BASE), I * T + H >= a.N, st.ucol + (size_t)p * nt + I, I + 1);
-#if GPF_DIAG_PRIO
   __builtin_amdgcn_s_setprio(0);
-#endif
 }
 
 // U tile (J, K), K < J (see the file comment).
@@ -293,7 +286,7 @@ __device__ __forceinline__ void p_utile(const PItem& a, const PState& st, int J,
       for (int e = 0; e < 4; ++e) {
         const int row = 16 * (2 * P + j) + 4 * e;  // + g
         const double v = o[j][e];
-        gst<GPF_PERSIST_WT>(&ucol[(size_t)row * ld], v);
+        gst<true>(&ucol[(size_t)row * ld], v);
         a2[h] = fma(v, v, a2[h]);
         az[h] = fma(v, zj[row + g], az[h]);
       }
@@ -318,7 +311,7 @@ __device__ __forceinline__ void p_utile(const PItem& a, const PState& st, int J,
 // what the deadlock-freedom argument needs; and as one item per workgroup the register allocation
 // is k_step's (a loop over items kept the decode and addressing state live across the tile bodies
 // and spilled). The grid equals the number of items, so every workgroup finds a ticket.
-__global__ __launch_bounds__(STEP_NTH, GPF_STEP_WAVES_PER_SIMD) void k_factor(PItem a, PState st, int P,
+__global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_factor(PItem a, PState st, int P,
                                                                                 unsigned long long* __restrict__ clk) {
   __shared__ unsigned long long sclk[2];
   const ClockSpan span(sclk);

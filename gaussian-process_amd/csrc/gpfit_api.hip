@@ -54,11 +54,6 @@ struct gpf_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t sub[MAX_GROUPS] = {};  // one stream per particle group (run_factor)
-  hipStream_t pside = nullptr;       // gpf_predict's side stream (lowest priority: V beside the factor)
-  // gpf_predict's CU-partitioned pipeline (GPF_PRED_VCU > 0): V's row tiles on p_vcu CUs (pv), the
-  // single-particle factorisation on the others (pf); created on first use, sized by p_vcu
-  hipStream_t pv = nullptr, pf = nullptr;
-  int p_vcu = 0;
   hipEvent_t fork = nullptr, join[MAX_GROUPS] = {};
   std::string err;
 
@@ -103,8 +98,6 @@ struct gpf_ctx {
   double *p_xf = nullptr, *p_ks = nullptr, *p_vsq = nullptr, *p_mu = nullptr, *p_sd = nullptr;
   double *p_hx = nullptr, *p_hout = nullptr;  // pinned staging: query coordinates, (mu, sd)
   double* p_vz = nullptr;                      // per row tile of V = U K_s: V^T z partials of mu (gpf::k_predict_vsq)
-  std::vector<hipEvent_t> pev;                 // gpf_predict: factor launch J done (row tile J of U final), nt of them
-  hipEvent_t pev_x = nullptr, pev_side = nullptr, pev_cc = nullptr, pev_v = nullptr, pev_f = nullptr;
   int64_t p_cols = 0, p_np = 0;
   int p_d = 0, p_nt = 0;
   // gpf_prob_surface's row-chunk buffers, kept between calls like the prediction's
@@ -360,9 +353,9 @@ static int step_group(int pc) {
 // N=4096 4.17 -> 3.90 ms, N=2048 equal, N=8192 already 8 (512/63), S=16 there 16.4 vs 13.5 ms
 // (profiles/r2/predict_splitk_ab.txt). GPF_SPLIT_K overrides (1 = off). Not for tiny problems (nt < 4).
 static int split_k(int tiles, int nt) {
-  int S = (nt >= 4 && GPF_KFUSE && tiles <= 64) ? std::max(1, std::min(8, 512 / std::max(1, tiles))) : 1;
+  int S = (nt >= 4 && tiles <= 64) ? std::max(1, std::min(8, 512 / std::max(1, tiles))) : 1;
   if (const char* s = getenv("GPF_SPLIT_K")) S = std::max(1, std::min(32, atoi(s)));
-  if (nt < 4 || !GPF_KFUSE) S = 1;
+  if (nt < 4) S = 1;
   return S;
 }
 
@@ -467,7 +460,7 @@ static int wait_spins() {
 // GPF_SPLIT_CRIT_MIN = minimum chunks per piece.
 static int split_crit(int pc, int nt, int J, int grp, int S_all) {
   // the last launch (J = nt-1) has no L tiles: its w = 0 is a U tile, which never splits
-  if (S_all > 1 || grp > 0 || J == 0 || J >= nt - 1 || nt < 4 || !GPF_KFUSE) return 1;
+  if (S_all > 1 || grp > 0 || J == 0 || J >= nt - 1 || nt < 4) return 1;
   // + the diagonal and the SYRK workgroups
   const int slots = 512, tiles = pc * (nt - 1) + (early_diag(pc, nt) ? pc : 0) + (defer_syrk() && J <= nt - 2 ? pc : 0);
   int S = 1, minch = 16;
@@ -573,7 +566,9 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
       l.la = ((la_ok && next_none && J >= 1 && J <= nt - 3) ? 1 : 0) | ((la_ok && prev_none && J >= 2 && J <= nt - 2) ? 2 : 0);
       // reordered dispatch: only where the first 3 gc workgroups (the light U tiles, which wait for
       // the diagonal workgroups behind them, and the SYRK workgroups) fit the chip's CUs at once
-      l.ro = (reorder_on() && l.ed && l.sy && l.split == gpf::SPLIT_NONE && l.grp == 0 && J >= 1 && 3 * l.gc <= 256) ? 1 : 0;
+      // and one group (a concurrent group's launch could hold the slots the waiters need)
+      l.ro = (reorder_on() && ng == 1 && l.ed && l.sy && l.split == gpf::SPLIT_NONE && l.grp == 0 && J >= 1 &&
+              3 * l.gc <= 256) ? 1 : 0;
       int nall = 0;
       for (int w = 0; S > 1 && w < nt - 1; ++w) nall += gpf::split_all_pieces(J, w, nt, l.S);
       l.grid = (S > 1 ? l.gc * nall : l.gc * (nt - 1) + l.gc * (Sc - 1)) + (l.ed ? l.gc : 0) + (l.sy ? l.gc : 0) +
@@ -592,7 +587,7 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
 // factors block 0 first and each launch J factors block J+1 at the end of its critical tile;
 // with the early diagonal factor launch J itself starts with the factor of block J. Joins back
 // into c->stream.
-static int run_factor(gpf_ctx* c, int pc, hipEvent_t* after = nullptr) {
+static int run_factor(gpf_ctx* c, int pc) {
   const int nt = c->nt, Np = (int)c->Npad, N = (int)c->N;
   const double Tf = (double)T, t3 = Tf * Tf * Tf;
   const int nb = Np / BT;
@@ -647,8 +642,8 @@ static int run_factor(gpf_ctx* c, int pc, hipEvent_t* after = nullptr) {
     double* szg = c->d_szp + (size_t)p0 * nt * ld;
     int* ig = c->d_info + p0;
     const double* lsg = c->d_ls + (size_t)p0 * c->d;
-    // with GPF_KFUSE only the diagonal blocks are built here; k_step computes the other tiles
-    const int nbuild = (GPF_KFUSE && nt > 1) ? 3 * nt : ntri;
+    // only the diagonal blocks are built here; k_step computes the other tiles
+    const int nbuild = nt > 1 ? 3 * nt : ntri;
     int rc = launch_on(c, st, PC_BUILD, 8.0 * nbuild * BT * BT * (double)gc, [&] {
       hipLaunchKernelGGL(gpf::k_build_cov, dim3(nbuild, gc), dim3(NTHR), 0, st, N, Np, c->d, c->d_x, c->d_y, c->d_e,
                          lsg, Lg, yg, ig, (int)(nbuild != ntri), c->d_flag + p0, c->d_cflag + p0,
@@ -678,7 +673,6 @@ static int run_factor(gpf_ctx* c, int pc, hipEvent_t* after = nullptr) {
     });
     if (rc) return rc;
     total += fl * pc;
-    for (int J = 0; after && J < nt; ++J) GPF_HIP(c, hipEventRecord(after[J], c->stream));
     if (c->prof && wa && wb) {
       hipEventRecord(wb, c->stream);
       c->pend.push_back({wa, wb, PC_FACTOR, total});
@@ -716,13 +710,11 @@ static int run_factor(gpf_ctx* c, int pc, hipEvent_t* after = nullptr) {
                          c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc, l.grp, N, c->d_x,
                          c->d_ls + (size_t)p0 * c->d, c->d, l.S, l.S2, partg, cntg, c->d_flag + p0, l.ed,
                          c->d_cflag + p0, l.defer, l.sy, spins,
-                         l.la | ((l.la & 2) ? la_delay : 0) | (after ? 8 : 0) | (l.ro ? 32 : 0),
+                         l.la | ((l.la & 2) ? la_delay : 0) | (l.ro ? 32 : 0),
                          l.la ? c->d_la + 2 * (size_t)p0 * T * T : nullptr, c->prof ? c->d_clk : nullptr);
     });
     if (rc) return rc;
     total += fl * gc;
-    // (ng == 1 where events are asked for: the single-particle factorisation of gpf_predict)
-    if (after && l.g == 0) GPF_HIP(c, hipEventRecord(after[l.J], st));
   }
   if (ng > 1) {
     for (int g = 0; g < ng; ++g) {
@@ -818,9 +810,6 @@ int gpf_open(int device, gpf_ctx** out) {
   for (int g = 0; ok && g < MAX_GROUPS; ++g)
     ok = hipStreamCreateWithFlags(&c->sub[g], hipStreamNonBlocking) == hipSuccess &&
          hipEventCreateWithFlags(&c->join[g], hipEventDisableTiming) == hipSuccess;
-  int prio_least = 0, prio_greatest = 0;
-  ok = ok && hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) == hipSuccess &&
-       hipStreamCreateWithPriority(&c->pside, hipStreamNonBlocking, prio_least) == hipSuccess;
   if (!ok) {
     gpf_close(c);
     return GPF_HIP_ERROR;
@@ -840,14 +829,6 @@ void gpf_close(gpf_ctx* c) {
   hipFree(c->d_sig); hipFree(c->d_exp); hipFree(c->d_lo); hipFree(c->d_hi);
   hipFree(c->km_x); hipFree(c->km_c); hipFree(c->km_dist); hipFree(c->km_sums); hipFree(c->km_cnt); hipFree(c->km_lab);
   for (auto e : c->pool) hipEventDestroy(e);
-  for (auto e : c->pev) hipEventDestroy(e);
-  if (c->pev_x) hipEventDestroy(c->pev_x);
-  if (c->pev_side) hipEventDestroy(c->pev_side);
-  for (hipEvent_t e : {c->pev_cc, c->pev_v, c->pev_f})
-    if (e) hipEventDestroy(e);
-  if (c->pv) hipStreamDestroy(c->pv);
-  if (c->pf) hipStreamDestroy(c->pf);
-  if (c->pside) hipStreamDestroy(c->pside);
   for (int g = 0; g < MAX_GROUPS; ++g) {
     if (c->sub[g]) hipStreamDestroy(c->sub[g]);
     if (c->join[g]) hipEventDestroy(c->join[g]);
@@ -1043,13 +1024,13 @@ int gpf_eval_batch(gpf_ctx* c, const double* ls, int P, double* loss, double* mu
   return GPF_OK;
 }
 
-// Factorise one particle (slot 0 of the workspace) and produce alpha on device, without waiting:
-// the factor's status word is copied to the pinned c->h_info[0] behind it on c->stream, and the
-// caller checks it (factor_status) after its next synchronisation — gpf_predict queues the query
-// kernels right behind the factorisation instead of idling the GPU for a host round trip.
-// ls == nullptr: the length scales are already in d_ls (queued on c->stream by the caller).
-// after (nullable): an event per block column, recorded behind its launch.
-static int factor_single_async(gpf_ctx* c, const double* ls, double** alpha_out, hipEvent_t* after = nullptr) {
+// Factorise one particle (slot 0 of the workspace) without waiting: the factor's status word is
+// copied to the pinned c->h_info[0] behind it on c->stream, and the caller checks it (factor_status)
+// after its next synchronisation — gpf_predict queues the query kernels right behind the
+// factorisation instead of idling the GPU for a host round trip. ls == nullptr: the length scales
+// are already in d_ls (queued on c->stream by the caller). alpha_out (nullable): alpha = K^-1 y
+// into the mu slot of particle 0 (gpf_predict forms its mean from V^T z and does not need it).
+static int factor_single_async(gpf_ctx* c, const double* ls, double** alpha_out) {
   int rc = ensure_work(c, 1);
   if (rc) return rc;
   if (ls) {
@@ -1057,16 +1038,17 @@ static int factor_single_async(gpf_ctx* c, const double* ls, double** alpha_out,
     GPF_HIP(c, hipMemcpyAsync(c->d_ls, c->h_ls, (size_t)c->d * 8, hipMemcpyHostToDevice, c->stream));
   }
   GPF_HIP(c, hipMemsetAsync(c->d_info, 0, 4, c->stream));
-  rc = run_factor(c, 1, after);
+  rc = run_factor(c, 1);
   if (rc) return rc;
-  // alpha into the mu slot of particle 0
-  rc = launch(c, PC_LOSS, 0.0, [&] {
-    hipLaunchKernelGGL(gpf::k_alpha, dim3((unsigned)((c->N + NTHR - 1) / NTHR)), dim3(NTHR), 0, c->stream,
-                       (int)c->N, (int)c->Npad, c->nt, c->d_szp, c->d_mu);
-  });
-  if (rc) return rc;
+  if (alpha_out) {
+    rc = launch(c, PC_LOSS, 0.0, [&] {
+      hipLaunchKernelGGL(gpf::k_alpha, dim3((unsigned)((c->N + NTHR - 1) / NTHR)), dim3(NTHR), 0, c->stream,
+                         (int)c->N, (int)c->Npad, c->nt, c->d_szp, c->d_mu);
+    });
+    if (rc) return rc;
+    *alpha_out = c->d_mu;
+  }
   GPF_HIP(c, hipMemcpyAsync(c->h_info, c->d_info, 4, hipMemcpyDeviceToHost, c->stream));
-  *alpha_out = c->d_mu;
   return GPF_OK;
 }
 
@@ -1091,48 +1073,6 @@ static int factor_single(gpf_ctx* c, const double* ls, double** alpha_out) {
   rc = factor_status(c);
   if (rc) *alpha_out = nullptr;
   return rc;
-}
-
-// The V set of the CU-partitioned prediction (include/gpfit.h): the CUs f(r) of ranks r < vcu,
-// f(r) = r[2:0] | r[4:3] << 3 | (r[2:0] ^ r[7:5]) << 5 — any 8 consecutive ranks cover the 8 values
-// of both bits [2:0] and bits [7:5] of the CU index, so a multiple of 8 CUs splits evenly over the
-// XCDs whether the mask bits interleave over them or block them (f is a bijection of 0..255).
-int gpf_cu_partition(int ncu, int vcu, uint32_t* mask, int words) {
-  if (ncu <= 0 || vcu < 0 || !mask || words * 32 < ncu) return -1;
-  for (int w = 0; w < words; ++w) mask[w] = 0;
-  int n = 0;
-  const int span = ncu <= 256 ? 256 : ncu;
-  for (int r = 0; r < span && n < vcu; ++r) {
-    const int i = ncu <= 256 ? ((r & 7) | (((r >> 3) & 3) << 3) | ((((r & 7) ^ (r >> 5)) & 7) << 5)) : r;
-    if (i >= ncu) continue;
-    mask[i >> 5] |= 1u << (i & 31);
-    ++n;
-  }
-  return n;
-}
-
-// gpf_predict's masked streams for vcu V CUs (created once per vcu; the old pair is destroyed
-// after the library stream drained, as gpf_predict enters with nothing of its own in flight)
-static int ensure_pred_streams(gpf_ctx* c, int vcu) {
-  if (c->pv && c->pf && c->p_vcu == vcu) return GPF_OK;
-  GPF_HIP(c, hipDeviceSynchronize());
-  if (c->pv) hipStreamDestroy(c->pv);
-  if (c->pf) hipStreamDestroy(c->pf);
-  c->pv = c->pf = nullptr;
-  c->p_vcu = 0;
-  const int words = (c->ncu + 31) / 32;
-  std::vector<uint32_t> mv(words), mf(words);
-  if (gpf_cu_partition(c->ncu, vcu, mv.data(), words) != vcu) return bad_arg(c, "GPF_PRED_VCU: bad CU count");
-  for (int w = 0; w < words; ++w) {
-    const int bits = std::min(32, c->ncu - 32 * w);
-    mf[w] = ~mv[w] & (bits == 32 ? 0xffffffffu : ((1u << bits) - 1u));
-  }
-  GPF_HIP(c, hipExtStreamCreateWithCUMask(&c->pv, (uint32_t)words, mv.data()));
-  GPF_HIP(c, hipExtStreamCreateWithCUMask(&c->pf, (uint32_t)words, mf.data()));
-  for (hipEvent_t* e : {&c->pev_cc, &c->pev_v, &c->pev_f})
-    if (!*e) GPF_HIP(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
-  c->p_vcu = vcu;
-  return GPF_OK;
 }
 
 int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int64_t batch, double* mu,
@@ -1182,115 +1122,25 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
     c->p_d = c->d;
     c->p_nt = c->nt;
   }
-  // Pipelined (GPF_PREDICT_PIPE, default on): the first query chunk's cross-covariance and its
-  // V = U K_s run on a side stream beside the factorisation, row tile t of V as soon as the
-  // factor's launch t has finished row tile t of U (and z_t): the single-particle factorisation
-  // is a chain of nt latency-bound launches that leave most of the chip idle, and V's row tiles
-  // fill it (GP_fit.py:32 -> GP_func.py:22-40). Later chunks follow on the main stream.
-  // Off by default: beside V's row tiles the factorisation's latency-bound chain slowed from
-  // 2.99 to 7.7 ms at N=4096 (M=10,000: 7.41-7.45 ms vs 5.52 ms serial, one box,
-  // profiles/r4/ab_r4g_summary.txt), despite V's lowest-priority stream, one V workgroup per CU
-  // and the factor's raised wave priority. GPF_PREDICT_PIPE=1 enables it.
-  bool pipe = false;
-  if (const char* e = getenv("GPF_PREDICT_PIPE")) pipe = atoi(e) != 0 && c->nt >= 2;
-  hipStream_t side = c->pside;
-  // CU-partitioned pipeline (GPF_PRED_VCU = V's CUs, with GPF_PREDICT_PIPE): beside the
-  // factorisation V's row tiles run on their own CUs (a stream CU mask, gpf_cu_partition) and the
-  // factor's workgroups on the others, so no V workgroup shares a CU with the factor's
-  // latency-bound chain; the row tiles of the factor's last GPF_PRED_VTAIL launches run after it on
-  // the whole chip
-  int vcu = 0, vtail = 4;
-  if (const char* e = getenv("GPF_PRED_VCU")) vcu = pipe ? std::max(0, std::min(c->ncu - 8, atoi(e))) : 0;
-  if (const char* e = getenv("GPF_PRED_VTAIL")) vtail = std::max(1, atoi(e));
-  const bool masked = vcu > 0;
-  if (masked)
-    if (int rs = ensure_pred_streams(c, vcu)) return rs;
-  hipStream_t vst = masked ? c->pv : side;  // V's row tiles beside the factorisation
-  if (pipe) {
-    if (!c->pev_x) GPF_HIP(c, hipEventCreateWithFlags(&c->pev_x, hipEventDisableTiming));
-    if (!c->pev_side) GPF_HIP(c, hipEventCreateWithFlags(&c->pev_side, hipEventDisableTiming));
-    while ((int)c->pev.size() < c->nt) {
-      hipEvent_t e = nullptr;
-      GPF_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      c->pev.push_back(e);
-    }
-  }
+  // (Two overlaps of V = U K_s with the single-particle factorisation were built and measured in
+  // round 4 — V's row tiles on a low-priority side stream behind each factor launch, and the same
+  // with the CUs partitioned by stream CU masks — and removed: the factorisation's latency-bound
+  // chain needs the whole chip, profiles/r4/ab_r4g_summary.txt, ab_pred_cumask.txt.)
   double *d_xf = c->p_xf, *d_ks = c->p_ks, *d_vsq = c->p_vsq, *d_vz = c->p_vz, *d_mu = c->p_mu, *d_sd = c->p_sd;
   double* hx = c->p_hx;
-  const double* d_z = c->d_yb;  // z = U y of particle slot 0 (row tile t final after factor launch t)
+  const double* d_z = c->d_yb;  // z = U y of particle slot 0
   auto stage_chunk = [&](int64_t s0, int64_t m) -> int {
     for (int k = 0; k < c->d; ++k) std::memcpy(hx + (size_t)k * Cp, xfit + (size_t)k * M + s0, (size_t)m * 8);
     GPF_HIP(c, hipMemcpyAsync(d_xf, hx, (size_t)c->d * Cp * 8, hipMemcpyHostToDevice, c->stream));
     return GPF_OK;
-  };
-  auto cross_cov = [&](hipStream_t st, int64_t m, int Cm) {
-    return launch_on(c, st, PC_PREDK, 8.0 * Np * Cm, [&] {
-      gpf::launch_cross_cov(st, (int)c->N, (int)m, (int)Np, Cm, c->d, c->d_x, (int)c->N, d_xf, (int)Cp, c->d_ls, d_ks,
-                            (int64_t)Cp);
-    });
-  };
-  // V = U K_s for row tiles [t0, t0 + rows): row tile t of U has (t+1) column tiles, the last triangular
-  // beside the factor, V's workgroups are held to one per CU (dynamic LDS: 64 + 17 KiB > half a
-  // CU's 160 KiB), so every CU keeps a slot for the factor's workgroups (one per CU under the
-  // balanced split), and the factor's waves run at a higher issue priority (k_step, la bit 8)
-  auto vsq = [&](hipStream_t st, int nqt, int t0, int rows) {
-    const size_t pad = (st == side && !masked) ? 17 * 1024 : 0;
-    const double Cm = (double)nqt * T;
-    const double vflops = 2.0 * T * T * Cm * ((double)(t0 + rows) * (t0 + rows + 1) / 2 - (double)t0 * (t0 + 1) / 2) -
-                          (double)T * T * Cm * rows;
-    return launch_on(c, st, PC_PRED, vflops, [&] {
-      hipLaunchKernelGGL(gpf::k_predict_vsq, dim3(nqt, rows), dim3(gpf::Geo<T>::NTH), pad, st, (int)Np, c->d_U, d_ks,
-                         (int)Cp, d_vsq, d_z, d_vz, t0);
-    });
   };
   // the length scales and chunk 0's coordinates first, then the factorisation
   std::memcpy(c->h_ls, ls, (size_t)c->d * 8);
   GPF_HIP(c, hipMemcpyAsync(c->d_ls, c->h_ls, (size_t)c->d * 8, hipMemcpyHostToDevice, c->stream));
   int rc = stage_chunk(0, std::min<int64_t>(chunk, M));
   if (rc) return rc;
-  if (pipe) GPF_HIP(c, hipEventRecord(c->pev_x, c->stream));
-  double* alpha = nullptr;
-  if (masked) {  // the factorisation on its CUs: run_factor queues on c->stream, so lend it pf
-    GPF_HIP(c, hipStreamWaitEvent(c->pf, c->pev_x, 0));
-    std::swap(c->stream, c->pf);
-  }
-  rc = factor_single_async(c, nullptr, &alpha, pipe ? c->pev.data() : nullptr);
-  if (masked) {
-    std::swap(c->stream, c->pf);
-    if (!rc) rc = hipEventRecord(c->pev_f, c->pf) == hipSuccess && hipStreamWaitEvent(c->stream, c->pev_f, 0) == hipSuccess
-                      ? GPF_OK
-                      : GPF_HIP_ERROR;
-  }
+  rc = factor_single_async(c, nullptr, nullptr);
   if (rc) return rc;
-  if (pipe) {
-    const int64_t m = std::min<int64_t>(chunk, M);
-    const int nqt = (int)((m + T - 1) / T);
-    GPF_HIP(c, hipStreamWaitEvent(vst, c->pev_x, 0));
-    rc = cross_cov(vst, m, nqt * T);
-    if (!rc && masked) GPF_HIP(c, hipEventRecord(c->pev_cc, vst));
-    // row tiles in batches of >= 512 workgroups (a batch of nqt workgroups per row tile alone
-    // would leave most slots idle and serialise the side stream behind the factor); on the V CUs,
-    // batches of about two workgroups per CU, then the last vtail row tiles in one batch on the
-    // whole chip once the factorisation is done
-    const int rows = masked ? std::max(1, (2 * vcu + nqt - 1) / nqt) : std::max(1, std::min(c->nt, (512 + nqt - 1) / nqt));
-    const int tlate = masked ? std::max(0, c->nt - vtail) : c->nt;
-    for (int t = 0; rc == GPF_OK && t < c->nt;) {
-      const bool late = t >= tlate;
-      const int r = late ? c->nt - t : std::min(rows, tlate - t);
-      hipStream_t st = late ? side : vst;
-      if (late) GPF_HIP(c, hipStreamWaitEvent(side, c->pev_cc, 0));
-      GPF_HIP(c, hipStreamWaitEvent(st, c->pev[t + r - 1], 0));
-      rc = vsq(st, nqt, t, r);
-      t += r;
-    }
-    if (rc) return rc;
-    GPF_HIP(c, hipEventRecord(c->pev_side, side));
-    GPF_HIP(c, hipStreamWaitEvent(c->stream, c->pev_side, 0));
-    if (masked) {
-      GPF_HIP(c, hipEventRecord(c->pev_v, vst));
-      GPF_HIP(c, hipStreamWaitEvent(c->stream, c->pev_v, 0));
-    }
-  }
   for (int64_t s = 0; s < M && rc == GPF_OK; s += chunk) {
     const int64_t m = std::min<int64_t>(chunk, M - s);
     const int nqt = (int)((m + T - 1) / T);
@@ -1302,10 +1152,18 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
       }
       if ((rc = stage_chunk(s, m))) break;
     }
-    if (!(pipe && s == 0)) {
-      if ((rc = cross_cov(c->stream, m, Cm))) break;
-      if ((rc = vsq(c->stream, nqt, 0, c->nt))) break;
-    }
+    rc = launch(c, PC_PREDK, 8.0 * Np * Cm, [&] {
+      gpf::launch_cross_cov(c->stream, (int)c->N, (int)m, (int)Np, Cm, c->d, c->d_x, (int)c->N, d_xf, (int)Cp, c->d_ls,
+                            d_ks, (int64_t)Cp);
+    });
+    if (rc) break;
+    // V = U K_s over every row tile of U (row tile t has t+1 column tiles, the last triangular)
+    const double vflops = 2.0 * T * T * (double)Cm * ((double)c->nt * (c->nt + 1) / 2) - (double)T * T * Cm * c->nt;
+    rc = launch(c, PC_PRED, vflops, [&] {
+      hipLaunchKernelGGL(gpf::k_predict_vsq, dim3(nqt, c->nt), dim3(gpf::Geo<T>::NTH), 0, c->stream, (int)Np, c->d_U,
+                         d_ks, (int)Cp, d_vsq, d_z, d_vz, 0);
+    });
+    if (rc) break;
     rc = launch(c, PC_LOSS, 0.0, [&] {
       hipLaunchKernelGGL(gpf::k_predict_out, dim3((unsigned)((m + NTHR - 1) / NTHR)), dim3(NTHR), 0, c->stream, c->nt,
                          (int)m, d_vz, (int)Cp, d_vsq, d_mu, d_sd);
@@ -1324,11 +1182,6 @@ int gpf_predict(gpf_ctx* c, const double* ls, const double* xfit, int64_t M, int
     }
     std::memcpy(mu + s, c->p_hout, (size_t)m * 8);
     std::memcpy(sd + s, c->p_hout + Cp, (size_t)m * 8);
-  }
-  if (pipe) hipStreamSynchronize(side);
-  if (masked) {
-    hipStreamSynchronize(c->pv);
-    hipStreamSynchronize(c->pf);
   }
   hipStreamSynchronize(c->stream);
   if (c->prof) harvest(c);
@@ -1365,8 +1218,9 @@ int gpf_kmeans_step(gpf_ctx* c, const double* centers, int k, int update, int* l
   if (!c) return GPF_BAD_ARG;
   if (c->km_n <= 0) return bad_arg(c, "gpf_kmeans_step: call gpf_kmeans_set first");
   const int d = c->km_d;
-  if (k <= 0 || (int64_t)k * d > gpf::KM_MAXKD || !centers || !labels || (update && (!sums || !counts)))
-    return bad_arg(c, "gpf_kmeans_step: bad arguments");
+  if (k <= 0 || !centers || !labels || (update && (!sums || !counts))) return bad_arg(c, "gpf_kmeans_step: bad arguments");
+  if ((int64_t)k * (d + 1) > gpf::KM_MAXKD)  // centres + norms in LDS (gpfit.kmeans falls back to the host fit)
+    return bad_arg(c, "gpf_kmeans_step: k x (d + 1) exceeds KM_MAXKD (8192)");
   hipSetDevice(c->device);
   if (k > c->km_kcap || d != c->km_cd) {  // the centre buffers are k x d: both sizes matter
     GPF_HIP(c, hipStreamSynchronize(c->stream));
@@ -1381,9 +1235,7 @@ int gpf_kmeans_step(gpf_ctx* c, const double* centers, int k, int update, int* l
   }
   const int64_t n = c->km_n;
   GPF_HIP(c, hipMemcpyAsync(c->km_c, centers, (size_t)k * d * 8, hipMemcpyHostToDevice, c->stream));
-  const size_t lds = (size_t)(k * d + k) * 8;
-  hipLaunchKernelGGL(gpf::k_km_assign, dim3((unsigned)((n + NTHR - 1) / NTHR)), dim3(NTHR), lds, c->stream, n, d, k,
-                     c->km_x, c->km_c, c->km_lab, c->km_dist);
+  gpf::launch_km_assign(c->stream, n, d, k, c->km_x, c->km_c, c->km_lab, c->km_dist);
   GPF_HIP(c, hipGetLastError());
   if (update) {
     hipLaunchKernelGGL(gpf::k_km_sums, dim3((unsigned)k), dim3(NTHR), 0, c->stream, n, d, c->km_x, c->km_lab, c->km_sums,
@@ -1587,7 +1439,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     if ((la_prev[l.g] & 1) && !(l.la & 2))
       return plan_fail(msg, msg_len, "J=%d g=%d: look-ahead partials of launch J-1 left unused", l.J, l.g);
     la_prev[l.g] = l.la;
-    if (l.ro && (!l.ed || !l.sy || l.split != gpf::SPLIT_NONE || l.grp != 0 || l.J < 1 || 3 * l.gc > 256 ||
+    if (l.ro && (ng != 1 || !l.ed || !l.sy || l.split != gpf::SPLIT_NONE || l.grp != 0 || l.J < 1 || 3 * l.gc > 256 ||
                  l.grid != (unsigned)(l.gc * (nt - 1) + 2 * l.gc)))
       return plan_fail(msg, msg_len, "J=%d g=%d: reordered dispatch out of place", l.J, l.g);
     std::vector<int> lawg((size_t)l.gc, 0);

@@ -69,7 +69,6 @@ SIGNATURES = {
     "gpf_bench_clock": (ctypes.c_int, [_vp, _dp]),
     "gpf_kmeans_set": (ctypes.c_int, [_vp, _dp, ctypes.c_int64, ctypes.c_int]),
     "gpf_kmeans_step": (ctypes.c_int, [_vp, _dp, ctypes.c_int, ctypes.c_int, _ip, _dp, _dp, _dp]),
-    "gpf_cu_partition": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]),
 }
 
 _LIB = None
@@ -114,16 +113,6 @@ def plan_check(particles, nt):
     keys = ("launches", "workgroups", "whole_tiles", "split_tiles", "S", "Smax", "groups", "diag_workgroups",
             "syrk_workgroups", "persistent")
     return dict(zip(keys, list(stats)))
-
-
-def cu_partition(ncu, vcu):
-    """The CU indices gpf_predict's V stream gets under GPF_PRED_VCU=vcu (gpf_cu_partition)."""
-    words = (int(ncu) + 31) // 32
-    mask = (ctypes.c_uint32 * words)()
-    n = load_library().gpf_cu_partition(int(ncu), int(vcu), mask, words)
-    if n < 0:
-        raise ValueError("gpf_cu_partition: bad arguments")
-    return [i for i in range(ncu) if (mask[i >> 5] >> (i & 31)) & 1]
 
 
 def _f64(a):

@@ -16,6 +16,13 @@ reference's on its fixtures (F10) and on the test sweep; the centres to rounding
 """
 import numpy as np
 
+KM_MAXKD = 8192  # gpf_kmeans_step's LDS bound on k x (d + 1) (csrc/gpf_kmeans.hip)
+
+
+def fits_device(n_clusters, d):
+    """Whether gpf_kmeans_step can stage n_clusters centres of dimension d (and their norms)."""
+    return n_clusters * (d + 1) <= KM_MAXKD
+
 
 def kmeans_fit(ctx, X, n_clusters, *, random_state=0, max_iter=300, tol=1e-4):
     """labels, cluster_centers_ of KMeans(n_clusters, n_init='auto', random_state).fit(X) (X: n x d)."""

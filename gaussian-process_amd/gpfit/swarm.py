@@ -220,14 +220,15 @@ class Swarm:
 def prepare(x_known, y_known, e_known, *, max_points=MAX_POINTS, verbose=True, ctx=None):
     """KMeans subsample above max_points (:25-47), bounds (:56-61), sigma grid (:66-67). With a GPU
     context the KMeans fit's Lloyd iterations run on it (gpfit.kmeans, r4); without one (the
-    injected-evaluator path of the CPU tests) sklearn's fit runs on the host, as in the reference."""
+    injected-evaluator path of the CPU tests), or with more centres than the device step stages
+    (max_points x (d + 1) > 8192), sklearn's fit runs on the host, as in the reference."""
     if x_known.shape[1] > max_points:
         if verbose:
             print(f"Dataset too large ({x_known.shape[1]} points). Subsampling to {max_points} for hyperparameter optimisation.")
-        if ctx is not None:
-            from .kmeans import kmeans_representatives_gpu
+        from .kmeans import fits_device, kmeans_representatives_gpu
+        if ctx is not None and fits_device(max_points, x_known.shape[0]):
             x_known, y_known, e_known = kmeans_representatives_gpu(ctx, x_known, y_known, e_known, max_points)
-        else:
+        else:  # no device, or more centres than gpf_kmeans_step stages in LDS (ADVICE r4): sklearn's fit
             x_known, y_known, e_known = kmeans_representatives(x_known, y_known, e_known, max_points)
     lower, upper = search_bounds(x_known)
     sigma_vals, expected = sigma_grid()

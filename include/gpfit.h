@@ -114,7 +114,8 @@ int gpf_hull_fetch(gpf_ctx* ctx, double* out);
  * n_init='auto', random_state=0)). gpf_kmeans_set keeps n points x d
  * (row-major, already centred by their mean as sklearn's fit does) on the device. One
  * gpf_kmeans_step = the E-step (and with update != 0 the M-step sums) of sklearn's
- * lloyd_iter_chunked_dense with unit weights against k centres (k x d, row-major, k*d <= 8192):
+ * lloyd_iter_chunked_dense with unit weights against k centres (k x d, row-major; k*(d+1) <= 8192,
+ * else GPF_BAD_ARG and gpfit.kmeans keeps sklearn's host fit):
  * labels[i] = the first j minimising ||c_j||^2 - 2 x_i.c_j; sums (k x d) and counts (k) of each
  * cluster's members; dist[i] = ||x_i - c_labels[i]||^2 (optional, may be NULL). The host runs
  * sklearn's loop around it (gaussian-process_amd/gpfit/kmeans.py). */
@@ -230,13 +231,6 @@ const char* gpf_build_info(void);
  * workgroups, SYRK workgroups (items), persistent (0/1). Returns GPF_OK, or
  * GPF_BAD_ARG with a description of the first violation in msg. */
 int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len);
-
-/* Host-only: the CU mask (words x 32 bits, bit i = CU i) that gpf_predict gives its V stream
- * under GPF_PRED_VCU = vcu (the factorisation's stream gets the complement): CU i is the V set's
- * if its rank in an order that deals consecutive CUs over the 8 XCDs whether the mask bits
- * interleave over the XCDs (XCD = i % 8) or block them (XCD = i / 32) is < vcu. Returns the
- * number of CUs set, or -1 on bad arguments. */
-int gpf_cu_partition(int ncu, int vcu, uint32_t* mask, int words);
 
 /* Self-test of the f64 MFMA fragment layout: C = A(16x4) B(4x16) on device,
  * compared on the host by the caller. a: 16x4 row-major, b: 4x16 row-major,

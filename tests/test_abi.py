@@ -87,19 +87,3 @@ def test_comm_transport_codes():
     assert lib.gpf_comm_open(None, 0, 1, b"127.0.0.1", 29999, L.GPF_COMM_HOST, ctypes.byref(out)) == L.GPF_OK
     assert out.value
     lib.gpf_comm_close(out)
-
-
-@pytest.mark.parametrize("vcu", [8, 64, 96, 128, 160])
-def test_prediction_cu_partition_is_even_over_xcds(vcu):
-    """gpf_predict's CU-partitioned pipeline (GPF_PRED_VCU) gives V a stream CU mask with vcu
-    CUs: a multiple of 8 CUs lands evenly on the 8 XCDs whether the mask bits interleave over the
-    XCDs (XCD = i % 8) or block them (XCD = i // 32), so neither V nor the factorisation is held
-    to a few XCDs' L2s."""
-    import gpfit._lib as L
-    cus = L.cu_partition(256, vcu)
-    assert len(cus) == len(set(cus)) == vcu and all(0 <= i < 256 for i in cus)
-    for xcd in (lambda i: i % 8, lambda i: i // 32):
-        per = [sum(1 for i in cus if xcd(i) == x) for x in range(8)]
-        assert per == [vcu // 8] * 8, per
-    assert sorted(L.cu_partition(256, 256)) == list(range(256))
-    assert len(L.cu_partition(80, 16)) == 16

@@ -147,3 +147,26 @@ def test_kmeans_fit_keeps_the_reference_points_f10():
         xs, ys, es = kmeans_representatives_gpu(_NumpyKMeansSteps(), _fx(x), y, e, 100)
         idx = f[f"c{i}_idx"]
         assert np.array_equal(xs, x[:, idx]) and np.array_equal(ys, y[idx]) and np.array_equal(es, e[idx])
+
+
+def test_kmeans_above_device_cap_uses_host_fit():
+    """max_points x (d + 1) > 8192 (gpf_kmeans_step's LDS bound) keeps sklearn's host fit instead of
+    raising: prepare() with a context stand-in that must not be asked for a step; just
+    under the cap the device path (here its NumPy stand-in) is taken and keeps the same points."""
+    from gpfit.kmeans import fits_device
+    from gpfit.swarm import kmeans_representatives, prepare
+
+    class _Refuse(_NumpyKMeansSteps):
+        def kmeans_step(self, *a, **k):
+            raise AssertionError("device KMeans step above its cap")
+
+    assert not fits_device(1000, 9) and not fits_device(300, 32) and fits_device(1000, 7)
+    rng = np.random.default_rng(3)
+    x = rng.uniform(size=(9, 1200))
+    y, e = np.sin(3 * x[0]), np.full(1200, 0.1)
+    xs, ys, es = prepare(x, y, e, max_points=1000, verbose=False, ctx=_Refuse())[:3]
+    want = kmeans_representatives(x, y, e, 1000)
+    assert np.array_equal(xs, want[0]) and np.array_equal(ys, want[1]) and np.array_equal(es, want[2])
+    x7 = x[:7, :1100]
+    xs7 = prepare(x7, y[:1100], e[:1100], max_points=1000, verbose=False, ctx=_NumpyKMeansSteps())[0]
+    assert np.array_equal(xs7, kmeans_representatives(x7, y[:1100], e[:1100], 1000)[0])
