@@ -20,8 +20,6 @@ typedef double d2 __attribute__((ext_vector_type(2)));  // plain vector type: SR
 constexpr int NTHR = 256;   // 4 waves of 64 lanes per workgroup (covariance / objective kernels)
 constexpr int DNTH = 512;   // 8 waves: the factorisation kernels (k_step, k_diag)
 constexpr int T = 128;      // factorisation block (block column width, padding granule)
-constexpr int H = 64;       // half block: the unblocked diagonal factor works on 64x64
-constexpr int LDH = H + 1;  // [row][k] stride of an LDS-resident 64x64 tile (odd: conflict-free b64 / read2_b64)
 constexpr int DMAX = 32;    // max input dimensionality of the covariance builders
 constexpr int KGRID_MAX = 4096;
 
@@ -37,9 +35,6 @@ __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
 template <int TM> struct TileCfg;
 template <> struct TileCfg<128> {  // the factorisation / prediction GEMMs: 8 waves, 128x16 per wave
   static constexpr int KC = 16, NW = 8, WR = 1, WC = 8;
-};
-template <> struct TileCfg<64> {   // LDS-resident 64x64 products inside the diagonal factor: 8 waves, 32x16 each
-  static constexpr int KC = 32, NW = 8, WR = 2, WC = 4;
 };
 
 template <int TM> struct Geo {
@@ -579,62 +574,6 @@ __device__ __forceinline__ void trmm_acc(d4 (&out)[2], const Acc<128>& X, const 
   }
 }
 
-// 64x64x64 GEMM with both operands resident in LDS (8 waves, 32x16 each):
-//   A (r,k) at sA[r*la + k];  B (k,c) at sB[c*lb + k] (!NN) or sB[k*lb + c] (NN).
-// TRI: known-zero structure (as in the streamed GEMMs): each wave runs only the k-steps whose
-// 16x16x4 blocks can be non-zero (wave-uniform bounds; 16-aligned blocks, so every skipped
-// MFMA would add exact zeros: results are bitwise those of the dense loop).
-template <bool NN, int TRI = TRI_NONE>
-__device__ __forceinline__ void gemm_lds64(Acc<64>& acc, const double* sA, int la, const double* sB, int lb,
-                                           const Quad<64>& qd) {
-  constexpr int MBR = Geo<64>::MBR, MBC = Geo<64>::MBC;
-  static_assert(MBR == 2 && MBC == 1, "wave sub-tile of the 64-tile GEMM");
-  const int lr = qd.lane & 15, lk = qd.lane >> 4;
-  int k0 = 0, k1 = H;
-  if (TRI == TRI_B_KLEC) k1 = qd.cb + 16;           // B(k,c) = 0 for k > c
-  if (TRI == TRI_B_KGEC) k0 = qd.cb;                // B(k,c) = 0 for k < c
-  if (TRI == TRI_A_KLER) k1 = qd.rb + 32;           // A(r,k) = 0 for k > r (row block 0 stops at rb + 16)
-  const bool live0 = TRI != TRI_C_LOWER || qd.cb < qd.rb + 16;  // lower-only output: row block 0
-  const bool live1 = TRI != TRI_C_LOWER || qd.cb < qd.rb + 32;  // ... row block 1
-  // every bound is a multiple of 16: 16-deep blocks of 4 k-steps (an exact unroll by 4; a
-  // `#pragma unroll 4` on the runtime-bounded loop could not be honoured)
-#pragma unroll 1
-  for (int k16 = k0; k16 < k1; k16 += 16)
-#pragma unroll
-  for (int ks = k16; ks < k16 + 16; ks += 4) {
-    double a[MBR], b[MBC];
-#pragma unroll
-    for (int mi = 0; mi < MBR; ++mi) a[mi] = sA[(qd.rb + mi * 16 + lr) * la + ks + lk];
-#pragma unroll
-    for (int ni = 0; ni < MBC; ++ni) {
-      if (!NN)
-        b[ni] = sB[(qd.cb + ni * 16 + lr) * lb + ks + lk];
-      else
-        b[ni] = sB[(ks + lk) * lb + qd.cb + ni * 16 + lr];
-    }
-    const bool m0 = TRI == TRI_A_KLER ? ks < qd.rb + 16 : live0;
-    if (m0) acc.v[0][0] = mfma(a[0], b[0], acc.v[0][0]);
-    if (live1) acc.v[1][0] = mfma(a[1], b[0], acc.v[1][0]);
-  }
-}
-
-// Coalesced 64x64 global tile -> LDS [row][col] with stride ld, 16 B per lane (DNTH threads).
-// (The global tile pointers of these helpers are laundered: factor128 loads and later stores the
-// same 64x64 tiles, and with the addresses shared the compiler kept them live across the factor
-// and spilled them.)
-__device__ __forceinline__ void tile64_to_lds(double* s, int ld, const double* __restrict__ g, size_t gld) {
-  const int tid = threadIdx.x;
-  g = launder(g);
-#pragma unroll
-  for (int u = 0; u < 2048 / DNTH; ++u) {
-    const int q = tid + DNTH * u;
-    const int row = q >> 5, c2 = q & 31;
-    const d2 v = *reinterpret_cast<const d2*>(g + (size_t)row * gld + 2 * c2);
-    s[row * ld + 2 * c2] = v.x;
-    s[row * ld + 2 * c2 + 1] = v.y;
-  }
-}
-
 // Global store of one double; WT: write-through (agent-scope relaxed atomic store: the line is
 // written to memory without an L2 write-back fence), for data another workgroup of the same
 // launch reads after a flag hand-off (the early diagonal factor, k_step).
@@ -645,47 +584,6 @@ __device__ __forceinline__ void gst(double* p, double v) {
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else
     *p = v;
-}
-
-// LDS 64x64 -> global, optionally zeroing the strict upper triangle.
-template <bool WT = false>
-__device__ __forceinline__ void lds_to_tile64(double* __restrict__ g, size_t gld, const double* s, int ld,
-                                              bool lower_only) {
-  const int tid = threadIdx.x;
-  g = launder(g);
-#pragma unroll
-  for (int u = 0; u < 2048 / DNTH; ++u) {
-    const int q = tid + DNTH * u;
-    const int row = q >> 5, c2 = q & 31;
-    d2 v;
-    v.x = (lower_only && 2 * c2 > row) ? 0.0 : s[row * ld + 2 * c2];
-    v.y = (lower_only && 2 * c2 + 1 > row) ? 0.0 : s[row * ld + 2 * c2 + 1];
-    double* gp = g + (size_t)row * gld + 2 * c2;
-    if (WT) {
-      gst<true>(gp, v.x);
-      gst<true>(gp + 1, v.y);
-    } else {
-      *reinterpret_cast<d2*>(gp) = v;
-    }
-  }
-}
-
-template <bool WT = false>
-__device__ __forceinline__ void zero_tile64(double* __restrict__ g, size_t gld) {
-  const int tid = threadIdx.x;
-  g = launder(g);
-#pragma unroll
-  for (int u = 0; u < 2048 / DNTH; ++u) {
-    const int q = tid + DNTH * u;
-    const int row = q >> 5, c2 = q & 31;
-    double* gp = g + (size_t)row * gld + 2 * c2;
-    if (WT) {
-      gst<true>(gp, 0.0);
-      gst<true>(gp + 1, 0.0);
-    } else {
-      *reinterpret_cast<d2*>(gp) = d2{0.0, 0.0};
-    }
-  }
 }
 
 // Shader-clock probe of the factorisation kernels (profiling passes only; clk == nullptr

@@ -8,21 +8,19 @@
 // latency-bound launch, ~48 us).
 //
 // The block is an 8 x 8 grid of 16 x 16 blocks, right-looking, one 16-wide block column ("panel")
-// per step k, everything LDS-resident (the 36 lower blocks, 72 KiB) or in registers:
-//   P_k  wave 0 factors panel k on its own: the rows of blocks k .. k+3 (lane = row, registers
-//        only: pivot by v_readlane, 1/sqrt by v_rsq + Newton, rank-1 updates with the column's
-//        entries by v_readlane), carrying the forward substitution of y (z_k) and the inverse of
-//        the diagonal block X_kk = L_kk^-1 ([A | I] elimination, lane = column) along;
-//   Q_k  (one barrier later, the chain) every wave: the next panel's blocks A(i,k+1) -= L(i,k)
-//        L(k+1,k)^T for the window rows i <= k+4, and the rows below wave 0's 64-row window
-//        (k <= 3) by MFMA: L(i,k)^T = X_kk A(i,k)^T, their y update y_i -= L(i,k) z_k;
+// per step k, the 36 lower blocks LDS-resident (stride 17: 76.5 KiB) or in registers:
+//   P_k  wave 0 factors the diagonal block A_kk on its own (db_panel): L_kk, X_kk = L_kk^-1 and
+//        z_k in one [A | I | y] elimination, lane = row / column;
+//   Q_k  (one barrier later) the rows below it by MFMA, L(i,k)^T = X_kk A(i,k)^T, their y update
+//        y_i -= L(i,k) z_k, and on the chain the next diagonal block A(k+1,k+1) -= L(k+1,k)
+//        L(k+1,k)^T;
 //   and, beside wave 0's next panel (P_{k+1}), on waves 1-3 and 5-7 (not wave 4: FP64 MFMAs and
 //   VALU share a SIMD's FP64 units, and wave 4 shares wave 0's SIMD):
-//        the rest of step k's trailing update A(i,j) -= L(i,k) L(j,k)^T (k+2 <= j <= i);
+//        the rest of step k's trailing update A(i,j) -= L(i,k) L(j,k)^T (k+1 <= j <= i);
 //        step k of the inverse, right-looking by block columns: the owner wave of column j of
 //        X = L^-1 (its blocks in registers, the accumulator layout) finalises X_kj = -X_kk S_kj
-//        (j < k; X_kk: the panel's) and adds S_ij += L(i,k) X_kj for i > k, stores X_kj (U_JJ) and
-//        adds its share of the column partials.
+//        (j < k) and adds S_ij += L(i,k) X_kj for i > k, stores X_kj (U_JJ) and adds its share
+//        of the column partials.
 // Two barriers per panel. Every product is a 16x16x16 MFMA product (4 v_mfma_f64_16x16x4) with
 // operands from LDS or from the owner's accumulators (register e of a 16x16 accumulator is the
 // B operand of k-step e: X_kj and L(i,k)^T never move). Fixed assignment of work to waves and a
@@ -32,6 +30,59 @@
 #include "gpf_common.hip"
 
 namespace gpf {
+
+#ifdef GPF_DB_STAMPS
+// Probe builds only (scripts/probes/f128_probe.hip): s_memtime of wave W's lane 0 in workgroup 0 at
+// phase ends, [W][slot]: slot 2k: after panel k / step k-1's work, 2k+1: after Q_k; 16: end.
+__device__ unsigned long long g_db_stamps[8][20];
+#define DB_STAMP(W, i)                                                              \
+  do {                                                                              \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) {                               \
+      unsigned long long t_;                                                        \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");    \
+      g_db_stamps[W][i] = t_;                                                       \
+    }                                                                               \
+  } while (0)
+#else
+#define DB_STAMP(W, i) \
+  do {                \
+  } while (0)
+#endif
+
+// The diagonal-block routines run on all DNTH (= 512) threads of the factorisation workgroups
+// (k_diag, and fused or as the early diagonal workgroup in k_step / k_factor).
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const long long i = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)i, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(i >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Barrier for LDS-only hand-offs between the waves of the diagonal factor: every wave's LDS
+// operations retired, then s_barrier (the asm's memory clobber keeps the compiler from moving
+// memory operations across it). Unlike __syncthreads() (a workgroup-scope release fence) it does
+// not wait for the wave's outstanding global stores, so the L/U tile stores of the factor drain
+// behind its LDS phases instead of stalling every barrier.
+__device__ __forceinline__ void lsync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// 1/sqrt(p) for the pivots of the diagonal factor: v_rsq_f64 and two Newton steps
+// (y += y (1/2 - p/2 y^2)), a short dependent chain instead of the ~25 ops of a correctly
+// rounded sqrt followed by a division; within a few ulp of 1/sqrt(p).
+__device__ __forceinline__ double rsqrt_nr1(double p) {  // (probe A/B: one Newton step)
+  double y = __builtin_amdgcn_rsq(p);
+  const double t = fma(-((0.5 * p) * y), y, 0.5);
+  return fma(y, t, y);
+}
+__device__ __forceinline__ double rsqrt_nr(double p) {
+  double y = __builtin_amdgcn_rsq(p);
+  const double h = 0.5 * p;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const double t = fma(-(h * y), y, 0.5);
+    y = fma(y, t, y);
+  }
+  return y;
+}
 
 constexpr int DB_LD = 17;                   // row stride of a 16x16 block in LDS (doubles)
 constexpr int DB_BLK = 16 * DB_LD;          // doubles per block
@@ -99,7 +150,7 @@ __device__ __forceinline__ d4 db_mul_ax(d4 acc, const double* A, const d4& X) {
   return acc;
 }
 
-// ---- static work assignment (compile-time k, block indices; runtime wave) ----
+// ---- static work assignment (compile-time k, block indices, waves) ----
 // owner wave of column j of X (SIMD s holds waves s and s + 4): columns 0, 3, 6 on SIMD 1, 1, 4, 7
 // on SIMD 2, 2, 5 on SIMD 3, so that each step's active columns spread over the three SIMDs
 __host__ __device__ constexpr int db_col_wave(int j) {
@@ -107,9 +158,11 @@ __host__ __device__ constexpr int db_col_wave(int j) {
 }
 // products the owner of column j does in step t of the inverse (finalise + contributions)
 __host__ __device__ constexpr int db_x_work(int t, int j) { return j > t ? 0 : (j < t ? 1 : 0) + (7 - t); }
-// the trailing-update blocks of step k beside panel k+1: (i, j) with k+2 <= j <= i, and the blocks
-// (i, k+1) below panel k+1's window (i >= k+5; the window's blocks are Q_k's)
-__host__ __device__ constexpr bool db_in_bulk(int k, int i, int j) { return j >= k + 1 && i >= j && i < 8 && (j >= k + 2 || i >= k + 5); }
+// the trailing-update blocks of step k beside panel k+1: every (i, j), k+1 <= j <= i, but the next
+// diagonal block (k+1, k+1), which Q_k updates on the chain
+__host__ __device__ constexpr bool db_in_bulk(int k, int i, int j) {
+  return j >= k + 1 && i >= j && i < 8 && !(i == k + 1 && j == k + 1);
+}
 // owner wave of the trailing-update block (i, j) of step k: greedy in a fixed block order onto the
 // least-loaded SIMD (1-3) counting step k's inverse work, then its less-loaded wave
 __host__ __device__ constexpr int db_bulk_wave(int k, int bi, int bj) {
@@ -127,94 +180,180 @@ __host__ __device__ constexpr int db_bulk_wave(int k, int bi, int bj) {
     }
   return -1;
 }
-// Q_k items: m = 0: rows k+4 (TRSM + the next panel's update; k <= 3); m = 1..3: the next panel's
-// blocks i = k + m (i <= 7); m = 4..6: rows i = k + 1 + m below the window (TRSM only; i <= 7).
-// Item m runs on wave db_q_wave(m): the first four on four different SIMDs.
-__host__ __device__ constexpr int db_q_wave(int m) {
-  return m == 0 ? 1 : m == 1 ? 2 : m == 2 ? 3 : m == 3 ? 0 : m == 4 ? 5 : m == 5 ? 6 : 7;
+// Q_k: the block rows i = k+1 .. 7 below the panel, one TRSM each; row k+1 (which also updates the
+// next diagonal block: the chain) on wave 4, alone on its SIMD while wave 0 waits, the others on
+// waves 1-3, 5-7
+__host__ __device__ constexpr int db_q_wave(int k, int i) {
+  return i == k + 1 ? 4 : (i - k - 2 == 0 ? 1 : i - k - 2 == 1 ? 2 : i - k - 2 == 2 ? 3 : i - k - 2 == 3 ? 5 : i - k - 2 == 4 ? 6 : 7);
 }
 
 // ---- the panel: wave 0 ----
-// Rows R = 16 k + r of blocks k .. k+3 (lane r < 64, R < 128): columns 16k .. 16k+15. Lane q holds
-// row 16 k + q of the diagonal block; its pivot reaches every lane by v_readlane. The rank-1
-// update of column q takes L(s, q) (s > q) from lane s by v_readlane, one fma per entry; the same
-// scalars finish X_kk's rows (lane c < 16 holds column c) and the forward substitution of y.
-// Writes L to LDS (blocks i > k) and global (rows R), X_kk to LDS (the diagonal slot) and global
-// (U), z_k / the reduced y of the window to LDS. Returns whether a pivot was not > 0.
-template <bool WT>
+// The 16 x 16 diagonal block A_kk, as an [A | I | y] elimination on one wave: lane r < 16 holds row r
+// of A (columns <= r), lane 16 + c column c of X_kk = L_kk^-1 (the identity to start), lane 32 the
+// block's 16 entries of y. Every role takes the same update, x[s] -= m * L(s, q), with its
+// multiplier m (A: L(r, q); X: X(q, c); y: z_q) — one fma per entry and column for the whole wave.
+// Column q: the pivot from lane q (v_readlane), 1/sqrt by v_rsq + Newton, the scaled column; the
+// entry the next pivot needs, L(q+1, q), by v_readlane (the chain); the others go through LDS
+// (column q written by lanes 0..15, read back as broadcasts) and are applied one column later,
+// beside the next pivot's chain: a v_readlane pair per entry, its hazard wait and a scalar-operand
+// fma per entry (round 4) cost ~550 cycles per column, issue-bound. Writes L_kk (zeros above the
+// diagonal) to global, X_kk to the LDS diagonal slot (its column buffer during the panel) and to
+// U, z_k to the LDS y. Returns whether a pivot was not > 0.
+#ifndef GPF_DB_PANEL
+#define GPF_DB_PANEL 0  // probe A/B: 0 = LDS broadcast, one column deferred; 1 = v_readlane for every entry
+#endif
+template <bool WT, int VAR = GPF_DB_PANEL>
 __device__ __forceinline__ bool db_panel(double* lds, int k, double* __restrict__ Lt, double* __restrict__ Ut, size_t ld) {
   const int r = threadIdx.x & 63;
-  const int R = 16 * k + r;
-  const bool live = R < T;
-  const int rr = r & 15;
-  double* blk = lds + db_bid(live ? k + (r >> 4) : k, k) * DB_BLK;
-  double a[16], w[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) a[c] = (live && (r >= 16 || c <= rr)) ? blk[db_off(rr, c)] : 0.0;
-  double yr = live ? lds[DB_Y + R] : 0.0;
+  double* blk = lds + db_bid(k, k) * DB_BLK;  // A_kk; the column buffer [q][s] during the panel; X_kk
+  const bool arow = r < 16, xcol = r >= 16 && r < 32, ylane = r == 32;
   int ro = r;
-  asm volatile("" : "+v"(ro));  // (an opaque lane index: the identity below is not kept live across panels)
+  asm volatile("" : "+v"(ro));  // (an opaque lane index: the initial values are not kept live across panels)
+  double x[16];
 #pragma unroll
-  for (int s = 0; s < 16; ++s) w[s] = (s == ro) ? 1.0 : 0.0;
+  for (int c = 0; c < 16; ++c) {  // (every lane loads, then selects: no divergent loads)
+    double va = blk[db_off(ro & 15, c)], vy = lds[DB_Y + 16 * k + c];
+    asm volatile("" : "+v"(va), "+v"(vy));  // (keeps the loads from being sunk into per-role branches)
+    x[c] = arow ? (c <= ro ? va : 0.0) : (xcol ? (c == ro - 16 ? 1.0 : 0.0) : (ylane ? vy : 0.0));
+  }
   bool bad = false;
+  double mprev = 0.0, cv[16];
+  if constexpr (VAR == 4) {
+    // the uniform pivot chain (below) and few VALU instructions per column: the entries s = q+1,
+    // q+2 of column q by v_readlane (the next alpha / beta need them one step later), the others
+    // through LDS (column q written by the A lanes, read back as broadcasts, applied one step later:
+    // a full column of slack for the LDS round trip)
+    double p = readlane_f64(x[0], 0);
+    double alpha = readlane_f64(x[0], 1), beta = readlane_f64(x[1], 1);
+    double inv = rsqrt_nr(p);
+    bad = !(p > 0.0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const double m = (arow && r < q) ? 0.0 : x[q] * inv;
+      x[q] = m;
+      double inv_next = 0.0;
+      if (q < 15) {  // the chain
+        const double l1 = alpha * inv;
+        const double p1 = fma(-l1, l1, beta);
+        bad = bad | !(p1 > 0.0);
+        inv_next = rsqrt_nr(p1);
+      }
+      if (q + 3 < 16 && arow) blk[q * 16 + r] = m;  // column q for the entries s >= q+3
+#pragma unroll
+      for (int s = q + 1; s < 16 && s <= q + 2; ++s) x[s] = fma(-m, readlane_f64(m, s), x[s]);
+      if (q >= 1) {  // column q-1's entries s >= q+2, read back at step q-1
+#pragma unroll
+        for (int s = q + 2; s < 16; ++s) {
+          x[s] = fma(-mprev, cv[s], x[s]);
+          asm volatile("" : "+v"(x[s]));
+        }
+      }
+      if (q + 2 < 16) {  // the next step's alpha, beta: row q+2's entries in columns q+1, q+2
+        alpha = readlane_f64(x[q + 1], q + 2);
+        beta = readlane_f64(x[q + 2], q + 2);
+      }
+      if (q + 3 < 16) {
+#pragma unroll
+        for (int s = q + 3; s < 16; ++s) cv[s] = blk[q * 16 + s];  // (broadcasts)
+      }
+      mprev = m;
+      inv = inv_next;
+    }
+  } else if constexpr (VAR >= 2) {
+    // The pivot chain on uniform values, off the lanes: p_{q+1} = beta - (alpha inv_q)^2 with alpha,
+    // beta = row q+1's entries in columns q and q+1 after the columns < q (read from lane q+1 one
+    // step ahead) — the same operations lane q+1 applies to its own diagonal entry, so bitwise the
+    // same pivot; per column the chain is a mul, an fma and 1/sqrt, no cross-lane traffic.
+    double p = readlane_f64(x[0], 0);
+    double alpha = readlane_f64(x[0], 1), beta = readlane_f64(x[1], 1);
+    double inv = VAR == 3 ? rsqrt_nr1(p) : rsqrt_nr(p);
+    bad = !(p > 0.0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const double m = (arow && r < q) ? 0.0 : x[q] * inv;
+      x[q] = m;
+      double inv_next = 0.0;
+      if (q < 15) {
+        const double l1 = alpha * inv;
+        const double p1 = fma(-l1, l1, beta);
+        bad = bad | !(p1 > 0.0);
+        inv_next = VAR == 3 ? rsqrt_nr1(p1) : rsqrt_nr(p1);
+      }
+#pragma unroll
+      for (int s = q + 1; s < 16; ++s) {
+        x[s] = fma(-m, readlane_f64(m, s), x[s]);
+        if (s == q + 2 && q + 2 < 16) {  // the next step's alpha, beta from lane q+2
+          alpha = readlane_f64(x[q + 1], q + 2);
+          beta = readlane_f64(x[q + 2], q + 2);
+        }
+        if (((s - q) & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+      }
+      inv = inv_next;
+    }
+  } else
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
-    const double p = readlane_f64(a[q], q);
+    const double p = readlane_f64(x[q], q);
     bad = bad | !(p > 0.0);
     const double inv = rsqrt_nr(p);
-    // lanes r < q hold exact zeros in column q (the diagonal block's upper triangle was zeroed and
-    // every update of it is by a zero multiplier), lane q its pivot: no selects
-    const double l = a[q] * inv;
-    a[q] = l;
-    const double zq = readlane_f64(yr, q) * inv;
-    yr = (r == q) ? zq : fma(-l, zq, yr);
-    const double wq = w[q] * inv;
-    w[q] = wq;
-    asm volatile("" : "+v"(w[q]));  // (w is stored only by lanes < 16: keep its updates from sinking there)
+    const double m = (arow && r < q) ? 0.0 : x[q] * inv;
+    x[q] = m;
+    if constexpr (VAR == 1) {
 #pragma unroll
-    for (int s = q + 1; s < 16; ++s) {
-      const double lsq = readlane_f64(l, s);
-      a[s] = fma(-l, lsq, a[s]);
-      w[s] = fma(-lsq, wq, w[s]);
-      asm volatile("" : "+v"(w[s]));
-      if (((s - q) & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+      for (int s = q + 1; s < 16; ++s) {
+        x[s] = fma(-m, readlane_f64(m, s), x[s]);
+        if (((s - q) & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+      }
+      continue;
     }
-  }
-  if (live) {
-    if (r >= 16) {
-#pragma unroll
-      for (int c = 0; c < 16; ++c) blk[db_off(rr, c)] = a[c];
+    if (q < 15) {  // the next pivot's entry first
+      const double l1 = readlane_f64(m, q + 1);
+      x[q + 1] = fma(-m, l1, x[q + 1]);
     }
-    double* gl = Lt + (size_t)R * ld + 16 * k;
+    if (q < 14 && arow) blk[q * 16 + r] = m;  // column q for the entries s >= q+2
+    if (q >= 1) {  // column q-1's deferred entries s >= q+1 (read back at step q-1)
 #pragma unroll
-    for (int c = 0; c < 16; c += 2) *reinterpret_cast<d2*>(gl + c) = d2{a[c], a[c + 1]};
-    lds[DB_Y + R] = yr;
+      for (int s = q + 1; s < 16; ++s) {
+        x[s] = fma(-mprev, cv[s], x[s]);
+        asm volatile("" : "+v"(x[s]));  // (applied here: sunk to each entry's next use, the read-back
+                                        // values of every column stayed live and spilled)
+      }
+    }
+    if (q < 14) {
+#pragma unroll
+      for (int s = q + 2; s < 16; ++s) cv[s] = blk[q * 16 + s];  // (uniform addresses: broadcasts)
+    }
+    mprev = m;
   }
-  if (r < 16) {  // X_kk: lane r holds column r
-    double* xs = lds + db_bid(k, k) * DB_BLK;
-    double* gu = Ut + (size_t)(16 * k) * ld + 16 * k + r;
+  // (the diagonal row's own entries right of its pivot took updates with m = L(q, q): not stored)
+  if (arow) {
+    double* gl = Lt + (size_t)(16 * k + r) * ld + 16 * k;
+#pragma unroll
+    for (int c = 0; c < 16; c += 2) *reinterpret_cast<d2*>(gl + c) = d2{c <= r ? x[c] : 0.0, c + 1 <= r ? x[c + 1] : 0.0};
+  }
+  if (xcol) {  // X_kk: lane 16 + c holds column c
+    const int c = r - 16;
+    double* gu = Ut + (size_t)(16 * k) * ld + 16 * k + c;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      xs[db_off(s, r)] = w[s];
-      gst<WT>(gu + (size_t)s * ld, w[s]);
+      blk[db_off(s, c)] = x[s];
+      gst<WT>(gu + (size_t)s * ld, x[s]);
     }
+  }
+  if (ylane) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) lds[DB_Y + 16 * k + s] = x[s];
   }
   return bad;
 }
 
-// Q_k item m on this wave (see db_q_wave): the chain between panels k and k+1
+// Q_k, block row i > k: L(i,k)^T = X_kk A(i,k)^T (the B operand A(i,k)^T is the A-operand read of
+// A(i,k)), y_i -= L(i,k) z_k, L(i,k) to LDS and L; row k+1 then updates the next diagonal block
+// A(k+1,k+1) -= L(k+1,k) L(k+1,k)^T (its A operand: the rows just stored, read back by this wave).
 template <bool WT>
-__device__ __forceinline__ void db_q_item(double* lds, int k, int m, double* __restrict__ Lt, size_t ld) {
+__device__ __forceinline__ void db_q_item(double* lds, int k, int i, double* __restrict__ Lt, size_t ld) {
   const int l = threadIdx.x & 63, c = l & 15, g = l >> 4;
-  auto B = [&](int i, int j) { return lds + db_bid(i, j) * DB_BLK; };
-  if (m >= 1 && m <= 3) {  // the next panel's block (k + m, k + 1), L(k + m, k) from wave 0
-    const int i = k + m;
-    double* C = B(i, k + 1);
-    db_st(C, db_sub_abt(db_ld(C), B(i, k), B(k + 1, k)));
-    return;
-  }
-  // rows below wave 0's window: L(i,k)^T = X_kk A(i,k)^T (B operand A(i,k)^T: the A-operand read of A(i,k))
-  const int i = m == 0 ? k + 4 : k + 1 + m;
+  auto B = [&](int ii, int jj) { return lds + db_bid(ii, jj) * DB_BLK; };
   double* Aik = B(i, k);
   double xa[4], ab[4];
   db_opa(B(k, k), xa);
@@ -227,15 +366,15 @@ __device__ __forceinline__ void db_q_item(double* lds, int k, int m, double* __r
 #pragma unroll
   for (int e = 0; e < 4; ++e) yp = fma(lt[e], lds[DB_Y + 16 * k + 4 * e + g], yp);
   yp = sum_lane_groups(yp);
-  if (m == 0) {  // the next panel's block (k+4, k+1)^T -= L(k+1,k) L(k+4,k)^T (lt: the B operands)
-    double* C = B(i, k + 1);
-    db_st_t(C, db_mul_ax<true>(db_ld_t(C), B(k + 1, k), lt));
-  }
   db_st_t(Aik, lt);  // L(i,k) for the trailing updates and the inverse
+  if (g == 0) lds[DB_Y + 16 * i + c] = lds[DB_Y + 16 * i + c] - yp;
+  if (i == k + 1) {
+    double* C = B(i, i);
+    db_st(C, db_mul_ax<true>(db_ld(C), Aik, lt));
+  }
   double* gl = Lt + (size_t)(16 * i + c) * ld + 16 * k + g;
 #pragma unroll
   for (int e = 0; e < 4; ++e) gl[4 * e] = lt[e];
-  if (g == 0) lds[DB_Y + 16 * i + c] = lds[DB_Y + 16 * i + c] - yp;
 }
 
 // Column j of X = L^-1 on its owner wave: S_ij (i > t) and the current X_tj in registers
@@ -312,10 +451,10 @@ __device__ __forceinline__ void db_bulk(double* lds) {
 template <bool WT, int k, int W>
 __device__ __forceinline__ void db_q(double* lds, double* __restrict__ Lt, size_t ld) {
 #pragma unroll
-  for (int m = 0; m < 7; ++m) {
-    const bool valid = m == 0 ? k <= 3 : (m <= 3 ? k + m <= 7 : k + 1 + m <= 7);
-    if (valid && db_q_wave(m) == W) db_q_item<WT>(lds, k, m, Lt, ld);
-  }
+  for (int i = k + 1; i < 8; ++i)
+    if constexpr (true) {
+      if (db_q_wave(k, i) == W) db_q_item<WT>(lds, k, i, Lt, ld);
+    }
 }
 
 // Each wave runs its own path (a compile-time wave: every ownership decision is static, so no
@@ -335,9 +474,11 @@ template <bool WT, int k>
 __device__ __forceinline__ void db_step_panel(double* lds, bool& bad, double* __restrict__ Lt, double* __restrict__ Ut,
                                               size_t ld) {
   bad = db_panel<WT>(lds, k, Lt, Ut, ld) | bad;
+  DB_STAMP(0, 2 * k);
   lsync();
   if constexpr (k < 7) {
     db_q<WT, k, 0>(lds, Lt, ld);
+    DB_STAMP(0, 2 * k + 1);
     lsync();
   }
 }
@@ -355,6 +496,7 @@ __device__ __forceinline__ void db_path_panel(double* lds, double* __restrict__ 
   db_step_panel<WT, 6>(lds, bad, Lt, Ut, ld);
   db_step_panel<WT, 7>(lds, bad, Lt, Ut, ld);
   db_publish<WT>(yseg, lds, pub, pub_val);
+  DB_STAMP(0, 16);
   if (bad && threadIdx.x == 0 && *info == 0) *info = 1;  // (the pivots are wave-uniform)
 }
 
@@ -367,9 +509,11 @@ __device__ __forceinline__ void db_step_other(double* lds, DbCol& c0, DbCol& c1,
     if constexpr (J0 >= 0 && J0 <= k - 1) db_x_step<WT, k - 1, J0>(c0, lds, Ut, ld);
     if constexpr (J1 >= 0 && J1 <= k - 1) db_x_step<WT, k - 1, J1>(c1, lds, Ut, ld);
   }
+  DB_STAMP(W, 2 * k);
   lsync();
   if constexpr (k < 7) {
     db_q<WT, k, W>(lds, Lt, ld);
+    DB_STAMP(W, 2 * k + 1);
     lsync();
   }
 }
@@ -391,6 +535,7 @@ __device__ __forceinline__ void db_path_other(double* lds, double* __restrict__ 
   // the last inverse step (X_7j = -X_77 S_7j)
   if constexpr (J0 >= 0) db_x_step<WT, 7, J0>(c0, lds, Ut, ld);
   if constexpr (J1 >= 0) db_x_step<WT, 7, J1>(c1, lds, Ut, ld);
+  DB_STAMP(W, 16);
   db_publish<WT>(yseg, lds, pub, pub_val);
   // column partials (after the publish: the launch's tiles do not read them): lane (g, c) holds
   // rows 4 e + g of every block of the column
@@ -425,9 +570,11 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
   // A's 36 lower blocks -> LDS (16 B per lane from memory), y -> LDS
   {
     const double* A = launder(Lt);
+    int to = tid;
+    asm volatile("" : "+v"(to));  // (the thread's load decode is formed here, not hoisted into the caller and spilled)
 #pragma unroll
     for (int u = 0; u < (DB_NB * 16 * 8) / DNTH; ++u) {
-      const int q = tid + DNTH * u, row = q >> 3, cp = q & 7;  // block row `row` (0..575), pair cp
+      const int q = to + DNTH * u, row = q >> 3, cp = q & 7;  // block row `row` (0..575), pair cp
       int bi = 0, rem = row;
 #pragma unroll
       for (int t = 1; t < 8; ++t)
@@ -455,6 +602,7 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
         gst<WT>(Ut + o + 1, 0.0);
       }
   }
+  DB_STAMP(0, 17);
   lsync();
   switch (wave) {
     case 0: db_path_panel<WT>(lds, Lt, Ut, ld, yseg, info, pub, pub_val); break;

@@ -23,494 +23,9 @@
 
 #pragma once
 #include "gpf_common.hip"
+#include "gpf_diag.hip"
 
 namespace gpf {
-
-#ifdef GPF_DIAG_STAMPS
-// Diagnostic build only (-DGPF_DIAG_STAMPS): thread 0 of workgroup 0 records s_memtime at
-// phase boundaries of factor128 into a buffer nothing else reads.
-// [0, 32): factor128 phases and the k = 4 details; [32, 32 + 16 * 16): per panel k of the last
-// factor64 call, slot 16 k + s: s < 8 wave s arriving at the panel barrier, 8 wave 0 leaving it,
-// 9 wave 0 after its strip update, 10 wave 0 after its panel factor, 11-13 update wave
-// DIAG_UW after its block slot j, 14 wave DIAG_UW leaving the barrier
-#ifndef DIAG_UW
-#define DIAG_UW 4
-#endif
-constexpr int DIAG_NSTAMPS = 32 + 16 * 16;
-__device__ unsigned long long g_diag_stamps[DIAG_NSTAMPS];
-#define DIAG_STAMP(i) DIAG_STAMP_T(i, 0)
-#define DIAG_STAMP_T(i, thr)                                                                       \
-  do {                                                                                           \
-    __builtin_amdgcn_sched_barrier(0);                                                           \
-    if (threadIdx.x == (thr) && blockIdx.x == 0 && blockIdx.y == 0) {  /* WG (p 0, w 0) */                                \
-      unsigned long long t_;                                                                     \
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                  \
-      g_diag_stamps[i] = t_;                                                                     \
-    }                                                                                            \
-    __builtin_amdgcn_sched_barrier(0);                                                           \
-  } while (0)
-#else
-#define DIAG_STAMP(i) \
-  do {               \
-  } while (0)
-#define DIAG_STAMP_T(i, thr) \
-  do {                      \
-  } while (0)
-#endif
-
-// The diagonal-block routines below run on all DNTH (= 512) threads of the
-// factorisation workgroups (k_diag and, fused, k_step).
-
-__device__ __forceinline__ double readlane_f64(double v, int lane) {
-  const long long i = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)i, lane);
-  const int hi = __builtin_amdgcn_readlane((int)(i >> 32), lane);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-// Barrier for LDS-only hand-offs between the waves of the diagonal factor: every wave's LDS
-// operations retired, then s_barrier (the asm's memory clobber keeps the compiler from moving
-// memory operations across it). Unlike __syncthreads() (a workgroup-scope release fence) it does
-// not wait for the wave's outstanding global stores, so the L/U tile stores of the factor drain
-// behind its LDS phases instead of stalling every barrier.
-__device__ __forceinline__ void lsync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// 1/sqrt(p) for the pivots of the diagonal factor: v_rsq_f64 and two Newton steps
-// (y += y (1/2 - p/2 y^2)), a short dependent chain instead of the ~25 ops of a correctly
-// rounded sqrt followed by a division; within a few ulp of 1/sqrt(p).
-__device__ __forceinline__ double rsqrt_nr(double p) {
-  double y = __builtin_amdgcn_rsq(p);
-  const double h = 0.5 * p;
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const double t = fma(-(h * y), y, 0.5);
-    y = fma(y, t, y);
-  }
-  return y;
-}
-
-constexpr int F64_BUF = 1024;  // LDS scratch of the diagonal factor (>= the 512-double reduction scratch)
-
-// ----------------------------------------------------------------------------
-// Blocked 64x64 factor: 16-wide block columns, right-looking.
-// Round 2's 4-wide panels passed 17 barriers and put the 4x4 pivot chain, the strip hand-off and
-// the update waves' serialised operand loads on every 4 columns (~3.4k cycles per panel,
-// profiles/r3/factor64_panel_stamps.txt). Here one wave factors a whole 16-column block column
-// (all rows below the diagonal at once, lane = row, registers only), and everything else is
-// 16x16x16 MFMA products between LDS blocks on the other waves, two barriers per block column:
-//   P1(k): wave 0 factors block column k (rows 16k..63) -> L_{.,k};   other waves, off the
-//          chain: the trailing updates of columns >= k+1 by block column k-1, X_{k-1,k-1} =
-//          L_{k-1,k-1}^-1 (one lane per column, forward substitution) and the inverse's products
-//   P2(k): the chain: A_{i,k+1} -= L_ik L_{k+1,k}^T (i > k, one wave per block); inverse products
-// then three short phases finish the last block row of X = L^-1:
-//   X_ij = -X_ii sum_{t=j}^{i-1} L_it X_tj   (block back-substitution, accumulated in X's blocks)
-// Deterministic (a fixed assignment of blocks to waves); not bitwise the 4-wide panels' result.
-// Waves w and w+4 share a SIMD: while wave 0 factors a block column, wave 4 stays idle and the
-// longest side job (the 16x16 inversion) runs on wave 6.
-// ----------------------------------------------------------------------------
-
-// D (+)= (NEG ? -1 : 1) A B for 16x16 blocks in LDS: A row-major [r][k] at pa; B as [k][c] at pb
-// (BT = false) or given transposed, Bt[c][k] at pb (BT = true); D row-major at pc (ACC: D is
-// also the addend). One wave.
-template <bool BT, bool NEG, bool ACC>
-__device__ __forceinline__ void mm16(double* pc, int ldc, const double* pa, int lda, const double* pb, int ldb) {
-  const int lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
-  double a[4], b[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    a[s] = pa[lr * lda + 4 * s + lk];
-    b[s] = BT ? pb[lr * ldb + 4 * s + lk] : pb[(4 * s + lk) * ldb + lr];
-  }
-  d4 acc;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) acc[e] = ACC ? pc[(lk + 4 * e) * ldc + lr] : 0.0;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) acc = NEG ? mfma_neg_a(a[s], b[s], acc) : mfma(a[s], b[s], acc);
-#pragma unroll
-  for (int e = 0; e < 4; ++e) pc[(lk + 4 * e) * ldc + lr] = acc[e];
-}
-
-// Block column k (rows 16k..63, columns 16k..16k+15, fully updated by the earlier columns) on one
-// wave: lane r holds row 16k + r. Column by column: pivot from lane q (readlane), 1/sqrt by
-// v_rsq + Newton, scale the column, rank-1 update of the lane's row (one fma per entry) with the
-// column's other diagonal-block entries (readlanes, a few per scheduling region: the scheduler
-// would otherwise hoist a column's readlanes together and spill the scalar registers; an LDS
-// column buffer instead measured more vector spills inside k_step). Writes L (zeros above the
-// diagonal of block (k,k)) and the pivots' reciprocal square roots dinv[16k + q]. Returns whether
-// a pivot was not > 0.
-__device__ __forceinline__ bool f64b_column(double* sA, int la, int k, double* dinv) {
-  const int r = threadIdx.x & 63;
-  const int R = 16 * k + r;
-  const bool live = R < 64;
-  double* row = sA + (live ? R : 0) * la + 16 * k;
-  double a[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) a[c] = (live && (r >= 16 || c <= r)) ? row[c] : 0.0;
-  bool bad = false;
-  double myinv = 0.0;  // lane q: the reciprocal square root of pivot q
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const double p = readlane_f64(a[q], q);
-    bad = bad | !(p > 0.0);
-    const double inv = rsqrt_nr(p);
-    const double l = (r > q) ? a[q] * inv : ((r == q) ? p * inv : 0.0);
-    a[q] = l;
-    myinv = (r == q) ? inv : myinv;
-#pragma unroll
-    for (int s = q + 1; s < 16; ++s) {
-      a[s] = fma(-l, readlane_f64(l, s), a[s]);
-      if (((s - q) & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  if (r < 16) dinv[16 * k + r] = myinv;
-  if (live) {
-#pragma unroll
-    for (int c = 0; c < 16; ++c) row[c] = (r < 16 && c > r) ? 0.0 : a[c];
-  }
-  return bad;
-}
-
-// X_kk = L_kk^-1 of a 16x16 lower-triangular block (zeros above its diagonal in LDS): lane c
-// (c < 16) forward-substitutes column c, x_i = -(sum_{j<i} L_ij x_j) * dinv_i, x_c = dinv_c (the
-// [A | I] elimination's X_qq); the L entries are uniform LDS reads. One wave; writes zeros above
-// the diagonal of X_kk. (A column-oriented variant, every later row taking x_j's term at once,
-// spilled inside k_step.)
-__device__ __forceinline__ void f64b_inv(const double* sL, int la, double* sXo, int lx, const double* dv) {
-  const int lane = threadIdx.x & 63, c = lane & 15;
-  double x[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    double dot = 0.0;
-#pragma unroll
-    for (int j = 0; j < i; ++j) dot = fma(sL[i * la + j], x[j], dot);
-    x[i] = (i < c) ? 0.0 : ((i == c) ? dv[i] : -dot * dv[i]);
-    __builtin_amdgcn_sched_barrier(0);  // a row of uniform L reads per region (register budget)
-  }
-  if (lane < 16) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) sXo[i * lx + c] = x[i];
-  }
-}
-
-__device__ __forceinline__ bool factor64_blocked(double* sA, int la, double* sX, int lx, double* buf) {
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  double* dinv = buf;  // [64]
-  auto Ab = [&](int i, int j) { return sA + 16 * i * la + 16 * j; };
-  auto Xb = [&](int i, int j) { return sX + 16 * i * lx + 16 * j; };
-  bool bad = false;
-  DIAG_STAMP_T(31, 0);
-  // P1(0) / P2(0)
-  if (wave == 0) {
-    bad = f64b_column(sA, la, 0, dinv);
-    DIAG_STAMP_T(41, 0);
-  }
-  lsync();
-  DIAG_STAMP_T(32, 0);  // (diagnostic build) thread 0 leaves barrier 0
-  if (wave >= 1 && wave <= 3) mm16<true, true, true>(Ab(wave, 1), la, Ab(wave, 0), la, Ab(1, 0), la);  // A_i1 -= L_i0 L_10^T
-  lsync();
-  DIAG_STAMP_T(33, 0);  // (diagnostic build) thread 0 leaves barrier 1
-  // P1(1): column 1 | X_00, A_22 / A_32 / A_33 -= (column 0 terms)
-  if (wave == 0) {
-    bad = f64b_column(sA, la, 1, dinv) | bad;
-    DIAG_STAMP_T(42, 0);
-  }
-  else if (wave == 1) mm16<true, true, true>(Ab(2, 2), la, Ab(2, 0), la, Ab(2, 0), la);
-  else if (wave == 2) mm16<true, true, true>(Ab(3, 2), la, Ab(3, 0), la, Ab(2, 0), la);
-  else if (wave == 3) mm16<true, true, true>(Ab(3, 3), la, Ab(3, 0), la, Ab(3, 0), la);
-  else if (wave == 6) f64b_inv(Ab(0, 0), la, Xb(0, 0), lx, dinv);
-  lsync();
-  DIAG_STAMP_T(34, 0);  // (diagnostic build) thread 0 leaves barrier 2
-  // P2(1): A_i2 -= L_i1 L_21^T | Xcur_i0 = L_i0 X_00
-  if (wave == 1 || wave == 2) mm16<true, true, true>(Ab(wave + 1, 2), la, Ab(wave + 1, 1), la, Ab(2, 1), la);
-  else if (wave >= 4 && wave <= 6) mm16<false, false, false>(Xb(wave - 3, 0), lx, Ab(wave - 3, 0), la, Xb(0, 0), lx);
-  lsync();
-  DIAG_STAMP_T(35, 0);  // (diagnostic build) thread 0 leaves barrier 3
-  // P1(2): column 2 | X_11, A_33 -= L_31 L_31^T
-  if (wave == 0) {
-    bad = f64b_column(sA, la, 2, dinv) | bad;
-    DIAG_STAMP_T(43, 0);
-  }
-  else if (wave == 3) mm16<true, true, true>(Ab(3, 3), la, Ab(3, 1), la, Ab(3, 1), la);
-  else if (wave == 6) f64b_inv(Ab(1, 1), la, Xb(1, 1), lx, dinv + 16);
-  lsync();
-  DIAG_STAMP_T(36, 0);  // (diagnostic build) thread 0 leaves barrier 4
-  // P2(2): A_33 -= L_32 L_32^T | X_10 = -X_11 Xcur_10, Xcur_21 = L_21 X_11, Xcur_31 = L_31 X_11
-  if (wave == 1) mm16<true, true, true>(Ab(3, 3), la, Ab(3, 2), la, Ab(3, 2), la);
-  else if (wave == 4) mm16<false, true, false>(Xb(1, 0), lx, Xb(1, 1), lx, Xb(1, 0), lx);
-  else if (wave == 5) mm16<false, false, false>(Xb(2, 1), lx, Ab(2, 1), la, Xb(1, 1), lx);
-  else if (wave == 6) mm16<false, false, false>(Xb(3, 1), lx, Ab(3, 1), la, Xb(1, 1), lx);
-  lsync();
-  DIAG_STAMP_T(37, 0);  // (diagnostic build) thread 0 leaves barrier 5
-  // P1(3): column 3 | X_22, Xcur_20 += L_21 X_10, Xcur_30 += L_31 X_10
-  if (wave == 0) {
-    bad = f64b_column(sA, la, 3, dinv) | bad;
-    DIAG_STAMP_T(44, 0);
-  }
-  else if (wave == 6) f64b_inv(Ab(2, 2), la, Xb(2, 2), lx, dinv + 32);
-  else if (wave == 5) mm16<false, false, true>(Xb(2, 0), lx, Ab(2, 1), la, Xb(1, 0), lx);
-  else if (wave == 7) mm16<false, false, true>(Xb(3, 0), lx, Ab(3, 1), la, Xb(1, 0), lx);
-  lsync();
-  DIAG_STAMP_T(38, 0);  // (diagnostic build) thread 0 leaves barrier 6
-  // T1: X_33 | X_20 = -X_22 Xcur_20, X_21 = -X_22 Xcur_21, Xcur_32 = L_32 X_22
-  if (wave == 4) f64b_inv(Ab(3, 3), la, Xb(3, 3), lx, dinv + 48);
-  else if (wave == 5) mm16<false, true, false>(Xb(2, 0), lx, Xb(2, 2), lx, Xb(2, 0), lx);
-  else if (wave == 6) mm16<false, true, false>(Xb(2, 1), lx, Xb(2, 2), lx, Xb(2, 1), lx);
-  else if (wave == 7) mm16<false, false, false>(Xb(3, 2), lx, Ab(3, 2), la, Xb(2, 2), lx);
-  lsync();
-  DIAG_STAMP_T(39, 0);  // (diagnostic build) thread 0 leaves barrier 7
-  // T2: Xcur_30 += L_32 X_20, Xcur_31 += L_32 X_21
-  if (wave == 5 || wave == 6) mm16<false, false, true>(Xb(3, wave - 5), lx, Ab(3, 2), la, Xb(2, wave - 5), lx);
-  lsync();
-  DIAG_STAMP_T(40, 0);  // (diagnostic build) thread 0 leaves barrier 8
-  // T3: X_3j = -X_33 Xcur_3j; zeros above the diagonal blocks of L and X
-  if (wave >= 5) mm16<false, true, false>(Xb(3, wave - 5), lx, Xb(3, 3), lx, Xb(3, wave - 5), lx);
-#pragma unroll
-  for (int u = 0; u < 6 * 256 / DNTH; ++u) {
-    const int i = threadIdx.x + DNTH * u;
-    const int t = i >> 8, e = i & 255;  // upper blocks (0,1) (0,2) (0,3) (1,2) (1,3) (2,3)
-    const int bi = (t < 3) ? 0 : (t < 5) ? 1 : 2;
-    const int bj = (t < 3) ? t + 1 : (t < 5) ? t - 1 : 3;
-    const int rr = 16 * bi + (e >> 4), cc = 16 * bj + (e & 15);
-    sA[rr * la + cc] = 0.0;
-    sX[rr * lx + cc] = 0.0;
-  }
-  return bad;
-}
-
-__device__ __forceinline__ bool factor64(double* sA, int la, double* sX, int lx, double* buf) {
-  return factor64_blocked(sA, la, sX, lx, buf);
-}
-
-// Fixed-order sum of the 8 partials scratch[q*64 + i], q = 0..7.
-__device__ __forceinline__ double sum8(const double* scratch, int i) {
-  return (((scratch[i] + scratch[64 + i]) + (scratch[128 + i] + scratch[192 + i])) +
-          ((scratch[256 + i] + scratch[320 + i]) + (scratch[384 + i] + scratch[448 + i])));
-}
-
-// out[r] = (sum_c s1[r][c] v1[c]) for r < 64 (or out[r] -= that); 8 partial sums
-// per row combined in fixed order. Ends with a barrier.
-__device__ __forceinline__ void rows_dot64(double* out, const double* s1, int l1, const double* v1, double* scratch,
-                                           bool accumulate) {
-  const int tid = threadIdx.x;
-  const int r = tid & 63, q = tid >> 6;
-  double acc = 0.0;
-  for (int c = q * 8; c < q * 8 + 8; ++c) acc = fma(s1[r * l1 + c], v1[c], acc);
-  scratch[q * 64 + r] = acc;
-  lsync();
-  if (tid < 64) {
-    const double s = sum8(scratch, tid);
-    out[tid] = accumulate ? out[tid] - s : s;
-  }
-  lsync();
-}
-
-// Column partials of a 64x64 LDS tile s (rows r, cols c): s2[c] += sum_r s^2,
-// sz[c] += sum_r s * z[r]. Fixed order. Ends with a barrier. scratch: 512 doubles.
-__device__ __forceinline__ void cols_partial64(double* s2, double* sz, const double* s, int ls, const double* z,
-                                               double* scratch) {
-  const int tid = threadIdx.x;
-  const int c = tid & 63, q = tid >> 6;
-  double a2 = 0.0, az = 0.0;
-  for (int r = q * 8; r < q * 8 + 8; ++r) {
-    const double v = s[r * ls + c];
-    a2 = fma(v, v, a2);
-    az = fma(v, z[r], az);
-  }
-  scratch[q * 64 + c] = a2;
-  lsync();
-  if (tid < 64) s2[tid] = s2[tid] + sum8(scratch, tid);
-  lsync();
-  scratch[q * 64 + c] = az;
-  lsync();
-  if (tid < 64) sz[tid] = sz[tid] + sum8(scratch, tid);
-  lsync();
-}
-
-struct DiagSmem {
-  double* t0;       // 64 x LDH
-  double* t1;       // 64 x LDH
-  double* y;        // 128
-  double* z;        // 128
-  double* ps2;      // 128
-  double* psz;      // 128
-  double* scratch;  // DIAG_SMALL (>= 512)
-};
-
-// ----------------------------------------------------------------------------
-// Factor one fully reduced 128x128 diagonal block in place (2x2 blocks of 64):
-//   L11,U11 = factor64(A11) ; L21 = A21 U11^T ; A22 -= L21 L21^T ; L22,U22 = factor64(A22)
-//   U21 = -U22 (L21 U11) ; z = L^-1 y by forward substitution ; partials of colsum(U^2),
-//   U^T z for the 128 columns.
-// Lt/Ut: top-left of the block in the particle's L / U buffers (row stride ld);
-// yseg: the block's 128 RHS entries (replaced by z); s2o/szo: 128 partial outputs.
-// ----------------------------------------------------------------------------
-// pub (the early diagonal factor, WT = true): the per-particle flag to set to pub_val once U_JJ
-// and z_J — all a tile of the launch reads — are stored (write-through) and drained; the column
-// partials of the block (read only after the launch) are formed after the flag ("early publish").
-template <bool WT = false>
-__device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __restrict__ Ut, size_t ld,
-                                          double* __restrict__ yseg, double* __restrict__ s2o,
-                                          double* __restrict__ szo, int* __restrict__ info, const DiagSmem& sm,
-                                          bool pad2, int* pub = nullptr, int pub_val = 0) {
-  const int tid = threadIdx.x;
-  const Quad<64> qd;
-  double* const t0 = sm.t0;
-  double* const t1 = sm.t1;
-
-  DIAG_STAMP(0);
-  // (a) L11, U11, z1
-  tile64_to_lds(t0, LDH, Lt, ld);
-  if (tid < T) {
-    sm.y[tid] = yseg[tid];
-    sm.ps2[tid] = 0.0;
-    sm.psz[tid] = 0.0;
-  }
-  lsync();
-  bool bad = factor64(t0, LDH, t1, LDH, sm.scratch);
-  lsync();
-  DIAG_STAMP(1);
-  lds_to_tile64(Lt, ld, t0, LDH, true);
-  zero_tile64(Lt + H, ld);
-  lds_to_tile64<WT>(Ut, ld, t1, LDH, false);
-  zero_tile64<WT>(Ut + H, ld);
-  rows_dot64(sm.z, t1, LDH, sm.y, sm.scratch, false);          // z1 = U11 y1
-  cols_partial64(sm.ps2, sm.psz, t1, LDH, sm.z, sm.scratch);   // U11 columns
-
-  if (pad2) {
-    // rows/columns 64..127 of this block are all padding (A21 = 0, A22 = I from the K build and
-    // no earlier column touches them): L21 = U21 = 0, L22 = U22 = I, z2 = 0 — exactly what the
-    // general path computes, without the second 64x64 factor
-    zero_tile64(Lt + (size_t)H * ld, ld);
-    zero_tile64<WT>(Ut + (size_t)H * ld, ld);
-    for (int i = tid; i < H * H; i += DNTH) {
-      const int r = i >> 6, c = i & 63;
-      Lt[(size_t)(H + r) * ld + H + c] = (r == c) ? 1.0 : 0.0;
-      gst<WT>(&Ut[(size_t)(H + r) * ld + H + c], (r == c) ? 1.0 : 0.0);
-    }
-    if (tid < T) {
-      s2o[tid] = (tid < H) ? sm.ps2[tid] : 1.0;
-      szo[tid] = (tid < H) ? sm.psz[tid] : 0.0;
-      gst<WT>(&yseg[tid], (tid < H) ? sm.z[tid] : 0.0);
-    }
-    if (bad && tid == 0 && *info == 0) *info = 1;
-    if (pub) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) __hip_atomic_store(pub, pub_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return;
-  }
-
-  DIAG_STAMP(2);
-  // (b) L21 = A21 U11^T; A22 is read into registers now, so its load runs behind (b) and (c)
-  double* U21 = Ut + (size_t)H * ld;
-  const double* A22 = Lt + (size_t)H * ld + H;
-  Acc<64> a22;
-  a22.load(qd, A22, ld);
-  tile64_to_lds(t0, LDH, Lt + (size_t)H * ld, ld);
-  lsync();
-  Acc<64> acc;
-  acc.zero();
-  gemm_lds64<false, TRI_B_KLEC>(acc, t0, LDH, t1, LDH, qd);  // U11^T is upper triangular
-  lsync();
-  acc.foreach(qd, [&](int r, int c, double v) {
-      t0[r * LDH + c] = v;
-      Lt[(size_t)(H + r) * ld + c] = v;
-    });
-  lsync();
-
-  DIAG_STAMP(3);
-  // (c) A22 -= L21 L21^T ; y2 -= L21 z1 ; T = L21 U11 (to the U21 slot as scratch)
-  acc.zero();
-  gemm_lds64<false, TRI_C_LOWER>(acc, t0, LDH, t0, LDH, qd);  // factor64 reads the lower triangle only
-  rows_dot64(sm.y + H, t0, LDH, sm.z, sm.scratch, true);
-  Acc<64> tt;
-  tt.zero();
-  gemm_lds64<true, TRI_B_KGEC>(tt, t0, LDH, t1, LDH, qd);  // U11 is lower triangular
-  lsync();
-  tt.foreach(qd, [&](int r, int c, double v) { gst<WT>(&U21[(size_t)r * ld + c], v); });
-#pragma unroll
-  for (int mi = 0; mi < Acc<64>::MBR; ++mi)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) acc.v[mi][0][e] = a22.v[mi][0][e] - acc.v[mi][0][e];
-  acc.foreach(qd, [&](int r, int c, double v) { t0[r * LDH + c] = v; });
-  lsync();
-
-  DIAG_STAMP(4);
-  // (d) L22, U22
-  bad = factor64(t0, LDH, t1, LDH, sm.scratch) | bad;
-  lsync();
-  DIAG_STAMP(5);
-  // T (stored to the U21 slot in (c), long drained: the factor ran since) read back into
-  // registers first, so the loads run behind the stores of L22 and U22
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  d2 tv[2048 / DNTH];
-#pragma unroll
-  for (int u = 0; u < 2048 / DNTH; ++u) {
-    const int q = tid + DNTH * u, row = q >> 5, c2 = q & 31;
-    tv[u] = *reinterpret_cast<const d2*>(U21 + (size_t)row * ld + 2 * c2);
-  }
-  lds_to_tile64(Lt + (size_t)H * ld + H, ld, t0, LDH, true);
-  lds_to_tile64<WT>(Ut + (size_t)H * ld + H, ld, t1, LDH, false);
-  lsync();
-
-  DIAG_STAMP(6);
-  // (e) U21 = -U22 T
-#pragma unroll
-  for (int u = 0; u < 2048 / DNTH; ++u) {
-    const int q = tid + DNTH * u, row = q >> 5, c2 = q & 31;
-    t0[row * LDH + 2 * c2] = tv[u].x;
-    t0[row * LDH + 2 * c2 + 1] = tv[u].y;
-  }
-  lsync();
-  acc.zero();
-  gemm_lds64<true, TRI_A_KLER>(acc, t1, LDH, t0, LDH, qd);  // U22 is lower triangular
-  lsync();
-  acc.foreach(qd, [&](int r, int c, double v) {
-      t0[r * LDH + c] = -v;
-      gst<WT>(&U21[(size_t)r * ld + c], -v);
-    });
-  lsync();
-
-  DIAG_STAMP(7);
-  // (f) forward substitution: z2 = U22 (y2 - L21 z1) (y2 already reduced in (c))
-  rows_dot64(sm.z + H, t1, LDH, sm.y + H, sm.scratch, false);
-  if (pub) {  // early publish: U_JJ (stored write-through above) and z_J are complete
-    if (tid < T) gst<WT>(&yseg[tid], sm.z[tid]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's U_JJ and z_J stores drained
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(pub, pub_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  DIAG_STAMP(8);
-  // (g) partials: columns 0..63 get the U21 rows, columns 64..127 the U22 rows
-  cols_partial64(sm.ps2, sm.psz, t0, LDH, sm.z + H, sm.scratch);
-  cols_partial64(sm.ps2 + H, sm.psz + H, t1, LDH, sm.z + H, sm.scratch);
-  if (tid < T) {
-    s2o[tid] = sm.ps2[tid];
-    szo[tid] = sm.psz[tid];
-    if (!pub) gst<WT>(&yseg[tid], sm.z[tid]);
-  }
-  if (bad && tid == 0 && *info == 0) *info = 1;
-  DIAG_STAMP(9);
-}
-
-// Shared-memory carve-up for the diagonal factor: two 64x64 tiles and the small
-// vectors live in `base` (the GEMM staging area, DIAG_BASE doubles), the
-// 512-double reduction scratch in `small`.
-constexpr int DIAG_BASE = 2 * H * LDH + 4 * T;
-constexpr int DIAG_SMALL = F64_BUF;  // factor64's buffers (also >= the 512-double reduction scratch)
-__device__ __forceinline__ DiagSmem carve_diag(double* base, double* small) {
-  DiagSmem s;
-  s.t0 = base;
-  s.t1 = base + H * LDH;
-  s.y = base + 2 * H * LDH;
-  s.z = s.y + T;
-  s.ps2 = s.z + T;
-  s.psz = s.ps2 + T;
-  s.scratch = small;
-  return s;
-}
 
 // Diagonal block J of every particle (A_JJ already reduced by the look-ahead of
 // all earlier block columns). Launched for J = 0 only; every later diagonal
@@ -521,15 +36,13 @@ __global__ __launch_bounds__(DNTH) void k_diag(int J, int nt, int N, int Npad, d
                                                   double* __restrict__ s2p, double* __restrict__ szp,
                                                   int* __restrict__ info, int* __restrict__ dflag) {
   if (threadIdx.x == 0) dflag[blockIdx.x] = J;  // a new factorisation: block J published (launches follow in order)
-  __shared__ __attribute__((aligned(16))) double tiles[DIAG_BASE];
-  __shared__ __attribute__((aligned(16))) double small[DIAG_SMALL];
+  __shared__ __attribute__((aligned(16))) double lds[DB_LDS];
   const int p = blockIdx.x;
   const size_t ld = (size_t)Npad;
   const size_t off = (size_t)p * ld * ld + (size_t)J * T * ld + (size_t)J * T;
-  const DiagSmem sm = carve_diag(tiles, small);
   const size_t poff = ((size_t)p * nt + J) * Npad + (size_t)J * T;
-  factor128(Lb + off, Ub + off, ld, yb + (size_t)p * Npad + J * T, s2p + poff, szp + poff, info + p, sm,
-            J * T + H >= N);
+  factor128(Lb + off, Ub + off, ld, yb + (size_t)p * Npad + J * T, s2p + poff, szp + poff, info + p, lds);
+  (void)N;
 }
 
 // ----------------------------------------------------------------------------
@@ -688,11 +201,11 @@ __host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt,
 }
 
 // LDS of a k_step workgroup (doubles): the GEMM stages (DL_STAGE), the diagonal factor
-// (DIAG_BASE + DIAG_SMALL), the staged U_JJ of the triangular finishes (TRI_LDS) with z_J behind
+// (DB_LDS), the staged U_JJ of the triangular finishes (TRI_LDS) with z_J behind
 // it, or the coordinates of a covariance tile. ~77 KiB: two workgroups per CU.
 constexpr int STEP_ZJ = TRI_LDS;  // z_J (128 doubles) beside the staged U_JJ
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
-constexpr int STEP_LDS = cmax(cmax(DL_STAGE, DIAG_BASE + DIAG_SMALL), cmax(STEP_ZJ + T, 2 * DMAX * T + 2 * T));
+constexpr int STEP_LDS = cmax(cmax(DL_STAGE, DB_LDS), cmax(STEP_ZJ + T, 2 * DMAX * T + 2 * T));
 static_assert(STEP_LDS * 8 <= 80 * 1024, "two k_step workgroups per CU (160 KiB of LDS)");
 constexpr int STEP_NTH = Geo<T>::NTH;     // 512 threads: 8 waves, 128x16 per wave
 static_assert(STEP_NTH == DNTH, "the fused diagonal runs on the step workgroup");
@@ -806,13 +319,12 @@ constexpr int TREE_BATCH = 2;  // row blocks of the sibling's node sum read per 
 constexpr int SPLIT_TREE = 80;              // tickets per split tile: pair (level l < 5, pair k < 16) at l * 16 + k
 constexpr int SPLIT_CNT = 2 * SPLIT_TREE;   // + the pairs' ready flags at SPLIT_TREE + l * 16 + k
 
-template <bool NN, bool NEG, bool SEEDED = false, typename Seed>
-__device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int lda, const double* Bp, int ldb, int nch, int S,
-                           int s, double* __restrict__ pt, unsigned* __restrict__ ct, double* smem,
-                           const Quad<T>& qd, int* flag, int* info, int spins, Seed seed, int J) {
-  // piece boundaries over nch + e chunks, the first e of them standing for piece 0's seed (its
-  // covariance tile costs about SEED_CH chunks of GEMM), so that the seeded piece — the carrier
-  // of every tree level it reaches — ends its GEMM with the others
+// One piece's partial GEMM: piece boundaries over nch + e chunks, the first e of them standing
+// for piece 0's seed (its covariance tile costs about SEED_CH chunks of GEMM), so that the seeded
+// piece ends its GEMM with the others.
+template <bool NN, bool NEG, bool SEEDED, typename Seed>
+__device__ __forceinline__ void split_gemm(Acc<T>& acc, const double* Ap, int lda, const double* Bp, int ldb, int nch,
+                                           int S, int s, double* smem, const Quad<T>& qd, Seed seed) {
   const int e = SEEDED ? SEED_CH : 0;
   const int c0 = s == 0 ? 0 : max(0, s * (nch + e) / S - e), c1 = max(0, (s + 1) * (nch + e) / S - e);
   if (SEEDED && s == 0)
@@ -823,6 +335,37 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
     gemm_stream_dl<NN, NEG>(acc, Ap + (size_t)c0 * DL_KC, lda,
                             NN ? Bp + (size_t)c0 * DL_KC * ldb : Bp + (size_t)c0 * DL_KC, ldb, (c1 - c0) * DL_KC,
                             smem, qd);
+}
+
+// A partial (or node sum) to its 128 KiB slot in the accumulators' own layout: wave w's
+// registers at bytes [16 KiB w, 16 KiB (w+1)), register pair (mi, h) of every lane as one 1 KiB
+// block (16-B write-through stores, 1 KiB per wave instruction). Nothing but the split-K
+// reductions reads the slots.
+constexpr int NODE_WAVE = Acc<T>::MBR * Acc<T>::MBC * 2048;  // bytes per wave region
+__device__ __forceinline__ void store_node(const Acc<T>& acc, double* slot, const Quad<T>& qd) {
+  const auto ws = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(slot), 0, T * T * 8, 0x00020000);
+  const int wb = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * NODE_WAVE;
+#pragma unroll
+  for (int mi = 0; mi < Acc<T>::MBR; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < Acc<T>::MBC; ++ni)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const double a0 = acc.v[mi][ni][2 * h], a1 = acc.v[mi][ni][2 * h + 1];
+        const unsigned long long u0 = __builtin_bit_cast(unsigned long long, a0),
+                                 u1 = __builtin_bit_cast(unsigned long long, a1);
+        const __attribute__((ext_vector_type(4))) unsigned q4 = {(unsigned)u0, (unsigned)(u0 >> 32), (unsigned)u1,
+                                                                  (unsigned)(u1 >> 32)};
+        __builtin_amdgcn_raw_buffer_store_b128(q4, ws, qd.lane * 16, wb + ((mi * Acc<T>::MBC + ni) * 2 + h) * 1024,
+                                               16);  // sc1: write-through
+      }
+}
+
+template <bool NN, bool NEG, bool SEEDED = false, typename Seed>
+__device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int lda, const double* Bp, int ldb, int nch, int S,
+                           int s, double* __restrict__ pt, unsigned* __restrict__ ct, double* smem,
+                           const Quad<T>& qd, int* flag, int* info, int spins, Seed seed, int J) {
+  split_gemm<NN, NEG, SEEDED>(acc, Ap, lda, Bp, ldb, nch, S, s, smem, qd, seed);
 #ifdef GPF_WG_TRACE
   {
     const int tid = threadIdx.x;
@@ -840,25 +383,7 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
     if (threadIdx.x == 0) *flag = (int)__hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (*flag == 0) {  // first: publish the node sum, then the sibling carries the pair on
-      {  // register-native slot layout: 16-B write-through stores, 1 KiB per wave instruction
-        const auto ws = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(pt + (size_t)(c << l) * T * T), 0,
-                                                          T * T * 8, 0x00020000);
-        const int wb = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (Acc<T>::MBR * Acc<T>::MBC * 2048);
-#pragma unroll
-        for (int mi = 0; mi < Acc<T>::MBR; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < Acc<T>::MBC; ++ni)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const double a0 = acc.v[mi][ni][2 * h], a1 = acc.v[mi][ni][2 * h + 1];
-              const unsigned long long u0 = __builtin_bit_cast(unsigned long long, a0),
-                                       u1 = __builtin_bit_cast(unsigned long long, a1);
-              const __attribute__((ext_vector_type(4))) unsigned q4 = {(unsigned)u0, (unsigned)(u0 >> 32),
-                                                                        (unsigned)u1, (unsigned)(u1 >> 32)};
-              __builtin_amdgcn_raw_buffer_store_b128(q4, ws, qd.lane * 16, wb + ((mi * Acc<T>::MBC + ni) * 2 + h) * 1024,
-                                                     16);  // sc1: write-through
-            }
-      }
+      store_node(acc, pt + (size_t)(c << l) * T * T, qd);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its part of the node sum
       __syncthreads();
       if (threadIdx.x == 0) __hip_atomic_store(rdy, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -889,7 +414,7 @@ __device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int ld
     // loop and spilled)
     const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(pt + (size_t)(sib << l) * T * T), 0, T * T * 8,
                                                       0x00020000);
-    const int wb = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (Acc<T>::MBR * Acc<T>::MBC * 2048);
+    const int wb = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * NODE_WAVE;
 #pragma unroll
     for (int mi = 0; mi < Acc<T>::MBR; ++mi) {
 #pragma unroll
@@ -930,6 +455,262 @@ __device__ __forceinline__ bool wait_diag(const int* flag, int J, int* info, int
   }
   __syncthreads();
   return *sflag != 0;
+}
+
+// ----------------------------------------------------------------------------
+// Flat split-K finish (SPLIT_ALL; r5). The reduction tree above hands every tile's sum to one
+// workgroup, which then also runs the whole finish (the triangular multiply of the 8 column
+// slabs and, for an L tile, the 36-block diagonal update A_II -= L_IJ L_IJ^T) alone: for the
+// single-particle prediction that was ~30 us of tree plus ~20 us of one-CU finish per launch, on
+// every launch's chain. Here the np pieces of a tile share all of it:
+//   A  every piece stores its partial to its slot (write-through, drained) and counts in (c[0]);
+//   R  once all np are in, the 8 np waves of the pieces sum the slots' 128 1-KiB units (slot
+//      order, so results are deterministic), 16 slots per round trip, into slot 0 in place, and
+//      count each unit in on its wave region's counter (c[1 + r]);
+//   T  the pieces 0..min(np,8)-1 wait for the diagonal block (U_JJ, z_J), stage U_JJ, and wave v
+//      of piece s finishes region r = s + np v (< 8) once its 16 units are in: the triangular
+//      multiply, the stores (write-through for L tiles) and y_I (L) or the column partials (U);
+//      an L tile's region counts in on c[9];
+//   C  (L tiles) once all 8 regions are in, the 8 np waves take the 36 lower 16x16 blocks of
+//      A_II -= L_IJ L_IJ^T, each 32 MFMAs over k ascending with A_II as the seed — the per-element
+//      MFMA sequence of syrk_rows.
+// Every wait is bounded (`spins`; timeout: info bit 2, the wave or piece leaves). No wait can hold
+// the slots an awaited workgroup needs: the diagonal workgroups come first in the launch and wait
+// for nothing; the np <= SPLIT_MAXS pieces of a tile have consecutive workgroup ids, which the
+// dispatcher deals round-robin over the 8 XCDs and in order within each, so an XCD holds at most
+// 4 pieces of a tile — a stalled XCD (64 slots) would need all its slots taken by pieces of the
+// lowest incomplete tile. Counters: FLAT_CNT words per (particle, launch, tile), zeroed by the
+// factorisation's memset, never reused within it.
+constexpr int FLAT_CNT = 16;  // [0] partials stored, [1 + r] units of region r summed, [9] L regions finished
+__host__ __device__ __forceinline__ int split_cnt_stride(int nt) {  // counter words per split tile and particle
+  return SPLIT_CNT > FLAT_CNT * nt ? SPLIT_CNT : FLAT_CNT * nt;
+}
+__device__ __forceinline__ int region_slab(int r) { return r < 4 ? r : 11 - r; }  // Quad<128>::cb / 16 of wave r
+
+// Bounded wave-level wait for *c >= n, then an agent-scope acquire; true: timed out (info bit 2).
+__device__ __forceinline__ bool wave_wait(const unsigned* c, unsigned n, int* info, int spins) {
+  int k = 0;
+  while ((unsigned)__builtin_amdgcn_readfirstlane(
+             (int)__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < n) {
+    if (k++ >= spins) {
+      if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or(info, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return true;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return false;
+}
+
+// The same for the whole workgroup (thread 0 polls; ends with a barrier).
+__device__ __forceinline__ bool group_wait(const unsigned* c, unsigned n, int* info, int spins, int* sflag) {
+  if (threadIdx.x == 0) {
+    int k = 0, late = 0;
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) {
+      if (k++ >= spins) {
+        __hip_atomic_fetch_or(info, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        late = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    *sflag = late;
+  }
+  __syncthreads();
+  return *sflag != 0;
+}
+
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+
+// Phase R: unit u (bytes [1 KiB u, 1 KiB (u+1)) of a slot) summed over the np slots in slot order,
+// to slot 0 (write-through).
+__device__ __forceinline__ void flat_reduce_unit(double* pt, int np, int u) {
+  const int lane = threadIdx.x & 63;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(pt), 0, np * T * T * 8, 0x00020000);
+  d2 sum = {0.0, 0.0};
+  for (int i0 = 0; i0 < np; i0 += 16) {
+    u4v q[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i0 + i < np) q[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, (i0 + i) * (T * T * 8) + u * 1024, 0);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i0 + i < np) {
+        const d2 v = __builtin_bit_cast(d2, q[i]);
+        sum = (i0 + i == 0) ? v : sum + v;
+      }
+  }
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, sum), rs, lane * 16, u * 1024, 16);  // sc1: write-through
+}
+
+// Phase T's operand: wave region r of slot 0 into the accumulator layout.
+__device__ __forceinline__ void flat_load_region(Acc<T>& acc, const double* pt, int r) {
+  const int lane = threadIdx.x & 63;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(pt), 0, T * T * 8, 0x00020000);
+#pragma unroll
+  for (int mi = 0; mi < Acc<T>::MBR; ++mi)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const d2 v = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, r * NODE_WAVE + (2 * mi + h) * 1024, 0));
+      acc.v[mi][0][2 * h] = v.x;
+      acc.v[mi][0][2 * h + 1] = v.y;
+    }
+}
+
+// Phase C: block (ib, jb) (ib >= jb) of A_II -= L_IJ L_IJ^T: 32 MFMAs, k = 4 t + (lane >> 4)
+// ascending, seeded with A_II (syrk_rows' operands and order per element).
+__device__ __forceinline__ void flat_syrk_block(double* Aii, const double* Lij, size_t ld, int ib, int jb) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, cl = lane & 15;
+  const double* ar = launder(Lij + (size_t)(16 * ib + cl) * ld + g);
+  const double* br = launder(Lij + (size_t)(16 * jb + cl) * ld + g);
+  double* cp = launder(Aii + (size_t)(16 * ib + g) * ld + 16 * jb + cl);
+  d4 acc;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) acc[r] = cp[(size_t)(4 * r) * ld];
+#pragma unroll
+  for (int t0 = 0; t0 < 32; t0 += 16) {  // 16 k-steps of operands per round trip
+    double a[16], b[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      a[t] = ar[4 * (t0 + t)];
+      b[t] = br[4 * (t0 + t)];
+    }
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc = mfma_neg_a(a[t], b[t], acc);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) cp[(size_t)(4 * r) * ld] = acc[r];
+}
+
+// One piece (sidx of np) of tile w of launch J under the flat finish (see above); LT: an L tile.
+template <bool LT>
+__device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad, double* __restrict__ Lp,
+                                        double* __restrict__ Up, double* __restrict__ yp, double* __restrict__ s2p,
+                                        double* __restrict__ szp, int* __restrict__ info, int N,
+                                        const double* __restrict__ x, const double* __restrict__ lp, int d, int np,
+                                        int sidx, int S2, double* __restrict__ part, unsigned* __restrict__ cnt,
+                                        int* sflag, const int* __restrict__ dflag, int spins, double* lds) {
+  const int tid = threadIdx.x;
+  const size_t ld = (size_t)Npad;
+  const int nL = nt - 1 - J;
+  const int I = J + 1 + w, K = w - nL;
+  const Quad<T> qd;
+  const int g = qd.lane >> 4, cl = qd.lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  double* pt = part + (size_t)(p * (nt - 1) + w) * S2 * T * T;
+  unsigned* ca = cnt + (size_t)p * (nt - 1) * split_cnt_stride(nt) + (size_t)(J * (nt - 1) + w) * FLAT_CNT;
+  // A: the partial (piece 0 of an L tile seeded with the covariance tile A_IJ^T)
+  {
+    Acc<T> acc;
+    if (LT)
+      split_gemm<false, true, true>(acc, Lp + (size_t)J * T * ld, Npad, Lp + (size_t)I * T * ld, Npad, J * T / DL_KC,
+                                    np, sidx, lds, qd,
+                                    [&](Acc<T>& a) { cov_tile_acc(a, qd, x, lp, d, N, J, I, lds); });
+    else  // (the triangular first block runs dense: its upper part holds zeros)
+      split_gemm<true, false, false>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
+                                     Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T / DL_KC, np, sidx, lds,
+                                     qd, [](Acc<T>&) {});
+    store_node(acc, pt + (size_t)sidx * T * T, qd);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's part of the partial drained
+  __syncthreads();
+  if (tid == 0) __hip_atomic_fetch_add(ca, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  GPF_PHASE(3);
+  if (group_wait(ca, (unsigned)np, info, spins, sflag)) return;
+  // R
+  for (int u = sidx * 8 + wave; u < 128; u += 8 * np) {
+    flat_reduce_unit(pt, np, u);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (qd.lane == 0) __hip_atomic_fetch_add(ca + 1 + (u >> 4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // T
+  if (sidx < 8) {
+    double* zj = lds + STEP_ZJ;
+    if (wait_diag(dflag + p, J, info, spins, sflag)) return;  // U_JJ, z_J
+    if (tid < T) zj[tid] = yp[J * T + tid];
+    tri_to_lds(Up + (size_t)J * T * ld + (size_t)J * T, ld, lds);  // (its barrier also publishes z_J)
+    const int r = sidx + np * wave;  // the region this wave finishes
+    if (r < 8) {
+      if (wave_wait(ca + 1 + r, 16u, info, spins)) return;
+      Acc<T> acc;
+      flat_load_region(acc, pt, r);
+      const int cb = 16 * region_slab(r);
+      if (LT) {
+        // L_IJ^T = U_JJ D for the slab's 16 columns of D (rows cb.. of L_IJ); y_I -= L_IJ z_J
+        double* lrow = launder(Lp + (size_t)(I * T + cb + cl) * ld + (size_t)J * T + g);
+        double yr = 0.0;
+#pragma unroll
+        for (int P = 0; P < 4; ++P) {
+          d4 o[2];
+          switch (P) {
+            case 0: trmm_acc<0, false>(o, acc, lds); break;
+            case 1: trmm_acc<1, false>(o, acc, lds); break;
+            case 2: trmm_acc<2, false>(o, acc, lds); break;
+            default: trmm_acc<3, false>(o, acc, lds); break;
+          }
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              gst<true>(lrow + 16 * (2 * P + j) + 4 * e, o[j][e]);
+              yr = fma(o[j][e], zj[16 * (2 * P + j) + 4 * e + g], yr);
+            }
+        }
+        yr = sum_lane_groups(yr);
+        if (g == 0) yp[I * T + cb + cl] = yp[I * T + cb + cl] - yr;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the region's L drained
+        if (qd.lane == 0) __hip_atomic_fetch_add(ca + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        // U_JK = -U_JJ W; the column partials of colsum(U^2) and U^T z (per half, then summed)
+        double* ucol = launder(Up + (size_t)(J * T + g) * ld + (size_t)K * T + cb + cl);
+        double a2[2] = {0.0, 0.0}, az[2] = {0.0, 0.0};
+#pragma unroll
+        for (int P = 0; P < 4; ++P) {
+          d4 o[2];
+          switch (P) {
+            case 0: trmm_acc<0, true>(o, acc, lds); break;
+            case 1: trmm_acc<1, true>(o, acc, lds); break;
+            case 2: trmm_acc<2, true>(o, acc, lds); break;
+            default: trmm_acc<3, true>(o, acc, lds); break;
+          }
+          const int h = P >> 1;
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int row = 16 * (2 * P + j) + 4 * e;  // + g
+              const double v = o[j][e];
+              ucol[(size_t)row * ld] = v;
+              a2[h] = fma(v, v, a2[h]);
+              az[h] = fma(v, zj[row + g], az[h]);
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          a2[h] = sum_lane_groups(a2[h]);
+          az[h] = sum_lane_groups(az[h]);
+        }
+        if (g == 0) {
+          const size_t poff = ((size_t)p * nt + J) * Npad + (size_t)K * T + cb + cl;
+          s2p[poff] = a2[0] + a2[1];
+          szp[poff] = az[0] + az[1];
+        }
+      }
+    }
+  }
+  if (!LT) return;
+  // C
+  const int q0 = sidx * 8 + wave;
+  if (q0 >= 36) return;
+  if (wave_wait(ca + 9, 8u, info, spins)) return;
+  double* Aii = Lp + (size_t)I * T * ld + (size_t)I * T;
+  const double* Lij = Lp + (size_t)I * T * ld + (size_t)J * T;
+  for (int b = q0; b < 36; b += 8 * np) {
+    int ib = 0;
+    while ((ib + 1) * (ib + 2) / 2 <= b) ++ib;
+    flat_syrk_block(Aii, Lij, ld, ib, b - ib * (ib + 1) / 2);
+  }
 }
 
 // SYRK workgroup of launch J (deferred diagonal update, see step_decode): A_{J+1,J+1} -=
@@ -1006,6 +787,19 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
   double* Lp = Lb + (size_t)p * ld * ld;
   double* Up = Ub + (size_t)p * ld * ld;
   double* yp = yb + (size_t)p * Npad;
+  if constexpr (SPLIT == SPLIT_ALL) {
+    static_assert(ED, "the all-tile split runs with the early diagonal factor (host: early_diag)");
+    if (role == ROLE_PIECE) {
+      const int np = split_all_pieces(J, w, nt, S);
+      if (w < nL)
+        flat_piece<true>(J, w, p, nt, Npad, Lp, Up, yp, s2p, szp, info + p, N, x, ls + (size_t)p * d, d, np, sidx, S2,
+                         part, cnt, sflag, dflag, spins, lds);
+      else
+        flat_piece<false>(J, w, p, nt, Npad, Lp, Up, yp, s2p, szp, info + p, N, x, ls + (size_t)p * d, d, np, sidx, S2,
+                          part, cnt, sflag, dflag, spins, lds);
+      return;
+    }
+  }
   const Quad<T> qd;
   const int g = qd.lane >> 4, cl = qd.lane & 15;
   const double* Ujj = Up + (size_t)J * T * ld + (size_t)J * T;
@@ -1019,14 +813,12 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
     Acc<T> acc;
     // D = C^T = A_JI - L_J,<J L_I,<J^T (accumulator seeded with the covariance tile, A operand
     // negated through the MFMA modifier)
-    if (SPLIT != SPLIT_NONE && role == ROLE_PIECE) {
+    if (SPLIT == SPLIT_CRIT && role == ROLE_PIECE) {
       // split-K: partial GEMMs, the last workgroup to arrive finishes the tile; piece 0 seeds
       // its partial with the covariance tile (the unsplit path's accumulator seed)
-      // (S2 partial slots per tile; the all-tile split's pieces per tile from the chunk target S)
       double* pt = part + (size_t)(p * (nt - 1) + w) * S2 * T * T;
-      const int Sx = SPLIT == SPLIT_ALL ? split_all_pieces(J, w, nt, S) : S;
       if (!split_part<false, true, true>(acc, Lp + (size_t)J * T * ld, Npad, Lp + (size_t)I * T * ld, Npad,
-                                         J * T / DL_KC, Sx, sidx, pt, cnt + (size_t)(p * (nt - 1) + w) * SPLIT_CNT, lds,
+                                         J * T / DL_KC, S, sidx, pt, cnt + (size_t)(p * (nt - 1) + w) * split_cnt_stride(nt), lds,
                                          qd, sflag, info + p, spins,
                                          [&](Acc<T>& a) { cov_tile_acc(a, qd, x, lp, d, N, J, I, lds); }, J))
         return;  // (the finisher's accumulators hold D)
@@ -1088,27 +880,16 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
       __syncthreads();
       const size_t poff = ((size_t)p * nt + I) * Npad + (size_t)I * T;
       __builtin_amdgcn_s_setprio(3);  // latency-critical: the next launch waits for this block
-      factor128(Aii, Up + (size_t)I * T * ld + (size_t)I * T, ld, yp + I * T, s2p + poff, szp + poff, info + p,
-                carve_diag(lds, lds + DIAG_BASE), I * T + H >= N);
+      factor128(Aii, Up + (size_t)I * T * ld + (size_t)I * T, ld, yp + I * T, s2p + poff, szp + poff, info + p, lds);
     }
   } else {
     const int K = w - nL;
     double* Ujk = Up + (size_t)J * T * ld + (size_t)K * T;
     Acc<T> acc;
     // W = L_J,[K,J) U_[K,J),K (U_KK is lower triangular: the wave's first chunks add zeros)
-    if (SPLIT == SPLIT_ALL && role == ROLE_PIECE) {  // split-K (the triangular first block runs dense: its upper part holds zeros)
-      double* pt = part + (size_t)(p * (nt - 1) + w) * S2 * T * T;
-      const int Sx = split_all_pieces(J, w, nt, S);
-      if (!split_part<true, false, false>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
-                                          Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T / DL_KC, Sx, sidx,
-                                          pt, cnt + (size_t)(p * (nt - 1) + w) * SPLIT_CNT, lds, qd, sflag, info + p,
-                                          spins, [](Acc<T>&) {}, J))
-        return;
-    } else {
-      acc.zero();
-      gemm_stream_dl<true, false, TRI_B_KGEC>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
-                                              Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T, lds, qd);
-    }
+    acc.zero();
+    gemm_stream_dl<true, false, TRI_B_KGEC>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
+                                            Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T, lds, qd);
     GPF_PHASE(0);
     if (ED && wait_diag(dflag + p, J, info + p, spins, sflag)) return;  // U_JJ, z_J (U tiles exist for J > 0 only)
     if (tid < T) zj[tid] = yp[J * T + tid];
@@ -1221,8 +1002,8 @@ __global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_step(int J, i
     const size_t poff = ((size_t)p * nt + J) * Npad + (size_t)J * T;
     __builtin_amdgcn_s_setprio(3);  // the launch's tiles wait for this block
     // publishes block J (dflag[p] = J) as soon as U_JJ and z_J are stored, before its partials
-    factor128<true>(Lb + off, Ub + off, ld, yb + (size_t)p * Npad + J * T, s2p + poff, szp + poff, info + p,
-                    carve_diag(lds, lds + DIAG_BASE), J * T + H >= N, dflag + p, J);
+    factor128<true>(Lb + off, Ub + off, ld, yb + (size_t)p * Npad + J * T, s2p + poff, szp + poff, info + p, lds,
+                    dflag + p, J);
   } else {
     step_item<SPLIT, ED>(role, J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, S2, sidx, part, cnt, &sflag,
                          dflag, yflag, defer, spins, la, lab, lds);
@@ -1235,25 +1016,24 @@ __global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_step(int J, i
 }
 
 
-// Debug hook (gpf_debug_factor64): factor64 on two host-given 64x64 matrices in a row
-// (in: 2 x 64 x 64 row-major; out: L then X for each).
-__global__ __launch_bounds__(DNTH) void k_debug_factor64(const double* __restrict__ in, double* __restrict__ out,
-                                                         int* __restrict__ bad) {
-  __shared__ __attribute__((aligned(16))) double t[2 * H * LDH];
-  __shared__ __attribute__((aligned(16))) double scratch[F64_BUF];
-  const int tid = threadIdx.x;
-  for (int k = 0; k < 2; ++k) {
-    for (int i = tid; i < H * H; i += DNTH) t[(i / H) * LDH + i % H] = in[k * H * H + i];
-    __syncthreads();
-    const bool b = factor64(t, LDH, t + H * LDH, LDH, scratch);
-    __syncthreads();
-    for (int i = tid; i < H * H; i += DNTH) {
-      out[(2 * k) * H * H + i] = t[(i / H) * LDH + i % H];
-      out[(2 * k + 1) * H * H + i] = t[H * LDH + (i / H) * LDH + i % H];
-    }
-    if (tid == 0) bad[k] = b;
-    __syncthreads();
-  }
+// Debug / measurement hook (gpf_debug_factor128): factor128 on n host-given 128x128 blocks, one
+// workgroup each (in place: A -> L, the U blocks, y -> z, the partials); cyc[b] = the workgroup's
+// s_memtime cycles from the first load to the last store (nullable).
+__global__ __launch_bounds__(DNTH) void k_debug_factor128(double* __restrict__ L, double* __restrict__ U,
+                                                          double* __restrict__ y, double* __restrict__ s2,
+                                                          double* __restrict__ sz, int* __restrict__ bad,
+                                                          unsigned long long* __restrict__ cyc) {
+  __shared__ __attribute__((aligned(16))) double lds[DB_LDS];
+  const int b = blockIdx.x;
+  unsigned long long t0 = 0, t1 = 0;
+  __syncthreads();
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  factor128(L + (size_t)b * T * T, U + (size_t)b * T * T, T, y + (size_t)b * T, s2 + (size_t)b * T, sz + (size_t)b * T,
+            bad + b, lds);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+  if (cyc && threadIdx.x == 0) cyc[b] = t1 - t0;
 }
 
 // ----------------------------------------------------------------------------

@@ -242,7 +242,7 @@ __device__ __forceinline__ void p_ltile(const PItem& a, const PState& st, int J,
   __builtin_amdgcn_s_setprio(3);  // latency-critical: every tile of column I waits for this block
   // U_II and z_I are stored write-through and published (ucol[I] = I+1) before the partials
   factor128<true>(Aii, Up + (size_t)I * T * ld + (size_t)I * T, ld, yp + I * T, a.s2p + poff, a.szp + poff, info,
-                  carve_diag(lds, lds + DIAG_BASE), I * T + H >= a.N, st.ucol + (size_t)p * nt + I, I + 1);
+                  lds, st.ucol + (size_t)p * nt + I, I + 1);
   __builtin_amdgcn_s_setprio(0);
 }
 

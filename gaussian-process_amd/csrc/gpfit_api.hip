@@ -401,10 +401,16 @@ static int split_all_target(int pc, int nt, int J) {
 // slots are bound by the slot load instead, and their tiles would wait for the flag in the first
 // block columns (config C -0.7%, config D's 32-particle share -0.3%, E neutral), so they keep the
 // fused factor. pc: the particles of all concurrent groups. GPF_EARLY_DIAG = 0/1 overrides.
+// The all-tile split always runs it (its flat finish, gpf::flat_piece, waits for the diagonal block
+// inside the launch): GPF_EARLY_DIAG=0 does not apply there.
+static bool split_all_on(int pc, int nt) {
+  const int ng = num_groups(pc, nt);
+  return split_k(((pc + ng - 1) / ng) * (nt - 1), nt) > 1;
+}
 static bool early_diag(int pc, int nt) {
   bool on = (long long)pc * (nt - 1) <= 512;
   if (const char* s = getenv("GPF_EARLY_DIAG")) on = atoi(s) != 0;
-  return on && nt > 1;
+  return (on || split_all_on(pc, nt)) && nt > 1;
 }
 
 // Deferred diagonal update (gpf::syrk_item; see gpf::step_decode) for every factorisation without
@@ -473,7 +479,7 @@ static int split_crit(int pc, int nt, int J, int grp, int S_all) {
 }
 
 static int ensure_split(gpf_ctx* c, int tiles, int S) {
-  const size_t pb = (size_t)tiles * S * T * T * 8, cb = (size_t)tiles * gpf::SPLIT_CNT * 4;
+  const size_t pb = (size_t)tiles * S * T * T * 8, cb = (size_t)tiles * gpf::split_cnt_stride(c->nt) * 4;
   if (pb > c->part_cap) {
     clear_graphs(c);  // captured graphs hold the old pointers
     hipFree(c->d_part);
@@ -575,7 +581,7 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
                ((l.la & 1) && !l.sy ? l.gc : 0);  // (with SYRK workgroups the look-ahead rides on them)
       // one set of partial slots per group: groups run concurrently
       l.part_off = (size_t)l.p0 * (nt - 1) * Smax * T * T;
-      l.cnt_off = (size_t)l.p0 * (nt - 1) * gpf::SPLIT_CNT;
+      l.cnt_off = (size_t)l.p0 * (nt - 1) * gpf::split_cnt_stride(nt);
       out.push_back(l);
     }
   }
@@ -620,7 +626,8 @@ static int run_factor(gpf_ctx* c, int pc) {
   // finishing pieces re-zero what they used, but a hand-off that timed out (info bit 2) leaves its
   // pair's ticket and flag set, and the next tree would elect the wrong finisher;
   // ~20 KB at N=4096 for one particle, on c->stream ahead of the fork
-  if (Smax > 1) GPF_HIP(c, hipMemsetAsync(c->d_cnt, 0, (size_t)pc * (nt - 1) * gpf::SPLIT_CNT * 4, c->stream));
+  if (Smax > 1)
+    GPF_HIP(c, hipMemsetAsync(c->d_cnt, 0, (size_t)pc * (nt - 1) * gpf::split_cnt_stride(nt) * 4, c->stream));
   hipEvent_t wa = nullptr, wb = nullptr;
   if (c->prof) {
     wa = take_event(c);
@@ -701,7 +708,8 @@ static int run_factor(gpf_ctx* c, int pc) {
     // (every split launch gets its buffers: under SPLIT_ALL, l.S is chunks per piece, not a piece count)
     double* partg = l.split != gpf::SPLIT_NONE ? c->d_part + l.part_off : nullptr;
     unsigned* cntg = l.split != gpf::SPLIT_NONE ? c->d_cnt + l.cnt_off : nullptr;
-    const auto kern = l.split == gpf::SPLIT_ALL    ? (ed ? gpf::k_step<gpf::SPLIT_ALL, 1> : gpf::k_step<gpf::SPLIT_ALL, 0>)
+    if (l.split == gpf::SPLIT_ALL && !ed) return bad_arg(c, "internal: all-tile split without the early diagonal factor");
+    const auto kern = l.split == gpf::SPLIT_ALL    ? gpf::k_step<gpf::SPLIT_ALL, 1>
                       : l.split == gpf::SPLIT_CRIT ? (ed ? gpf::k_step<gpf::SPLIT_CRIT, 1> : gpf::k_step<gpf::SPLIT_CRIT, 0>)
                                                    : (ed ? gpf::k_step<gpf::SPLIT_NONE, 1> : gpf::k_step<gpf::SPLIT_NONE, 0>);
     const int rc = launch_on(c, st, PC_PANEL, fl * gc, [&] {
@@ -1398,7 +1406,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
   step_plan(pc, nt, S, Smax, plan);
   const int ntl = nt - 1, ng = num_groups(pc, nt);
   const size_t part_cap = Smax > 1 ? (size_t)pc * ntl * Smax * T * T : 0;
-  const size_t cnt_cap = Smax > 1 ? (size_t)pc * ntl * gpf::SPLIT_CNT : 0;
+  const size_t cstride = (size_t)gpf::split_cnt_stride(nt), cnt_cap = Smax > 1 ? (size_t)pc * ntl * cstride : 0;
   // partial-slot and counter ranges each group touches: groups run concurrently, so they must
   // be disjoint (within a group the launches are ordered on its stream)
   std::vector<size_t> plo(MAX_GROUPS, SIZE_MAX), phi(MAX_GROUPS, 0), clo(MAX_GROUPS, SIZE_MAX), chi(MAX_GROUPS, 0);
@@ -1431,6 +1439,9 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
       return plan_fail(msg, msg_len, "J=%d: SYRK workgroups without a diagonal block to reduce", l.J);
     if (l.defer && l.split == gpf::SPLIT_ALL)
       return plan_fail(msg, msg_len, "J=%d: deferred diagonal update under the all-tile split", l.J);
+    // the flat finish waits for the diagonal block inside the launch (gpf::flat_piece)
+    if (l.split == gpf::SPLIT_ALL && !l.ed)
+      return plan_fail(msg, msg_len, "J=%d: all-tile split launch without the early diagonal factor", l.J);
     // look-ahead: LA workgroups only where a next critical tile exists, no split, early diagonal
     // factor; a seeded launch follows a launch of the same group that ran them
     if (l.la && (l.split != gpf::SPLIT_NONE || !l.ed || ((l.la & 1) && (l.J < 1 || l.J > nt - 3)) ||
@@ -1478,14 +1489,21 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
         if (pieces_of(w) < 2) return plan_fail(msg, msg_len, "J=%d block %u is a piece of an unsplit tile", l.J, b);
         ++piece[(size_t)t * l.S2 + sidx];
         // slots as k_step addresses them: S2 per tile
-        const size_t off = l.part_off + ((size_t)t * l.S2 + sidx) * T * T, ci = l.cnt_off + (size_t)t * gpf::SPLIT_CNT;
-        if (off + (size_t)T * T > part_cap || ci + gpf::SPLIT_CNT > cnt_cap || l.S2 > gpf::SPLIT_MAXS)
+        // counters: the reduction tree's SPLIT_CNT words of the tile, or the flat finish's FLAT_CNT
+        // words of (particle, launch, tile) inside the particle's ntl * cstride (gpf::flat_piece)
+        const size_t off = l.part_off + ((size_t)t * l.S2 + sidx) * T * T;
+        const size_t ci = l.split == gpf::SPLIT_ALL
+                              ? l.cnt_off + (size_t)p * ntl * cstride + ((size_t)l.J * ntl + w) * gpf::FLAT_CNT
+                              : l.cnt_off + (size_t)t * cstride;
+        const size_t cn = l.split == gpf::SPLIT_ALL ? gpf::FLAT_CNT : gpf::SPLIT_CNT;
+        if (off + (size_t)T * T > part_cap || ci + cn > cnt_cap || l.S2 > gpf::SPLIT_MAXS ||
+            ci + cn > l.cnt_off + (size_t)(p + 1) * ntl * cstride)
           return plan_fail(msg, msg_len, "J=%d tile %d piece %d outside the split buffers (S=%d S2=%d)", l.J, t, sidx, l.S,
                            l.S2);
         plo[l.g] = std::min(plo[l.g], off);
         phi[l.g] = std::max(phi[l.g], off + (size_t)T * T);
         clo[l.g] = std::min(clo[l.g], ci);
-        chi[l.g] = std::max(chi[l.g], ci + gpf::SPLIT_CNT);
+        chi[l.g] = std::max(chi[l.g], ci + cn);
       }
       ++wgs;
     }
@@ -1819,22 +1837,38 @@ int gpf_gemm_bench(gpf_ctx* c, int mode, int Npad, int P, int tiles, int D, int 
   return GPF_OK;
 }
 
-// Debug hook: the 64x64 diagonal-leaf factor on two matrices (2*4096 in, 4*4096 out).
-int gpf_debug_factor64(gpf_ctx* c, const double* in, double* out, int* bad) {
-  if (!c || !in || !out || !bad) return GPF_BAD_ARG;
+// Debug / measurement hook: the diagonal-block factor (gpf::factor128) on n 128x128 blocks.
+int gpf_debug_factor128(gpf_ctx* c, const double* A, const double* y, int n, double* L, double* U, double* z, double* s2,
+                        double* sz, int* bad, double* cycles) {
+  if (!c || !A || !y || n <= 0 || !L || !U || !z || !s2 || !sz || !bad) return GPF_BAD_ARG;
   hipSetDevice(c->device);
-  double *di = nullptr, *dout = nullptr;
-  int* db = nullptr;
-  GPF_HIP(c, hipMalloc(&di, 2 * 4096 * 8));
-  GPF_HIP(c, hipMalloc(&dout, 4 * 4096 * 8));
-  GPF_HIP(c, hipMalloc(&db, 2 * 4));
-  GPF_HIP(c, hipMemcpy(di, in, 2 * 4096 * 8, hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(gpf::k_debug_factor64, dim3(1), dim3(gpf::DNTH), 0, c->stream, di, dout, db);
+  const size_t nb = (size_t)n * T * T, nv = (size_t)n * T;
+  DevBuf dL, dU, dy, ds2, dsz, db, dc;
+  GPF_HIP(c, dL.alloc(nb * 8, c->stream));
+  GPF_HIP(c, dU.alloc(nb * 8, c->stream));
+  GPF_HIP(c, dy.alloc(nv * 8, c->stream));
+  GPF_HIP(c, ds2.alloc(nv * 8, c->stream));
+  GPF_HIP(c, dsz.alloc(nv * 8, c->stream));
+  GPF_HIP(c, db.alloc((size_t)n * 4, c->stream));
+  GPF_HIP(c, dc.alloc((size_t)n * 8, c->stream));
+  GPF_HIP(c, hipMemcpyAsync(dL.p, A, nb * 8, hipMemcpyHostToDevice, c->stream));
+  GPF_HIP(c, hipMemsetAsync(dU.p, 0x7f, nb * 8, c->stream));  // (every entry must be written)
+  GPF_HIP(c, hipMemcpyAsync(dy.p, y, nv * 8, hipMemcpyHostToDevice, c->stream));
+  GPF_HIP(c, hipMemsetAsync(db.p, 0, (size_t)n * 4, c->stream));
+  hipLaunchKernelGGL(gpf::k_debug_factor128, dim3(n), dim3(gpf::DNTH), 0, c->stream, dL.as<double>(), dU.as<double>(),
+                     dy.as<double>(), ds2.as<double>(), dsz.as<double>(), db.as<int>(), dc.as<unsigned long long>());
   GPF_HIP(c, hipGetLastError());
+  GPF_HIP(c, hipMemcpyAsync(L, dL.p, nb * 8, hipMemcpyDeviceToHost, c->stream));
+  GPF_HIP(c, hipMemcpyAsync(U, dU.p, nb * 8, hipMemcpyDeviceToHost, c->stream));
+  GPF_HIP(c, hipMemcpyAsync(z, dy.p, nv * 8, hipMemcpyDeviceToHost, c->stream));
+  GPF_HIP(c, hipMemcpyAsync(s2, ds2.p, nv * 8, hipMemcpyDeviceToHost, c->stream));
+  GPF_HIP(c, hipMemcpyAsync(sz, dsz.p, nv * 8, hipMemcpyDeviceToHost, c->stream));
+  GPF_HIP(c, hipMemcpyAsync(bad, db.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+  std::vector<unsigned long long> cyc(n);
+  GPF_HIP(c, hipMemcpyAsync(cyc.data(), dc.p, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
   GPF_HIP(c, hipStreamSynchronize(c->stream));
-  GPF_HIP(c, hipMemcpy(out, dout, 4 * 4096 * 8, hipMemcpyDeviceToHost));
-  GPF_HIP(c, hipMemcpy(bad, db, 2 * 4, hipMemcpyDeviceToHost));
-  hipFree(di); hipFree(dout); hipFree(db);
+  if (cycles)
+    for (int i = 0; i < n; ++i) cycles[i] = (double)cyc[i];
   return GPF_OK;
 }
 
@@ -1861,17 +1895,6 @@ int gpf_debug_wg_phase(unsigned long long* out, int nj, int nwg) {
 }
 #endif
 
-#ifdef GPF_DIAG_STAMPS
-// diagnostic builds only: phase timestamps of factor128 (workgroup 0 of the last k_diag launch)
-int gpf_debug_diag_stamps(unsigned long long* out, int n) {
-  if (!out || n <= 0) return GPF_BAD_ARG;
-  hipDeviceSynchronize();
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gpf::g_diag_stamps), sizeof(unsigned long long) * std::min(n, gpf::DIAG_NSTAMPS)) !=
-      hipSuccess)
-    return GPF_HIP_ERROR;
-  return GPF_OK;
-}
-#endif
 
 }  // extern "C"
 

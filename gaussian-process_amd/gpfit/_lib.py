@@ -43,7 +43,7 @@ SIGNATURES = {
     "gpf_reset_profile": (ctypes.c_int, [_vp]),
     "gpf_selftest_mfma": (ctypes.c_int, [_vp, _dp, _dp, _dp]),
     "gpf_debug_factor": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _dp]),
-    "gpf_debug_factor64": (ctypes.c_int, [_vp, _dp, _dp, _ip]),
+    "gpf_debug_factor128": (ctypes.c_int, [_vp, _dp, _dp, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _ip, _dp]),
     "gpf_mfma_peak": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _dp]),
     "gpf_prob_surface": (ctypes.c_int, [_vp, _dp, ctypes.c_int64, ctypes.c_int, _dp, _dp,
                                         ctypes.POINTER(ctypes.c_int)]),
@@ -285,13 +285,18 @@ class Context:
             self._check(rc, "gpf_debug_factor")
         return L, U, z, al
 
-    def debug_factor64(self, a):
-        """factor64 on two 64x64 matrices a[2,64,64]: (L[2], X[2], bad[2]) (diagnostic)."""
-        a = np.ascontiguousarray(a, dtype=np.float64).reshape(2, 64, 64)
-        out = np.empty((4, 64, 64))
-        bad = np.zeros(2, dtype=np.int32)
-        self._check(self.lib.gpf_debug_factor64(self._h, _ptr(a), _ptr(out), bad.ctypes.data_as(_ip)), "gpf_debug_factor64")
-        return out[0::2], out[1::2], bad
+    def debug_factor128(self, a, y):
+        """factor128 on n 128x128 blocks a[n,128,128] with right-hand sides y[n,128] (diagnostic):
+        dict of L, U, z, s2, sz, bad, cycles (shader cycles per block)."""
+        a = np.ascontiguousarray(a, dtype=np.float64).reshape(-1, 128, 128)
+        n = a.shape[0]
+        y = np.ascontiguousarray(y, dtype=np.float64).reshape(n, 128)
+        L, U = np.empty_like(a), np.empty_like(a)
+        z, s2, sz, cyc = np.empty((n, 128)), np.empty((n, 128)), np.empty((n, 128)), np.empty(n)
+        bad = np.zeros(n, dtype=np.int32)
+        self._check(self.lib.gpf_debug_factor128(self._h, _ptr(a), _ptr(y), n, _ptr(L), _ptr(U), _ptr(z), _ptr(s2),
+                                                 _ptr(sz), bad.ctypes.data_as(_ip), _ptr(cyc)), "gpf_debug_factor128")
+        return {"L": L, "U": U, "z": z, "s2": s2, "sz": sz, "bad": bad, "cycles": cyc}
 
     def mfma_peak(self, blocks=1024, iters=4096):
         out = ctypes.c_double(0.0)

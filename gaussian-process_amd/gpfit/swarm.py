@@ -291,5 +291,7 @@ def particle_swarm(x_known, y_known, e_known, PSO_progress, *, num_particles=NUM
         print("Value of loss function:")
         print(sw.gbest)
         print(f"Total soft restarts: {sw.restarts}")
+    comm = score.comm
     return sw.gbest_pos, {"score": sw.gbest, "restarts": sw.restarts, "evals": sw.evals,
-                          "local_evals": score.evals}
+                          "local_evals": score.evals, "transport": comm.transport if comm is not None else None,
+                          "exchange": comm.stats() if comm is not None else None}

@@ -242,11 +242,13 @@ int gpf_selftest_mfma(gpf_ctx* ctx, const double* a, const double* b, double* c)
  * forward-substituted RHS z (Npad) and alpha (N). Npad = ceil(N/128)*128. */
 int gpf_debug_factor(gpf_ctx* ctx, const double* ls, double* L, double* U, double* z, double* alpha);
 
-/* Diagnostic: the 64x64 diagonal-leaf factor (factor64 in csrc/gpf_factor.hip) on two
- * host matrices in a row. in: 2 x 64 x 64 row-major (lower triangles read); out: per
- * matrix L then X = L^-1 (4 x 64 x 64, zeros above the diagonals); bad[k] != 0 when a
- * pivot of matrix k was not > 0. */
-int gpf_debug_factor64(gpf_ctx* ctx, const double* in, double* out, int* bad);
+/* Diagnostic / measurement: the 128x128 diagonal-block factor of the factorisation (factor128 in
+ * csrc/gpf_diag.hip) on n blocks, one workgroup each. A: n x 128 x 128 row-major (lower triangles
+ * read), y: n x 128. Out: L (zeros above the diagonal), U = L^-1 (likewise), z = U y, s2 / sz =
+ * the column partials colsum(U o U) and U^T z, bad[b] = 1 where a pivot was not > 0, cycles
+ * (nullable): each workgroup's shader cycles. */
+int gpf_debug_factor128(gpf_ctx* ctx, const double* A, const double* y, int n, double* L, double* U, double* z,
+                        double* s2, double* sz, int* bad, double* cycles);
 
 /* Diagnostic: measured FP64 MFMA throughput (TFLOP/s) of a register-only
  * v_mfma_f64_16x16x4_f64 loop over `blocks` workgroups of 4 waves. */

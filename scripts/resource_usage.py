@@ -17,7 +17,7 @@ KEYS = ["VGPRs", "AGPRs", "TotalSGPRs", "VGPRs Spill", "SGPRs Spill", "ScratchSi
 def main():
     with tempfile.TemporaryDirectory() as td:
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-               "-Wno-unused-value", "-Wno-unused-result", "--cuda-device-only", "-c",
+               "-Wno-unused-value", "-Wno-unused-result", "-mllvm", "--amdgpu-mfma-vgpr-form", "--cuda-device-only", "-c",
                "-Rpass-analysis=kernel-resource-usage", SRC, "-o", os.path.join(td, "dev.o")] + sys.argv[1:]
         r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode:

@@ -216,3 +216,43 @@ def test_rccl_exchange_single_rank():
     finally:
         comm.close()
         ctx.close()
+
+
+def _rccl_worker(rank, world, port, path, k, q):
+    """One rank per GPU over RCCL (the driver's N-GPU bench path): rank r on device r."""
+    _env(rank, world, port, GPFIT_DEVICE=str(rank), GPF_COMM_TRANSPORT="rccl")
+    import contextlib
+    import io
+    from gpfit.swarm import particle_swarm
+    f4 = np.load(path, allow_pickle=False)
+    x = np.asfortranarray(f4[f"c{k}_x"])
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        best, info = particle_swarm(x, f4[f"c{k}_y"], f4[f"c{k}_e"], True, init_positions=f4[f"c{k}_init"],
+                                    seed=int(f4[f"c{k}_seed"]), max_iter=150)
+    q.put((rank, best.tolist(), buf.getvalue(), info["local_evals"], info["evals"], info["transport"],
+           list(info["exchange"])))
+
+
+@pytest.mark.gpu
+def test_rccl_sharded_swarm_multi_gpu():
+    """RCCL with more than one rank: on a box with G >= 2 GPUs, min(G, 8) ranks,
+    one per GPU, each scoring its rows with gpf_eval_batch_sharded and exchanging over RCCL
+    (ncclAllReduce over xGMI); every rank's trajectory equals the single-rank GPU run bit for bit,
+    every particle scored once, and the exchange timing is recorded. Skipped on one-GPU boxes."""
+    import torch
+    n = min(torch.cuda.device_count(), 8)
+    if n < 2:
+        pytest.skip(f"{n} GPU visible: RCCL across ranks needs one GPU per rank")
+    from conftest import GOLDEN
+    path = str(GOLDEN / "f4_pso_trace.npz")
+    one = _spawn(_gpu_worker, 1, path, 0, timeout=600)[0]
+    res = _spawn(_rccl_worker, n, path, 0, timeout=600)
+    total_local = 0
+    for rank, best, log, local, evals, transport, (ms, count) in res:
+        assert best == one[1], rank
+        assert log == one[2], rank
+        assert transport == "rccl" and count > 0 and ms >= 0.0, (rank, transport, ms, count)
+        total_local += local
+    assert total_local == res[0][4] == one[4]
+

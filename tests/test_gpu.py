@@ -1000,28 +1000,55 @@ def test_handoff_timeout_is_reported(ctx, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_factor64(ctx):
-    """The 64x64 diagonal-leaf factor (csrc/gpf_factor.hip factor64) against LAPACK:
-    L = cholesky(A), X = L^-1, exact zeros above both diagonals, pivot failure flagged.
-    Matrices: a well-conditioned SPD one and a kernel-like one (SE covariance of 64 sorted
-    points + noise, the diagonal blocks k_step factors; cond ~1e8)."""
-    rng = np.random.default_rng(64)
-    g = rng.standard_normal((64, 64))
-    a0 = g @ g.T / 64 + np.eye(64)
-    t = np.sort(rng.uniform(size=64))
-    a1 = np.exp(-0.5 * (t[:, None] - t[None, :]) ** 2 / 0.2 ** 2) + np.diag(rng.uniform(1e-4, 1e-3, 64))
-    up = np.triu(np.full((64, 64), 7.0), 1)  # garbage above the diagonal must not be read
-    L, X, bad = ctx.debug_factor64(np.stack([np.tril(a0) + up, np.tril(a1) + up]))
-    assert bad.tolist() == [0, 0]
-    for k, a in enumerate((a0, a1)):
+def test_factor128(ctx):
+    """The 128x128 diagonal-block factor (csrc/gpf_diag.hip factor128, 16-blocked) against LAPACK:
+    L = cholesky(A), U = L^-1, z = U y, the column partials colsum(U o U) and U^T z; exact zeros
+    above both diagonals; garbage above A's diagonal never read; a padded block (identity in its
+    lower right) factors to the identity there; a pivot that is not > 0 flagged. Matrices: a
+    well-conditioned SPD one and kernel-like ones (SE covariance of 128 points + noise, the diagonal
+    blocks the factorisation meets; cond up to ~1e8)."""
+    rng = np.random.default_rng(128)
+    n = 128
+    g = rng.standard_normal((n, n))
+    a0 = g @ g.T / n + np.eye(n)
+    t = np.sort(rng.uniform(size=n))
+    a1 = np.exp(-0.5 * (t[:, None] - t[None, :]) ** 2 / 0.2 ** 2) + np.diag(rng.uniform(1e-4, 1e-3, n))
+    xs = rng.uniform(size=(3, n))
+    r2 = sum((xs[k][:, None] - xs[k][None, :]) ** 2 for k in range(3)) / 0.3 ** 2
+    a2 = np.exp(-0.5 * r2) + 0.01 * np.eye(n)
+    a3 = a2.copy()  # padded: rows / columns 100.. are the identity, as the K build pads
+    a3[100:, :] = 0.0
+    a3[:, 100:] = 0.0
+    a3[100:, 100:] = np.eye(n - 100)
+    mats = [a0, a1, a2, a3]
+    up = np.triu(np.full((n, n), 7.0), 1)  # garbage above the diagonal must not be read
+    A = np.stack([np.tril(a) + up for a in mats])
+    Y = rng.standard_normal((len(mats), n))
+    Y[3, 100:] = 0.0
+    out = ctx.debug_factor128(A, Y)
+    assert out["bad"].tolist() == [0, 0, 0, 0]
+    for k, a in enumerate(mats):
+        L, U, z = out["L"][k], out["U"][k], out["z"][k]
         Lr = np.linalg.cholesky(a)
-        assert np.all(np.triu(L[k], 1) == 0) and np.all(np.triu(X[k], 1) == 0)
+        Ur = np.linalg.inv(Lr)
+        assert np.all(np.triu(L, 1) == 0) and np.all(np.triu(U, 1) == 0)
         cond = np.linalg.cond(a)
-        assert np.abs(L[k] - Lr).max() <= 1e-13 * np.abs(Lr).max() * max(1.0, np.sqrt(cond))
-        assert np.abs(L[k] @ L[k].T - a).max() <= 1e-14 * 64 * np.abs(a).max()
-        assert np.abs(X[k] @ L[k] - np.eye(64)).max() <= 1e-15 * 64 * cond
-    # a pivot that is not > 0: flagged (numpy raises LinAlgError, GP_func.py:22)
-    a2 = a0.copy()
-    a2[40, 40] = -1.0
-    _, _, bad = ctx.debug_factor64(np.stack([np.tril(a0), np.tril(a2)]))
-    assert bad.tolist() == [0, 1]
+        assert np.abs(L - Lr).max() <= 1e-13 * np.abs(Lr).max() * max(1.0, np.sqrt(cond))
+        assert np.abs(L @ L.T - a).max() <= 1e-14 * n * np.abs(a).max()
+        assert np.abs(U @ L - np.eye(n)).max() <= 1e-15 * n * cond
+        assert np.abs(z - Ur @ Y[k]).max() <= 1e-15 * n * cond * max(1.0, np.abs(Y[k]).max())
+        np.testing.assert_allclose(out["s2"][k], np.sum(U * U, axis=0), rtol=1e-15 * n * cond, atol=0)
+        np.testing.assert_allclose(out["sz"][k], U.T @ z, rtol=1e-15 * n * cond,
+                                   atol=1e-15 * n * cond * np.abs(U.T @ z).max())
+    np.testing.assert_array_equal(out["L"][3][100:, 100:], np.eye(n - 100))
+    np.testing.assert_array_equal(out["U"][3][100:, 100:], np.eye(n - 100))
+    np.testing.assert_array_equal(out["z"][3][100:], 0.0)
+    assert np.all(out["cycles"] > 0)
+    # a pivot that is not > 0: flagged (numpy raises LinAlgError, GP_func.py:22); in every panel
+    bads = []
+    for piv in (5, 40, 77, 127):
+        ab = a0.copy()
+        ab[piv, piv] = -1.0
+        bads.append(np.tril(ab))
+    out = ctx.debug_factor128(np.stack([np.tril(a0)] + bads), np.zeros((5, n)))
+    assert out["bad"].tolist() == [0, 1, 1, 1, 1]
