@@ -503,28 +503,36 @@ __host__ __device__ constexpr int tri_chunk(int m) { return 16 * TRI_LD * (8 * m
 // U (row-major, leading dimension ld, lower triangle read) -> LDS: 576 chunk rows of 16 doubles,
 // 8 pairs each, 9 pairs per thread through registers (the odd stride rules out direct-to-LDS
 // transfers). Ends with a barrier.
+__device__ __forceinline__ int tri_row_chunk(int ri, int& rr) {  // chunk row ri (0..575) -> chunk m, row rr in it
+  int m = 0, base = 0;
+#pragma unroll
+  for (int mm = 0; mm < 7; ++mm)
+    if (ri >= base + 16 * (8 - m)) {
+      base += 16 * (8 - m);
+      ++m;
+    }
+  rr = ri - base;
+  return m;
+}
 __device__ __forceinline__ void tri_to_lds(const double* __restrict__ U, size_t ld, double* s) {
-  const int tid = threadIdx.x;
+  int tid = threadIdx.x;
   d2 v[9];
-  int dst[9];
 #pragma unroll
   for (int u = 0; u < 9; ++u) {
     const int i = tid + DNTH * u, ri = i >> 3, kp = i & 7;  // chunk row ri (0..575), pair kp
-    int m = 0, base = 0;
-#pragma unroll
-    for (int mm = 0; mm < 7; ++mm)
-      if (ri >= base + 16 * (8 - m)) {
-        base += 16 * (8 - m);
-        ++m;
-      }
-    const int rr = ri - base;  // row 16 m + rr of U
+    int rr;
+    const int m = tri_row_chunk(ri, rr);  // row 16 m + rr of U
     v[u] = *reinterpret_cast<const d2*>(U + (size_t)(16 * m + rr) * ld + 16 * m + 2 * kp);
-    dst[u] = tri_chunk(m) + rr * TRI_LD + 2 * kp;
   }
+  asm volatile("" : "+v"(tid));  // (the destinations are recomputed: not 9 more registers held across the loads)
 #pragma unroll
   for (int u = 0; u < 9; ++u) {
-    s[dst[u]] = v[u].x;
-    s[dst[u] + 1] = v[u].y;
+    const int i = tid + DNTH * u, ri = i >> 3, kp = i & 7;
+    int rr;
+    const int m = tri_row_chunk(ri, rr);
+    const int dst = tri_chunk(m) + rr * TRI_LD + 2 * kp;
+    s[dst] = v[u].x;
+    s[dst + 1] = v[u].y;
   }
   __syncthreads();
 }

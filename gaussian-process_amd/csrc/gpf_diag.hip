@@ -68,11 +68,6 @@ __device__ __forceinline__ void lsync() { asm volatile("s_waitcnt lgkmcnt(0)\n\t
 // 1/sqrt(p) for the pivots of the diagonal factor: v_rsq_f64 and two Newton steps
 // (y += y (1/2 - p/2 y^2)), a short dependent chain instead of the ~25 ops of a correctly
 // rounded sqrt followed by a division; within a few ulp of 1/sqrt(p).
-__device__ __forceinline__ double rsqrt_nr1(double p) {  // (probe A/B: one Newton step)
-  double y = __builtin_amdgcn_rsq(p);
-  const double t = fma(-((0.5 * p) * y), y, 0.5);
-  return fma(y, t, y);
-}
 __device__ __forceinline__ double rsqrt_nr(double p) {
   double y = __builtin_amdgcn_rsq(p);
   const double h = 0.5 * p;
@@ -192,20 +187,12 @@ __host__ __device__ constexpr int db_q_wave(int k, int i) {
 // of A (columns <= r), lane 16 + c column c of X_kk = L_kk^-1 (the identity to start), lane 32 the
 // block's 16 entries of y. Every role takes the same update, x[s] -= m * L(s, q), with its
 // multiplier m (A: L(r, q); X: X(q, c); y: z_q) — one fma per entry and column for the whole wave.
-// Column q: the pivot from lane q (v_readlane), 1/sqrt by v_rsq + Newton, the scaled column; the
-// entry the next pivot needs, L(q+1, q), by v_readlane (the chain); the others go through LDS
-// (column q written by lanes 0..15, read back as broadcasts) and are applied one column later,
-// beside the next pivot's chain: a v_readlane pair per entry, its hazard wait and a scalar-operand
-// fma per entry (round 4) cost ~550 cycles per column, issue-bound. Writes L_kk (zeros above the
-// diagonal) to global, X_kk to the LDS diagonal slot (its column buffer during the panel) and to
+// Writes L_kk (zeros above the diagonal) to global, X_kk to the LDS diagonal slot and to
 // U, z_k to the LDS y. Returns whether a pivot was not > 0.
-#ifndef GPF_DB_PANEL
-#define GPF_DB_PANEL 0  // probe A/B: 0 = LDS broadcast, one column deferred; 1 = v_readlane for every entry
-#endif
-template <bool WT, int VAR = GPF_DB_PANEL>
+template <bool WT>
 __device__ __forceinline__ bool db_panel(double* lds, int k, double* __restrict__ Lt, double* __restrict__ Ut, size_t ld) {
   const int r = threadIdx.x & 63;
-  double* blk = lds + db_bid(k, k) * DB_BLK;  // A_kk; the column buffer [q][s] during the panel; X_kk
+  double* blk = lds + db_bid(k, k) * DB_BLK;  // A_kk; then X_kk
   const bool arow = r < 16, xcol = r >= 16 && r < 32, ylane = r == 32;
   int ro = r;
   asm volatile("" : "+v"(ro));  // (an opaque lane index: the initial values are not kept live across panels)
@@ -217,80 +204,16 @@ __device__ __forceinline__ bool db_panel(double* lds, int k, double* __restrict_
     x[c] = arow ? (c <= ro ? va : 0.0) : (xcol ? (c == ro - 16 ? 1.0 : 0.0) : (ylane ? vy : 0.0));
   }
   bool bad = false;
-  double mprev = 0.0, cv[16];
-  if constexpr (VAR == 4) {
-    // the uniform pivot chain (below) and few VALU instructions per column: the entries s = q+1,
-    // q+2 of column q by v_readlane (the next alpha / beta need them one step later), the others
-    // through LDS (column q written by the A lanes, read back as broadcasts, applied one step later:
-    // a full column of slack for the LDS round trip)
-    double p = readlane_f64(x[0], 0);
-    double alpha = readlane_f64(x[0], 1), beta = readlane_f64(x[1], 1);
-    double inv = rsqrt_nr(p);
-    bad = !(p > 0.0);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const double m = (arow && r < q) ? 0.0 : x[q] * inv;
-      x[q] = m;
-      double inv_next = 0.0;
-      if (q < 15) {  // the chain
-        const double l1 = alpha * inv;
-        const double p1 = fma(-l1, l1, beta);
-        bad = bad | !(p1 > 0.0);
-        inv_next = rsqrt_nr(p1);
-      }
-      if (q + 3 < 16 && arow) blk[q * 16 + r] = m;  // column q for the entries s >= q+3
-#pragma unroll
-      for (int s = q + 1; s < 16 && s <= q + 2; ++s) x[s] = fma(-m, readlane_f64(m, s), x[s]);
-      if (q >= 1) {  // column q-1's entries s >= q+2, read back at step q-1
-#pragma unroll
-        for (int s = q + 2; s < 16; ++s) {
-          x[s] = fma(-mprev, cv[s], x[s]);
-          asm volatile("" : "+v"(x[s]));
-        }
-      }
-      if (q + 2 < 16) {  // the next step's alpha, beta: row q+2's entries in columns q+1, q+2
-        alpha = readlane_f64(x[q + 1], q + 2);
-        beta = readlane_f64(x[q + 2], q + 2);
-      }
-      if (q + 3 < 16) {
-#pragma unroll
-        for (int s = q + 3; s < 16; ++s) cv[s] = blk[q * 16 + s];  // (broadcasts)
-      }
-      mprev = m;
-      inv = inv_next;
-    }
-  } else if constexpr (VAR >= 2) {
-    // The pivot chain on uniform values, off the lanes: p_{q+1} = beta - (alpha inv_q)^2 with alpha,
-    // beta = row q+1's entries in columns q and q+1 after the columns < q (read from lane q+1 one
-    // step ahead) — the same operations lane q+1 applies to its own diagonal entry, so bitwise the
-    // same pivot; per column the chain is a mul, an fma and 1/sqrt, no cross-lane traffic.
-    double p = readlane_f64(x[0], 0);
-    double alpha = readlane_f64(x[0], 1), beta = readlane_f64(x[1], 1);
-    double inv = VAR == 3 ? rsqrt_nr1(p) : rsqrt_nr(p);
-    bad = !(p > 0.0);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const double m = (arow && r < q) ? 0.0 : x[q] * inv;
-      x[q] = m;
-      double inv_next = 0.0;
-      if (q < 15) {
-        const double l1 = alpha * inv;
-        const double p1 = fma(-l1, l1, beta);
-        bad = bad | !(p1 > 0.0);
-        inv_next = VAR == 3 ? rsqrt_nr1(p1) : rsqrt_nr(p1);
-      }
-#pragma unroll
-      for (int s = q + 1; s < 16; ++s) {
-        x[s] = fma(-m, readlane_f64(m, s), x[s]);
-        if (s == q + 2 && q + 2 < 16) {  // the next step's alpha, beta from lane q+2
-          alpha = readlane_f64(x[q + 1], q + 2);
-          beta = readlane_f64(x[q + 2], q + 2);
-        }
-        if (((s - q) & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-      }
-      inv = inv_next;
-    }
-  } else
+  // Column q: pivot from lane q, 1/sqrt by v_rsq + Newton, scale, then the rank-1 update of every
+  // later entry s of the lane's row with L(s, q) by v_readlane, in column order (each entry takes
+  // its updates q = 0, 1, .. in sequence, as a right-looking potrf does: an exactly singular
+  // block then ends with the same pivot rounding as LAPACK's column order, tests/test_gpu.py::
+  // test_not_positive_definite_raises_like_numpy). Measured variants (probe
+  // scripts/probes/f128_probe.hip, profiles/r5/f128_panel_variants.txt), cycles per column on one
+  // wave: this one 426; one column deferred through an LDS broadcast buffer 439-441 (and it
+  // reordered the updates); the pivot chain on uniform values, one step ahead 456-460; that with
+  // one Newton step 439-443; uniform chain + LDS buffer 436-440. The column is VALU issue and
+  // latency bound (~40 dependent f64 ops), not bound by the readlanes.
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const double p = readlane_f64(x[q], q);
@@ -298,32 +221,11 @@ __device__ __forceinline__ bool db_panel(double* lds, int k, double* __restrict_
     const double inv = rsqrt_nr(p);
     const double m = (arow && r < q) ? 0.0 : x[q] * inv;
     x[q] = m;
-    if constexpr (VAR == 1) {
 #pragma unroll
-      for (int s = q + 1; s < 16; ++s) {
-        x[s] = fma(-m, readlane_f64(m, s), x[s]);
-        if (((s - q) & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-      }
-      continue;
+    for (int s = q + 1; s < 16; ++s) {
+      x[s] = fma(-m, readlane_f64(m, s), x[s]);
+      if (((s - q) & 3) == 0) __builtin_amdgcn_sched_barrier(0);
     }
-    if (q < 15) {  // the next pivot's entry first
-      const double l1 = readlane_f64(m, q + 1);
-      x[q + 1] = fma(-m, l1, x[q + 1]);
-    }
-    if (q < 14 && arow) blk[q * 16 + r] = m;  // column q for the entries s >= q+2
-    if (q >= 1) {  // column q-1's deferred entries s >= q+1 (read back at step q-1)
-#pragma unroll
-      for (int s = q + 1; s < 16; ++s) {
-        x[s] = fma(-mprev, cv[s], x[s]);
-        asm volatile("" : "+v"(x[s]));  // (applied here: sunk to each entry's next use, the read-back
-                                        // values of every column stayed live and spilled)
-      }
-    }
-    if (q < 14) {
-#pragma unroll
-      for (int s = q + 2; s < 16; ++s) cv[s] = blk[q * 16 + s];  // (uniform addresses: broadcasts)
-    }
-    mprev = m;
   }
   // (the diagonal row's own entries right of its pivot took updates with m = L(q, q): not stored)
   if (arow) {

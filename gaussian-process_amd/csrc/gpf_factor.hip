@@ -467,13 +467,16 @@ __device__ __forceinline__ bool wait_diag(const int* flag, int J, int* info, int
 //   R  once all np are in, the 8 np waves of the pieces sum the slots' 128 1-KiB units (slot
 //      order, so results are deterministic), 16 slots per round trip, into slot 0 in place, and
 //      count each unit in on its wave region's counter (c[1 + r]);
-//   T  the pieces 0..min(np,8)-1 wait for the diagonal block (U_JJ, z_J), stage U_JJ, and wave v
-//      of piece s finishes region r = s + np v (< 8) once its 16 units are in: the triangular
-//      multiply, the stores (write-through for L tiles) and y_I (L) or the column partials (U);
-//      an L tile's region counts in on c[9];
-//   C  (L tiles) once all 8 regions are in, the 8 np waves take the 36 lower 16x16 blocks of
-//      A_II -= L_IJ L_IJ^T, each 32 MFMAs over k ascending with A_II as the seed — the per-element
-//      MFMA sequence of syrk_rows.
+//   T  the pieces 0..min(np,8)-1 load their regions' sums, wait for the diagonal block (U_JJ,
+//      z_J) and stage U_JJ; wave v of piece s finishes region r = s + np v (< 8): the triangular
+//      multiply, the stores and y_I (L tiles) or the column partials (U tiles); an L tile's wave
+//      also leaves its rows of L_IJ in slot 1 in the MFMA operand layout and counts in again;
+//   C  (L tiles) the 8 np waves take the 36 lower 16x16 blocks of A_II -= L_IJ L_IJ^T, block
+//      (ib, jb) as soon as the regions of slabs ib and jb are in: 32 MFMAs over k ascending with
+//      A_II as the seed — the per-element MFMA sequence of syrk_rows.
+// A tile of one piece (ONE: the early launches) runs the same phases T and C on its own
+// registers. r5, single-particle prediction N=4096: per launch ~70 us, of which the
+// finish after the diagonal block ~26 us (T ~10, C ~12; profiles/r5/predict_trace_*.txt).
 // Every wait is bounded (`spins`; timeout: info bit 2, the wave or piece leaves). No wait can hold
 // the slots an awaited workgroup needs: the diagonal workgroups come first in the launch and wait
 // for nothing; the np <= SPLIT_MAXS pieces of a tile have consecutive workgroup ids, which the
@@ -481,11 +484,14 @@ __device__ __forceinline__ bool wait_diag(const int* flag, int J, int* info, int
 // 4 pieces of a tile — a stalled XCD (64 slots) would need all its slots taken by pieces of the
 // lowest incomplete tile. Counters: FLAT_CNT words per (particle, launch, tile), zeroed by the
 // factorisation's memset, never reused within it.
-constexpr int FLAT_CNT = 16;  // [0] partials stored, [1 + r] units of region r summed, [9] L regions finished
+constexpr int FLAT_CNT = 16;  // [0] partials stored; [1 + r]: units of region r summed (16), + 1 once an L tile's
+                              // region is finished (its phase-C operands stored)
 __host__ __device__ __forceinline__ int split_cnt_stride(int nt) {  // counter words per split tile and particle
   return SPLIT_CNT > FLAT_CNT * nt ? SPLIT_CNT : FLAT_CNT * nt;
 }
-__device__ __forceinline__ int region_slab(int r) { return r < 4 ? r : 11 - r; }  // Quad<128>::cb / 16 of wave r
+// Quad<128>::cb / 16 of wave r: the column slab held in wave region r of a slot (an involution, so
+// also the region of slab s)
+__device__ __forceinline__ int region_slab(int r) { return r < 4 ? r : 11 - r; }
 
 // Bounded wave-level wait for *c >= n, then an agent-scope acquire; true: timed out (info bit 2).
 __device__ __forceinline__ bool wave_wait(const unsigned* c, unsigned n, int* info, int spins) {
@@ -558,33 +564,57 @@ __device__ __forceinline__ void flat_load_region(Acc<T>& acc, const double* pt, 
     }
 }
 
+// Phase T leaves each finished L region's rows of L_IJ in slot 1 in the MFMA operand layout: the
+// triangular multiply's output lane (g, c) holds L(cb + c, 4 t + g) for t = 0..31 — exactly the
+// A/B operand of k-step t of a 16x16 block product — stored as 16 pairs (t, t+1), 1 KiB per wave
+// instruction. Phase C's operands are then 16 coalesced 16-B loads per slab, not 32 strided 8-B
+// row reads.
+__device__ __forceinline__ void flat_store_operand(const d4 (&o)[2], double* slot1, int r, int P) {
+  const int lane = threadIdx.x & 63;
+  const auto ws = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(slot1), 0, T * T * 8, 0x00020000);
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; e += 2)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, d2{o[j][e], o[j][e + 1]}), ws, lane * 16,
+                                             r * NODE_WAVE + (2 * (2 * P + j) + e / 2) * 1024, 16);  // write-through
+}
+__device__ __forceinline__ void flat_load_operand(double (&a)[32], const double* slot1, int r) {
+  const int lane = threadIdx.x & 63;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(slot1), 0, T * T * 8, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const d2 v = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, r * NODE_WAVE + i * 1024, 0));
+    a[2 * i] = v.x;
+    a[2 * i + 1] = v.y;
+  }
+}
+
 // Phase C: block (ib, jb) (ib >= jb) of A_II -= L_IJ L_IJ^T: 32 MFMAs, k = 4 t + (lane >> 4)
 // ascending, seeded with A_II (syrk_rows' operands and order per element).
-__device__ __forceinline__ void flat_syrk_block(double* Aii, const double* Lij, size_t ld, int ib, int jb) {
+__device__ __forceinline__ void flat_syrk_block(double* Aii, size_t ld, const double* slot1, int ib, int jb) {
   const int lane = threadIdx.x & 63, g = lane >> 4, cl = lane & 15;
-  const double* ar = launder(Lij + (size_t)(16 * ib + cl) * ld + g);
-  const double* br = launder(Lij + (size_t)(16 * jb + cl) * ld + g);
   double* cp = launder(Aii + (size_t)(16 * ib + g) * ld + 16 * jb + cl);
   d4 acc;
 #pragma unroll
   for (int r = 0; r < 4; ++r) acc[r] = cp[(size_t)(4 * r) * ld];
+  double a[32];
+  flat_load_operand(a, slot1, region_slab(ib));
+  if (ib == jb) {
 #pragma unroll
-  for (int t0 = 0; t0 < 32; t0 += 16) {  // 16 k-steps of operands per round trip
-    double a[16], b[16];
+    for (int t = 0; t < 32; ++t) acc = mfma_neg_a(a[t], a[t], acc);
+  } else {
+    double b[32];
+    flat_load_operand(b, slot1, region_slab(jb));
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      a[t] = ar[4 * (t0 + t)];
-      b[t] = br[4 * (t0 + t)];
-    }
-#pragma unroll
-    for (int t = 0; t < 16; ++t) acc = mfma_neg_a(a[t], b[t], acc);
+    for (int t = 0; t < 32; ++t) acc = mfma_neg_a(a[t], b[t], acc);
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) cp[(size_t)(4 * r) * ld] = acc[r];
 }
 
 // One piece (sidx of np) of tile w of launch J under the flat finish (see above); LT: an L tile.
-template <bool LT>
+template <bool LT, bool ONE>
 __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad, double* __restrict__ Lp,
                                         double* __restrict__ Up, double* __restrict__ yp, double* __restrict__ s2p,
                                         double* __restrict__ szp, int* __restrict__ info, int N,
@@ -600,41 +630,50 @@ __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   double* pt = part + (size_t)(p * (nt - 1) + w) * S2 * T * T;
   unsigned* ca = cnt + (size_t)p * (nt - 1) * split_cnt_stride(nt) + (size_t)(J * (nt - 1) + w) * FLAT_CNT;
-  // A: the partial (piece 0 of an L tile seeded with the covariance tile A_IJ^T)
-  {
-    Acc<T> acc;
-    if (LT)
-      split_gemm<false, true, true>(acc, Lp + (size_t)J * T * ld, Npad, Lp + (size_t)I * T * ld, Npad, J * T / DL_KC,
-                                    np, sidx, lds, qd,
-                                    [&](Acc<T>& a) { cov_tile_acc(a, qd, x, lp, d, N, J, I, lds); });
-    else  // (the triangular first block runs dense: its upper part holds zeros)
-      split_gemm<true, false, false>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
-                                     Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T / DL_KC, np, sidx, lds,
-                                     qd, [](Acc<T>&) {});
+  // A: the partial (piece 0 of an L tile seeded with the covariance tile A_IJ^T). ONE (a tile of one
+  // piece, np = 1): the whole GEMM, kept in the registers — wave v's accumulators are region v.
+  Acc<T> acc;
+  if (LT)
+    split_gemm<false, true, true>(acc, Lp + (size_t)J * T * ld, Npad, Lp + (size_t)I * T * ld, Npad, J * T / DL_KC,
+                                  np, sidx, lds, qd, [&](Acc<T>& a) { cov_tile_acc(a, qd, x, lp, d, N, J, I, lds); });
+  else if (ONE) {  // (U_KK is lower triangular: the wave's first chunks add zeros, skipped)
+    acc.zero();
+    gemm_stream_dl<true, false, TRI_B_KGEC>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
+                                            Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T, lds, qd);
+  } else  // (the triangular first block runs dense: its upper part holds zeros)
+    split_gemm<true, false, false>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
+                                   Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T / DL_KC, np, sidx, lds, qd,
+                                   [](Acc<T>&) {});
+  if (!ONE) {
     store_node(acc, pt + (size_t)sidx * T * T, qd);
+    acc.zero();  // (dead until phase T reloads it: a constant, not 64 registers held across phase R)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's part of the partial drained
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(ca, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    GPF_PHASE(3);
+    if (group_wait(ca, (unsigned)np, info, spins, sflag)) return;
+    // R
+    for (int u = sidx * 8 + wave; u < 128; u += 8 * np) {
+      flat_reduce_unit(pt, np, u);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (qd.lane == 0) __hip_atomic_fetch_add(ca + 1 + (u >> 4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's part of the partial drained
-  __syncthreads();
-  if (tid == 0) __hip_atomic_fetch_add(ca, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  GPF_PHASE(3);
-  if (group_wait(ca, (unsigned)np, info, spins, sflag)) return;
-  // R
-  for (int u = sidx * 8 + wave; u < 128; u += 8 * np) {
-    flat_reduce_unit(pt, np, u);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (qd.lane == 0) __hip_atomic_fetch_add(ca + 1 + (u >> 4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // T
+  GPF_PHASE(0);
+  // T (the region's sum is loaded before the wait for the diagonal block: its latency hides there)
+  double* slot1 = pt + (size_t)T * T;
   if (sidx < 8) {
     double* zj = lds + STEP_ZJ;
+    const int r = sidx + np * wave;  // the region this wave finishes
+    bool late = false;
+    if (!ONE && r < 8) {
+      late = wave_wait(ca + 1 + r, 16u, info, spins);
+      if (!late) flat_load_region(acc, pt, r);
+    }
     if (wait_diag(dflag + p, J, info, spins, sflag)) return;  // U_JJ, z_J
     if (tid < T) zj[tid] = yp[J * T + tid];
     tri_to_lds(Up + (size_t)J * T * ld + (size_t)J * T, ld, lds);  // (its barrier also publishes z_J)
-    const int r = sidx + np * wave;  // the region this wave finishes
-    if (r < 8) {
-      if (wave_wait(ca + 1 + r, 16u, info, spins)) return;
-      Acc<T> acc;
-      flat_load_region(acc, pt, r);
+    if (r < 8 && !late) {
       const int cb = 16 * region_slab(r);
       if (LT) {
         // L_IJ^T = U_JJ D for the slab's 16 columns of D (rows cb.. of L_IJ); y_I -= L_IJ z_J
@@ -649,18 +688,19 @@ __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad
             case 2: trmm_acc<2, false>(o, acc, lds); break;
             default: trmm_acc<3, false>(o, acc, lds); break;
           }
+          flat_store_operand(o, slot1, r, P);
 #pragma unroll
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              gst<true>(lrow + 16 * (2 * P + j) + 4 * e, o[j][e]);
+              lrow[16 * (2 * P + j) + 4 * e] = o[j][e];
               yr = fma(o[j][e], zj[16 * (2 * P + j) + 4 * e + g], yr);
             }
         }
         yr = sum_lane_groups(yr);
         if (g == 0) yp[I * T + cb + cl] = yp[I * T + cb + cl] - yr;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the region's L drained
-        if (qd.lane == 0) __hip_atomic_fetch_add(ca + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the region's operands drained
+        if (qd.lane == 0) __hip_atomic_fetch_add(ca + 1 + r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         // U_JK = -U_JJ W; the column partials of colsum(U^2) and U^T z (per half, then summed)
         double* ucol = launder(Up + (size_t)(J * T + g) * ld + (size_t)K * T + cb + cl);
@@ -699,18 +739,21 @@ __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad
       }
     }
   }
+  GPF_PHASE(1);
   if (!LT) return;
   // C
-  const int q0 = sidx * 8 + wave;
-  if (q0 >= 36) return;
-  if (wave_wait(ca + 9, 8u, info, spins)) return;
+  // (block b = ib (ib + 1) / 2 + jb waits for the regions of slabs ib and jb only)
+  const unsigned ready = ONE ? 1u : 17u;
   double* Aii = Lp + (size_t)I * T * ld + (size_t)I * T;
-  const double* Lij = Lp + (size_t)I * T * ld + (size_t)J * T;
-  for (int b = q0; b < 36; b += 8 * np) {
+  for (int b = sidx * 8 + wave; b < 36; b += 8 * np) {
     int ib = 0;
     while ((ib + 1) * (ib + 2) / 2 <= b) ++ib;
-    flat_syrk_block(Aii, Lij, ld, ib, b - ib * (ib + 1) / 2);
+    const int jb = b - ib * (ib + 1) / 2;
+    if (wave_wait(ca + 1 + region_slab(ib), ready, info, spins) || wave_wait(ca + 1 + region_slab(jb), ready, info, spins))
+      return;
+    flat_syrk_block(Aii, ld, slot1, ib, jb);
   }
+  GPF_PHASE(2);
 }
 
 // SYRK workgroup of launch J (deferred diagonal update, see step_decode): A_{J+1,J+1} -=
@@ -789,16 +832,20 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
   double* yp = yb + (size_t)p * Npad;
   if constexpr (SPLIT == SPLIT_ALL) {
     static_assert(ED, "the all-tile split runs with the early diagonal factor (host: early_diag)");
-    if (role == ROLE_PIECE) {
-      const int np = split_all_pieces(J, w, nt, S);
-      if (w < nL)
-        flat_piece<true>(J, w, p, nt, Npad, Lp, Up, yp, s2p, szp, info + p, N, x, ls + (size_t)p * d, d, np, sidx, S2,
-                         part, cnt, sflag, dflag, spins, lds);
-      else
-        flat_piece<false>(J, w, p, nt, Npad, Lp, Up, yp, s2p, szp, info + p, N, x, ls + (size_t)p * d, d, np, sidx, S2,
-                          part, cnt, sflag, dflag, spins, lds);
-      return;
+    // (every tile of the launch: the single-piece ones, ROLE_WHOLE, finish the same way)
+    const int np = split_all_pieces(J, w, nt, S);
+#define GPF_FLAT(lt, one)                                                                                          \
+  flat_piece<lt, one>(J, w, p, nt, Npad, Lp, Up, yp, s2p, szp, info + p, N, x, ls + (size_t)p * d, d, np, sidx, S2, \
+                      part, cnt, sflag, dflag, spins, lds)
+    if (w < nL) {
+      if (role == ROLE_PIECE) GPF_FLAT(true, false);
+      else GPF_FLAT(true, true);
+    } else {
+      if (role == ROLE_PIECE) GPF_FLAT(false, false);
+      else GPF_FLAT(false, true);
     }
+#undef GPF_FLAT
+    return;
   }
   const Quad<T> qd;
   const int g = qd.lane >> 4, cl = qd.lane & 15;

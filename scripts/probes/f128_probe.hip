@@ -50,7 +50,6 @@ __global__ __launch_bounds__(DNTH) void k_new(double* L, double* U, double* y, d
 
 // the panel alone: wave 0 runs the 8 diagonal-block panels on block data in LDS (the other waves
 // exit after the load); cyc[p] = s_memtime cycles of the 8 panels
-template <int VAR>
 __global__ __launch_bounds__(DNTH) void k_panels(double* L, double* U, unsigned long long* cyc) {
   __shared__ __attribute__((aligned(16))) double lds[DB_LDS];
   const int p = blockIdx.x;
@@ -65,20 +64,19 @@ __global__ __launch_bounds__(DNTH) void k_panels(double* L, double* U, unsigned 
   const unsigned long long t0 = memtime();
   bool bad = false;
 #pragma unroll 1
-  for (int k = 0; k < 8; ++k) bad = db_panel<true, VAR>(lds, k, L + (size_t)p * NB * NB, U + (size_t)p * NB * NB, NB) | bad;
+  for (int k = 0; k < 8; ++k) bad = db_panel<true>(lds, k, L + (size_t)p * NB * NB, U + (size_t)p * NB * NB, NB) | bad;
   const unsigned long long t1 = memtime();
   if (threadIdx.x == 0) cyc[p] = t1 - t0 + (bad ? 1 : 0);
 }
 
-template <int VAR>
 static void panel_case(double* dL, double* dU, unsigned long long* dcyc, int P) {
-  hipLaunchKernelGGL(k_panels<VAR>, dim3(P), dim3(DNTH), 0, 0, dL, dU, dcyc);
+  hipLaunchKernelGGL(k_panels, dim3(P), dim3(DNTH), 0, 0, dL, dU, dcyc);
   CK(hipDeviceSynchronize());
   std::vector<unsigned long long> c(P);
   CK(hipMemcpy(c.data(), dcyc, P * 8, hipMemcpyDeviceToHost));
   double m = 0;
   for (int i = 0; i < P; ++i) m += (double)c[i];
-  printf("panel variant %d: 8 panels on wave 0 alone, %.0f cycles (%.0f per column)\n", VAR, m / P, m / P / 128);
+  printf("panel: 8 panels on wave 0 alone, %.0f cycles (%.0f per column)\n", m / P, m / P / 128);
 }
 
 // dependent-chain latency of single FP64 VALU ops on one wave (cycles per op, s_memtime)
@@ -346,11 +344,7 @@ int main(int argc, char** argv) {
   lat_case<1>("v_rsq_f64 + v_add_f64");
   lat_case<2>("v_readlane_b32 x2 + v_mul_f64");
   lat_case<3>("v_mul_f64");
-  panel_case<0>(dL[1], dU[1], dcyc, 256);
-  panel_case<1>(dL[1], dU[1], dcyc, 256);
-  panel_case<2>(dL[1], dU[1], dcyc, 256);
-  panel_case<3>(dL[1], dU[1], dcyc, 256);
-  panel_case<4>(dL[1], dU[1], dcyc, 256);
+  panel_case(dL[1], dU[1], dcyc, 256);
   mfma_case<8>(1);
   mfma_case<8>(2);
   mfma_case<8>(4);

@@ -17,7 +17,7 @@ def main():
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "dev.s")
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-                        "-Wno-unused-value", "-Wno-unused-result", "--cuda-device-only", "-gline-tables-only", "-S", SRC,
+                        "-Wno-unused-value", "-Wno-unused-result", "-mllvm", "--amdgpu-mfma-vgpr-form", "--cuda-device-only", "-gline-tables-only", "-S", SRC,
                         "-o", out], check=True, capture_output=True)
         lines = open(out).read().splitlines()
     files, fn, hist = {}, None, []

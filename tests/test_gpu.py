@@ -938,8 +938,10 @@ def test_early_diagonal_factor_matches_fused(ctx, monkeypatch, N, d, P):
     """The early diagonal factor (k_step<SPLIT, 1>: block J factored by extra workgroups at the
     start of launch J and handed to the tiles through a flag) against the fused factor at the end
     of the previous launch's critical tile: the same arithmetic, so bitwise equal scores, mean
-    and sd, on the critical-split (N=1000), unsplit and all-tile-split (one particle) paths; and
-    the factor itself bitwise equal for the prediction path. The deferred diagonal update (one
+    and sd, on the critical-split (N=1000) and unsplit paths. The all-tile split (one particle:
+    the prediction path) always runs the early factor (its flat finish waits for the diagonal
+    block inside the launch), so there GPF_EARLY_DIAG=0 must change nothing: the factor itself
+    bitwise equal. The deferred diagonal update (one
     SYRK workgroup per particle and launch applies the earlier terms to the next diagonal block,
     the critical tile the last one; GPF_DEFER_SYRK=0 restores the per-tile look-ahead) runs the
     same MFMAs per element in the same order: bitwise equal to the look-ahead, with either
