@@ -83,7 +83,8 @@ constexpr int DB_LD = 17;                   // row stride of a 16x16 block in LD
 constexpr int DB_BLK = 16 * DB_LD;          // doubles per block
 constexpr int DB_NB = 36;                   // lower blocks (i >= j) of the 8 x 8 grid
 constexpr int DB_Y = DB_NB * DB_BLK;        // y -> z, 128 doubles
-constexpr int DB_LDS = DB_Y + T;            // doubles of LDS the factor uses (77.5 KiB)
+constexpr int DB_UNIT = DB_Y + T;           // 31 doubles: 15 zeros, 1, 15 zeros (the X lanes' identity rows)
+constexpr int DB_LDS = DB_UNIT + 32;        // doubles of LDS the factor uses (78 KiB)
 
 __host__ __device__ constexpr int db_bid(int i, int j) { return i * (i + 1) / 2 + j; }
 // element (r, c) of a block: row-major, stride 17: the 16 rows x 2 depths of an MFMA operand read
@@ -182,6 +183,75 @@ __host__ __device__ constexpr int db_q_wave(int k, int i) {
   return i == k + 1 ? 4 : (i - k - 2 == 0 ? 1 : i - k - 2 == 1 ? 2 : i - k - 2 == 2 ? 3 : i - k - 2 == 3 ? 5 : i - k - 2 == 4 ? 6 : 7);
 }
 
+// m of lanes 0..15 copied to lanes 16..31, 32..47, 48..63 (v_permlane32_swap: lanes 32..63 take
+// lanes 0..31; v_permlane16_swap: rows 1 and 3 take rows 0 and 2), per 32-bit half.
+__device__ __forceinline__ unsigned row0_to_rows_u32(unsigned v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(a[0], a[0], false, false);
+  return b[0];
+}
+__device__ __forceinline__ double row0_to_rows(double m) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, m);
+  const unsigned lo = row0_to_rows_u32((unsigned)u), hi = row0_to_rows_u32((unsigned)(u >> 32));
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+// x -= L(S, q) * m with L(S, q) = lane S of the lane's row of mc (v_fmac_f64 with row_newbcast:S;
+// fma(-m, L, x) and fma(-L, m, x) are the same rounding)
+// (volatile: the column's DPP operations stay in order, and the first one carries the 2 wait states
+// a DPP read of a VGPR just written by a VALU operation needs — the compiler's hazard recognizer
+// does not look into inline asm)
+template <int S, bool FIRST>
+__device__ __forceinline__ void db_fmac_bcast(double& x, double mc, double m) {
+  if (FIRST)
+    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(x) : "v"(mc), "v"(m), "i"(S));
+  else
+    asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(x) : "v"(mc), "v"(m), "i"(S));
+}
+// the entries s = q + D .. 15 of column q (q runtime-constant after unrolling: a switch on s)
+template <int D>
+__device__ __forceinline__ void db_fmac_bcast_from(int q, double (&x)[16], double mc, double m) {
+#pragma unroll
+  for (int s = 0; s < 16; ++s)
+    if (s == q + D) {
+      switch (s) {
+        case 2: db_fmac_bcast<2, true>(x[s], mc, m); break;
+        case 3: db_fmac_bcast<3, true>(x[s], mc, m); break;
+        case 4: db_fmac_bcast<4, true>(x[s], mc, m); break;
+        case 5: db_fmac_bcast<5, true>(x[s], mc, m); break;
+        case 6: db_fmac_bcast<6, true>(x[s], mc, m); break;
+        case 7: db_fmac_bcast<7, true>(x[s], mc, m); break;
+        case 8: db_fmac_bcast<8, true>(x[s], mc, m); break;
+        case 9: db_fmac_bcast<9, true>(x[s], mc, m); break;
+        case 10: db_fmac_bcast<10, true>(x[s], mc, m); break;
+        case 11: db_fmac_bcast<11, true>(x[s], mc, m); break;
+        case 12: db_fmac_bcast<12, true>(x[s], mc, m); break;
+        case 13: db_fmac_bcast<13, true>(x[s], mc, m); break;
+        case 14: db_fmac_bcast<14, true>(x[s], mc, m); break;
+        default: db_fmac_bcast<15, true>(x[s], mc, m); break;
+      }
+    } else if (s > q + D) {
+      switch (s) {
+        case 0: db_fmac_bcast<0, false>(x[s], mc, m); break;
+        case 1: db_fmac_bcast<1, false>(x[s], mc, m); break;
+        case 2: db_fmac_bcast<2, false>(x[s], mc, m); break;
+        case 3: db_fmac_bcast<3, false>(x[s], mc, m); break;
+        case 4: db_fmac_bcast<4, false>(x[s], mc, m); break;
+        case 5: db_fmac_bcast<5, false>(x[s], mc, m); break;
+        case 6: db_fmac_bcast<6, false>(x[s], mc, m); break;
+        case 7: db_fmac_bcast<7, false>(x[s], mc, m); break;
+        case 8: db_fmac_bcast<8, false>(x[s], mc, m); break;
+        case 9: db_fmac_bcast<9, false>(x[s], mc, m); break;
+        case 10: db_fmac_bcast<10, false>(x[s], mc, m); break;
+        case 11: db_fmac_bcast<11, false>(x[s], mc, m); break;
+        case 12: db_fmac_bcast<12, false>(x[s], mc, m); break;
+        case 13: db_fmac_bcast<13, false>(x[s], mc, m); break;
+        case 14: db_fmac_bcast<14, false>(x[s], mc, m); break;
+        default: db_fmac_bcast<15, false>(x[s], mc, m); break;
+      }
+    }
+}
+
 // ---- the panel: wave 0 ----
 // The 16 x 16 diagonal block A_kk, as an [A | I | y] elimination on one wave: lane r < 16 holds row r
 // of A (columns <= r), lane 16 + c column c of X_kk = L_kk^-1 (the identity to start), lane 32 the
@@ -196,37 +266,105 @@ __device__ __forceinline__ bool db_panel(double* lds, int k, double* __restrict_
   const bool arow = r < 16, xcol = r >= 16 && r < 32, ylane = r == 32;
   int ro = r;
   asm volatile("" : "+v"(ro));  // (an opaque lane index: the initial values are not kept live across panels)
+  // Every lane loads its 16 entries from a row of its own — A rows from the block (the entries
+  // right of the diagonal are A's symmetric values: finite, updated, never stored or read), the X
+  // lanes from the unit vector (lane 16 + c: e_c), the y lane from y, the others anything — with
+  // no per-entry select: the role selects cost ~100 VALU instructions per panel (r5 probe).
+  const int row_off = arow ? db_bid(k, k) * DB_BLK + ro * DB_LD
+                           : (xcol ? DB_UNIT + 15 - (ro - 16) : (ylane ? DB_Y + 16 * k : DB_UNIT));
+  const double* src = lds + row_off;
   double x[16];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) {  // (every lane loads, then selects: no divergent loads)
-    double va = blk[db_off(ro & 15, c)], vy = lds[DB_Y + 16 * k + c];
-    asm volatile("" : "+v"(va), "+v"(vy));  // (keeps the loads from being sunk into per-role branches)
-    x[c] = arow ? (c <= ro ? va : 0.0) : (xcol ? (c == ro - 16 ? 1.0 : 0.0) : (ylane ? vy : 0.0));
-  }
+  for (int c = 0; c < 16; ++c) x[c] = src[c];
   bool bad = false;
   // Column q: pivot from lane q, 1/sqrt by v_rsq + Newton, scale, then the rank-1 update of every
   // later entry s of the lane's row with L(s, q) by v_readlane, in column order (each entry takes
   // its updates q = 0, 1, .. in sequence, as a right-looking potrf does: an exactly singular
   // block then ends with the same pivot rounding as LAPACK's column order, tests/test_gpu.py::
-  // test_not_positive_definite_raises_like_numpy). Measured variants (probe
-  // scripts/probes/f128_probe.hip, profiles/r5/f128_panel_variants.txt), cycles per column on one
-  // wave: this one 426; one column deferred through an LDS broadcast buffer 439-441 (and it
-  // reordered the updates); the pivot chain on uniform values, one step ahead 456-460; that with
-  // one Newton step 439-443; uniform chain + LDS buffer 436-440. The column is VALU issue and
-  // latency bound (~40 dependent f64 ops), not bound by the readlanes.
+  // test_not_positive_definite_raises_like_numpy).
+#ifndef GPF_PANEL_DPP
+#define GPF_PANEL_DPP 1  // (probe A/B only; removed once measured)
+#endif
+#if GPF_PANEL_DPP
+  // (r5) The updates s >= q+2 take L(s, q) through DPP instead of v_readlane: m of lanes 0..15 is
+  // copied to the other three rows of 16 lanes (two permlane swaps per 32-bit half), and each
+  // entry is then one v_fmac_f64 whose first operand is row_newbcast:s of that copy — lane s of
+  // the lane's own row, i.e. L(s, q) in every row — in place of two v_readlane, the SGPR hazard
+  // wait and a v_fma. The column was VALU-issue bound (~60 instructions, 426 cycles). The entry
+  // q+1 (the next pivot's) keeps the v_readlane: it is on the pivot chain. Bitwise the same
+  // products and sums.
+  double inv;
+  {
+    const double p0 = readlane_f64(x[0], 0);
+    bad = !(p0 > 0.0);
+    inv = rsqrt_nr(p0);
+  }
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
-    const double p = readlane_f64(x[q], q);
-    bad = bad | !(p > 0.0);
-    const double inv = rsqrt_nr(p);
     const double m = (arow && r < q) ? 0.0 : x[q] * inv;
     x[q] = m;
-#pragma unroll
-    for (int s = q + 1; s < 16; ++s) {
-      x[s] = fma(-m, readlane_f64(m, s), x[s]);
-      if (((s - q) & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+    if (q == 15) break;
+    x[q + 1] = fma(-m, readlane_f64(m, q + 1), x[q + 1]);
+    const double pn = readlane_f64(x[q + 1], q + 1);
+    bad = bad | !(pn > 0.0);
+    inv = rsqrt_nr(pn);
+    if (q + 2 < 16) {
+      db_fmac_bcast_from<2>(q, x, row0_to_rows(m), m);
     }
   }
+#else
+  // Software-pipelined (r5): the entry s = q+1 is updated first, the next pivot read from it, and
+  // the 7 dependent steps of its 1/sqrt (v_rsq, two Newton steps) are interleaved one by one with
+  // the remaining updates of column q, each group fenced by a scheduling barrier (a wave issues in
+  // order: with the chain after the updates, as the compiler placed it, a column cost the issue of
+  // all its ~50 VALU instructions plus the chain's latency, 426 cycles; profiles/r5/
+  // f128_panel_variants.txt). Same operations in the same order per value: bitwise unchanged.
+  // (Rejected, same probe: one column deferred through an LDS broadcast buffer 439-441 cycles per
+  // column, and it reordered the updates; the pivot chain on uniform values one step ahead 456-460;
+  // that with one Newton step 439-443; uniform chain + LDS buffer 436-440.)
+  double inv;
+  {
+    const double p0 = readlane_f64(x[0], 0);
+    bad = !(p0 > 0.0);
+    inv = rsqrt_nr(p0);
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const double m = (arow && r < q) ? 0.0 : x[q] * inv;
+    x[q] = m;
+    if (q == 15) break;
+    x[q + 1] = fma(-m, readlane_f64(m, q + 1), x[q + 1]);
+    const double pn = readlane_f64(x[q + 1], q + 1);
+    bad = bad | !(pn > 0.0);
+    int s = q + 2;
+    auto upd = [&](int n) {  // the next n entries of column q's update (compile-time s)
+#pragma unroll
+      for (int i = 0; i < n; ++i)
+        if (s < 16) {
+          x[s] = fma(-m, readlane_f64(m, s), x[s]);
+          ++s;
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    __builtin_amdgcn_sched_barrier(0);
+    double y = __builtin_amdgcn_rsq(pn);  // (rsqrt_nr's operations, in its order)
+    const double h = 0.5 * pn;
+    upd(1);
+    double hy = h * y;
+    upd(1);
+    double t = fma(-hy, y, 0.5);
+    upd(1);
+    y = fma(y, t, y);
+    upd(1);
+    hy = h * y;
+    upd(1);
+    t = fma(-hy, y, 0.5);
+    upd(1);
+    y = fma(y, t, y);
+    upd(16);
+    inv = y;
+  }
+#endif
   // (the diagonal row's own entries right of its pivot took updates with m = L(q, q): not stored)
   if (arow) {
     double* gl = Lt + (size_t)(16 * k + r) * ld + 16 * k;
@@ -260,6 +398,8 @@ __device__ __forceinline__ void db_q_item(double* lds, int k, int i, double* __r
   double xa[4], ab[4];
   db_opa(B(k, k), xa);
   db_opa(Aik, ab);
+  d4 cnext = {0.0, 0.0, 0.0, 0.0};
+  if (i == k + 1) cnext = db_ld(B(i, i));  // (read with the operands: off the chain below)
   d4 lt = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int s = 0; s < 4; ++s) lt = mfma(xa[s], ab[s], lt);
@@ -271,8 +411,12 @@ __device__ __forceinline__ void db_q_item(double* lds, int k, int i, double* __r
   db_st_t(Aik, lt);  // L(i,k) for the trailing updates and the inverse
   if (g == 0) lds[DB_Y + 16 * i + c] = lds[DB_Y + 16 * i + c] - yp;
   if (i == k + 1) {
-    double* C = B(i, i);
-    db_st(C, db_mul_ax<true>(db_ld(C), Aik, lt));
+    // (the A operand of k-step s, L(r, 4 s + g) at lane (g, r), is lt[s] itself — the same lane
+    // mapping as the B operand: no LDS round trip through the rows just stored, on the chain)
+    d4 acc = cnext;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = mfma_neg_a(lt[s], lt[s], acc);
+    db_st(B(i, i), acc);
   }
   double* gl = Lt + (size_t)(16 * i + c) * ld + 16 * k + g;
 #pragma unroll
@@ -372,31 +516,24 @@ __device__ __forceinline__ void db_publish(double* __restrict__ yseg, const doub
   }
 }
 
-template <bool WT, int k>
-__device__ __forceinline__ void db_step_panel(double* lds, bool& bad, double* __restrict__ Lt, double* __restrict__ Ut,
-                                              size_t ld) {
-  bad = db_panel<WT>(lds, k, Lt, Ut, ld) | bad;
-  DB_STAMP(0, 2 * k);
-  lsync();
-  if constexpr (k < 7) {
-    db_q<WT, k, 0>(lds, Lt, ld);
-    DB_STAMP(0, 2 * k + 1);
-    lsync();
-  }
-}
-
+// Wave 0's path: the 8 panels as a runtime loop over one copy of the panel code (no Q items are
+// wave 0's: db_q_wave). Unrolled per k (r5 first version) the path was ~8 x 8 KiB of straight-line
+// code, every panel fetched cold: in situ a panel cost ~60% more than the same code looping alone
+// (profiles/r5/f128_*.txt).
 template <bool WT>
 __device__ __forceinline__ void db_path_panel(double* lds, double* __restrict__ Lt, double* __restrict__ Ut, size_t ld,
                                               double* __restrict__ yseg, int* __restrict__ info, int* pub, int pub_val) {
   bool bad = false;
-  db_step_panel<WT, 0>(lds, bad, Lt, Ut, ld);
-  db_step_panel<WT, 1>(lds, bad, Lt, Ut, ld);
-  db_step_panel<WT, 2>(lds, bad, Lt, Ut, ld);
-  db_step_panel<WT, 3>(lds, bad, Lt, Ut, ld);
-  db_step_panel<WT, 4>(lds, bad, Lt, Ut, ld);
-  db_step_panel<WT, 5>(lds, bad, Lt, Ut, ld);
-  db_step_panel<WT, 6>(lds, bad, Lt, Ut, ld);
-  db_step_panel<WT, 7>(lds, bad, Lt, Ut, ld);
+#pragma unroll 1
+  for (int k = 0; k < 8; ++k) {
+    bad = db_panel<WT>(lds, k, Lt, Ut, ld) | bad;
+    DB_STAMP(0, 2 * k);
+    lsync();
+    if (k < 7) {
+      DB_STAMP(0, 2 * k + 1);
+      lsync();
+    }
+  }
   db_publish<WT>(yseg, lds, pub, pub_val);
   DB_STAMP(0, 16);
   if (bad && threadIdx.x == 0 && *info == 0) *info = 1;  // (the pivots are wave-uniform)
@@ -491,6 +628,7 @@ __device__ __forceinline__ void factor128(double* __restrict__ Lt, double* __res
       s[1] = v.y;
     }
     if (tid < T) lds[DB_Y + tid] = yseg[tid];
+    if (tid < 32) lds[DB_UNIT + tid] = tid == 15 ? 1.0 : 0.0;
   }
   // zeros above the diagonal blocks of L and U (wave 4: idle otherwise; nothing reads them here)
   if (wave == 4) {

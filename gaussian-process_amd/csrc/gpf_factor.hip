@@ -203,9 +203,10 @@ __host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt,
 // LDS of a k_step workgroup (doubles): the GEMM stages (DL_STAGE), the diagonal factor
 // (DB_LDS), the staged U_JJ of the triangular finishes (TRI_LDS) with z_J behind
 // it, or the coordinates of a covariance tile. ~77 KiB: two workgroups per CU.
-constexpr int STEP_ZJ = TRI_LDS;  // z_J (128 doubles) beside the staged U_JJ
+constexpr int STEP_ZJ = TRI_LDS;      // z_J (128 doubles) beside the staged U_JJ
+constexpr int STEP_XS = STEP_ZJ + T;  // flat finish: the U-tile column sums one wave hands the other (64)
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
-constexpr int STEP_LDS = cmax(cmax(DL_STAGE, DB_LDS), cmax(STEP_ZJ + T, 2 * DMAX * T + 2 * T));
+constexpr int STEP_LDS = cmax(cmax(DL_STAGE, DB_LDS), cmax(STEP_XS + 64, 2 * DMAX * T + 2 * T));
 static_assert(STEP_LDS * 8 <= 80 * 1024, "two k_step workgroups per CU (160 KiB of LDS)");
 constexpr int STEP_NTH = Geo<T>::NTH;     // 512 threads: 8 waves, 128x16 per wave
 static_assert(STEP_NTH == DNTH, "the fused diagonal runs on the step workgroup");
@@ -592,7 +593,8 @@ __device__ __forceinline__ void flat_load_operand(double (&a)[32], const double*
 
 // Phase C: block (ib, jb) (ib >= jb) of A_II -= L_IJ L_IJ^T: 32 MFMAs, k = 4 t + (lane >> 4)
 // ascending, seeded with A_II (syrk_rows' operands and order per element).
-__device__ __forceinline__ void flat_syrk_block(double* Aii, size_t ld, const double* slot1, int ib, int jb) {
+__device__ __forceinline__ void flat_syrk_block(double* Aii, size_t ld, const double* slot1, int ib, int jb, double* yi,
+                                                const double* zj) {
   const int lane = threadIdx.x & 63, g = lane >> 4, cl = lane & 15;
   double* cp = launder(Aii + (size_t)(16 * ib + g) * ld + 16 * jb + cl);
   d4 acc;
@@ -603,6 +605,13 @@ __device__ __forceinline__ void flat_syrk_block(double* Aii, size_t ld, const do
   if (ib == jb) {
 #pragma unroll
     for (int t = 0; t < 32; ++t) acc = mfma_neg_a(a[t], a[t], acc);
+    // y_I rows 16 ib + c: L(16 ib + c, k) z_k over k = 4 t + g ascending per lane, then the lane groups
+    const double* zg = launder(zj + g);
+    double yr = 0.0;
+#pragma unroll
+    for (int t = 0; t < 32; ++t) yr = fma(a[t], zg[4 * t], yr);
+    yr = sum_lane_groups(yr);
+    if (g == 0) yi[16 * ib + cl] = yi[16 * ib + cl] - yr;
   } else {
     double b[32];
     flat_load_operand(b, slot1, region_slab(jb));
@@ -660,27 +669,34 @@ __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad
     }
   }
   GPF_PHASE(0);
-  // T (the region's sum is loaded before the wait for the diagonal block: its latency hides there)
+  // T (the region's sum is loaded before the wait for the diagonal block: its latency hides
+  // there). With np >= 4 two waves share a region (WPR = 2, on different SIMDs): the triangular
+  // multiply's output row blocks {0,1, 6,7} (P = 0, 3) and {2,3, 4,5} (P = 1, 2), 72 of its 144
+  // MFMAs each.
+  const int WPR = (!ONE && np >= 4) ? 2 : 1;
+  const int half = WPR == 2 ? (wave & 1) : -1;  // -1: every P
   double* slot1 = pt + (size_t)T * T;
   if (sidx < 8) {
     double* zj = lds + STEP_ZJ;
-    const int r = sidx + np * wave;  // the region this wave finishes
+    const int r = sidx + np * (WPR == 2 ? (wave >> 1) : wave);  // the region this wave finishes
     bool late = false;
     if (!ONE && r < 8) {
       late = wave_wait(ca + 1 + r, 16u, info, spins);
       if (!late) flat_load_region(acc, pt, r);
     }
     if (wait_diag(dflag + p, J, info, spins, sflag)) return;  // U_JJ, z_J
-    if (tid < T) zj[tid] = yp[J * T + tid];
+    if (!LT && tid < T) zj[tid] = yp[J * T + tid];
     tri_to_lds(Up + (size_t)J * T * ld + (size_t)J * T, ld, lds);  // (its barrier also publishes z_J)
-    if (r < 8 && !late) {
-      const int cb = 16 * region_slab(r);
-      if (LT) {
-        // L_IJ^T = U_JJ D for the slab's 16 columns of D (rows cb.. of L_IJ); y_I -= L_IJ z_J
+    auto mine = [&](int P) { return half < 0 || (half == 0) == (P == 0 || P == 3); };
+    const int cb = 16 * region_slab(r < 8 ? r : 0);
+    if (LT) {
+      if (r < 8 && !late) {
+        // L_IJ^T = U_JJ D for the slab's 16 columns of D (rows cb.. of L_IJ); the rows also to slot 1
+        // in the operand layout (y_I -= L_IJ z_J follows in phase C, from those operands)
         double* lrow = launder(Lp + (size_t)(I * T + cb + cl) * ld + (size_t)J * T + g);
-        double yr = 0.0;
 #pragma unroll
         for (int P = 0; P < 4; ++P) {
+          if (!mine(P)) continue;
           d4 o[2];
           switch (P) {
             case 0: trmm_acc<0, false>(o, acc, lds); break;
@@ -692,21 +708,20 @@ __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad
 #pragma unroll
           for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              lrow[16 * (2 * P + j) + 4 * e] = o[j][e];
-              yr = fma(o[j][e], zj[16 * (2 * P + j) + 4 * e + g], yr);
-            }
+            for (int e = 0; e < 4; ++e) lrow[16 * (2 * P + j) + 4 * e] = o[j][e];
         }
-        yr = sum_lane_groups(yr);
-        if (g == 0) yp[I * T + cb + cl] = yp[I * T + cb + cl] - yr;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the region's operands drained
         if (qd.lane == 0) __hip_atomic_fetch_add(ca + 1 + r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        // U_JK = -U_JJ W; the column partials of colsum(U^2) and U^T z (per half, then summed)
+      }
+    } else {
+      // U_JK = -U_JJ W; the column partials of colsum(U^2) and U^T z: each wave's rows in P order,
+      // the 4 lane groups, then (WPR = 2) the two waves' sums, half 0's first
+      double a2 = 0.0, az = 0.0;
+      if (r < 8 && !late) {
         double* ucol = launder(Up + (size_t)(J * T + g) * ld + (size_t)K * T + cb + cl);
-        double a2[2] = {0.0, 0.0}, az[2] = {0.0, 0.0};
 #pragma unroll
         for (int P = 0; P < 4; ++P) {
+          if (!mine(P)) continue;
           d4 o[2];
           switch (P) {
             case 0: trmm_acc<0, true>(o, acc, lds); break;
@@ -714,7 +729,6 @@ __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad
             case 2: trmm_acc<2, true>(o, acc, lds); break;
             default: trmm_acc<3, true>(o, acc, lds); break;
           }
-          const int h = P >> 1;
 #pragma unroll
           for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -722,28 +736,37 @@ __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad
               const int row = 16 * (2 * P + j) + 4 * e;  // + g
               const double v = o[j][e];
               ucol[(size_t)row * ld] = v;
-              a2[h] = fma(v, v, a2[h]);
-              az[h] = fma(v, zj[row + g], az[h]);
+              a2 = fma(v, v, a2);
+              az = fma(v, zj[row + g], az);
             }
         }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          a2[h] = sum_lane_groups(a2[h]);
-          az[h] = sum_lane_groups(az[h]);
+        a2 = sum_lane_groups(a2);
+        az = sum_lane_groups(az);
+      }
+      double* xs = lds + STEP_XS + 32 * (wave >> 1);  // (WPR = 2) half 1's sums for half 0
+      if (WPR == 2) {
+        if (half == 1 && g == 0) {
+          xs[2 * cl] = a2;
+          xs[2 * cl + 1] = az;
         }
-        if (g == 0) {
-          const size_t poff = ((size_t)p * nt + J) * Npad + (size_t)K * T + cb + cl;
-          s2p[poff] = a2[0] + a2[1];
-          szp[poff] = az[0] + az[1];
+        __syncthreads();  // (every wave of the piece: none has left since the diagonal wait)
+      }
+      if (r < 8 && !late && half <= 0 && g == 0) {
+        if (WPR == 2) {
+          a2 = a2 + xs[2 * cl];
+          az = az + xs[2 * cl + 1];
         }
+        const size_t poff = ((size_t)p * nt + J) * Npad + (size_t)K * T + cb + cl;
+        s2p[poff] = a2;
+        szp[poff] = az;
       }
     }
   }
   GPF_PHASE(1);
   if (!LT) return;
-  // C
-  // (block b = ib (ib + 1) / 2 + jb waits for the regions of slabs ib and jb only)
-  const unsigned ready = ONE ? 1u : 17u;
+  // C (block b = ib (ib + 1) / 2 + jb waits for the regions of slabs ib and jb only; the diagonal
+  // blocks also apply y_I -= L_IJ z_J for their slab's rows, from the same operands)
+  const unsigned ready = (ONE ? 0u : 16u) + (unsigned)WPR;
   double* Aii = Lp + (size_t)I * T * ld + (size_t)I * T;
   for (int b = sidx * 8 + wave; b < 36; b += 8 * np) {
     int ib = 0;
@@ -751,7 +774,7 @@ __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad
     const int jb = b - ib * (ib + 1) / 2;
     if (wave_wait(ca + 1 + region_slab(ib), ready, info, spins) || wave_wait(ca + 1 + region_slab(jb), ready, info, spins))
       return;
-    flat_syrk_block(Aii, ld, slot1, ib, jb);
+    flat_syrk_block(Aii, ld, slot1, ib, jb, ib == jb ? yp + (size_t)I * T : nullptr, yp + (size_t)J * T);
   }
   GPF_PHASE(2);
 }

@@ -59,6 +59,7 @@ __global__ __launch_bounds__(DNTH) void k_panels(double* L, double* U, unsigned 
     if (c <= r) lds[db_bid(r / 16, c / 16) * DB_BLK + db_off(r % 16, c % 16)] = A[i];
   }
   for (int i = threadIdx.x; i < NB; i += DNTH) lds[DB_Y + i] = 1.0;
+  if (threadIdx.x < 32) lds[DB_UNIT + threadIdx.x] = threadIdx.x == 15 ? 1.0 : 0.0;
   __syncthreads();
   if (threadIdx.x >= 64) return;
   const unsigned long long t0 = memtime();
@@ -67,6 +68,78 @@ __global__ __launch_bounds__(DNTH) void k_panels(double* L, double* U, unsigned 
   for (int k = 0; k < 8; ++k) bad = db_panel<true>(lds, k, L + (size_t)p * NB * NB, U + (size_t)p * NB * NB, NB) | bad;
   const unsigned long long t1 = memtime();
   if (threadIdx.x == 0) cyc[p] = t1 - t0 + (bad ? 1 : 0);
+}
+
+// wave 0 runs the 8 panels (as k_panels) while waves 1..7 run MODE: 0 nothing, 1 an FP64 MFMA
+// chain loop (registers only), 2 FP64 v_fma loop, 3 LDS read loop; wave 0's cycles are reported
+template <int MODE>
+__global__ __launch_bounds__(DNTH) void k_contend(double* L, double* U, unsigned long long* cyc, double* sink) {
+  __shared__ __attribute__((aligned(16))) double lds[DB_LDS];
+  __shared__ int done;
+  const int p = blockIdx.x;
+  const double* A = L + (size_t)p * NB * NB;
+  for (int i = threadIdx.x; i < NB * NB; i += DNTH) {
+    const int r = i / NB, c = i % NB;
+    if (c <= r) lds[db_bid(r / 16, c / 16) * DB_BLK + db_off(r % 16, c % 16)] = A[i];
+  }
+  for (int i = threadIdx.x; i < NB; i += DNTH) lds[DB_Y + i] = 1.0;
+  if (threadIdx.x < 32) lds[DB_UNIT + threadIdx.x] = threadIdx.x == 15 ? 1.0 : 0.0;
+  if (threadIdx.x == 0) done = 0;
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (wave == 0) {
+    const unsigned long long t0 = memtime();
+    bool bad = false;
+#pragma unroll 1
+    for (int k = 0; k < 8; ++k) bad = db_panel<true>(lds, k, L + (size_t)p * NB * NB, U + (size_t)p * NB * NB, NB) | bad;
+    const unsigned long long t1 = memtime();
+    if (threadIdx.x == 0) {
+      cyc[p] = t1 - t0 + (bad ? 1 : 0);
+      __hip_atomic_store(&done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return;
+  }
+  if (MODE == 0) return;
+  if (MODE == 4 && wave == 4) return;  // MFMA on the other SIMDs only
+  if (MODE == 5 && wave != 4) return;  // MFMA on wave 0's SIMD only
+  double a = threadIdx.x * 1e-3, b = 0.999;
+  d4 acc[4] = {};
+  double v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) v[u] = a + u;
+  const double* lp = lds + (threadIdx.x & 63) * 2;
+  double ls = 0.0;
+  for (int it = 0; it < 100000; ++it) {
+    if (__hip_atomic_load(&done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+#pragma unroll
+    for (int rep = 0; rep < 8; ++rep) {
+      if (MODE == 1 || MODE >= 4)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[c], 0, 0, 0);
+      if (MODE == 2)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = fma(v[u], b, 0.25);
+      if (MODE == 3)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) ls += lp[(u * 128 + rep * 16) & 4095];
+    }
+  }
+  double t = ls;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) t += acc[c][0] + acc[c][1];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) t += v[u];
+  sink[threadIdx.x + blockIdx.x * DNTH] = t;
+}
+template <int MODE>
+static void contend_case(double* dL, double* dU, unsigned long long* dcyc, double* sink, int P, const char* name) {
+  hipLaunchKernelGGL(k_contend<MODE>, dim3(P), dim3(DNTH), 0, 0, dL, dU, dcyc, sink);
+  CK(hipDeviceSynchronize());
+  std::vector<unsigned long long> c(P);
+  CK(hipMemcpy(c.data(), dcyc, P * 8, hipMemcpyDeviceToHost));
+  double m = 0;
+  for (int i = 0; i < P; ++i) m += (double)c[i];
+  printf("panel with waves 1..7 running %-22s %.0f cycles (%.0f per column)\n", name, m / P, m / P / 128);
 }
 
 static void panel_case(double* dL, double* dU, unsigned long long* dcyc, int P) {
@@ -93,6 +166,24 @@ __global__ __launch_bounds__(64) void k_lat(double a, double b, int n, double* o
       if (OP == 2) x = readlane_f64(x, 5) * b;
       if (OP == 3) x = x * b;
     }
+    if (OP >= 4) {  // throughput: 8 independent chains
+      double y[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) y[u] = x + u;
+#pragma unroll
+      for (int rep = 0; rep < 4; ++rep)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (OP == 4) y[u] = fma(y[u], b, 0.25);
+          if (OP == 5) db_fmac_bcast<5, false>(y[u], x, b);
+          if (OP == 6) y[u] = y[u] * readlane_f64(x + u, 5);
+          if (OP == 7) y[u] = __builtin_amdgcn_rsq(y[u]);
+        }
+      double t = 0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t += y[u];
+      x = t * 1e-3;
+    }
   }
   const unsigned long long t1 = memtime();
   if (threadIdx.x == 0) {
@@ -100,6 +191,65 @@ __global__ __launch_bounds__(64) void k_lat(double a, double b, int n, double* o
     cyc[0] = t1 - t0;
   }
 }
+// the panel's column loop alone on register data (no LDS, no stores), 8 panels' worth of columns;
+// MODE 0: as db_panel; 1: no updates s >= q+2; 2: no 1/sqrt chain (inv fixed); 3: 1 + 2
+template <int MODE>
+__global__ __launch_bounds__(64) void k_col(const double* in, double* out, unsigned long long* cyc) {
+  const int r = threadIdx.x;
+  const bool arow = r < 16;
+  double x[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) x[c] = in[r * 16 + c];
+  bool bad = false;
+  const unsigned long long t0 = memtime();
+#pragma unroll 1
+  for (int k = 0; k < 8; ++k) {
+    double inv = MODE >= 2 ? 0.5 : rsqrt_nr(readlane_f64(x[0], 0));
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const double m = (arow && r < q) ? 0.0 : x[q] * inv;
+      x[q] = m;
+      if (q == 15) break;
+      x[q + 1] = fma(-m, readlane_f64(m, q + 1), x[q + 1]);
+      const double pn = readlane_f64(x[q + 1], q + 1);
+      bad = bad | !(pn > 0.0);
+      if (MODE < 2) inv = rsqrt_nr(pn);
+      if ((MODE & 1) == 0 && q + 2 < 16) db_fmac_bcast_from<2>(q, x, row0_to_rows(m), m);
+    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c) x[c] = x[c] * 1.0001 + 1.0;  // (keeps the values positive definite-ish)
+  }
+  const unsigned long long t1 = memtime();
+  double t = bad ? 1.0 : 0.0;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) t += x[c];
+  out[r] = t;
+  if (r == 0) cyc[0] = t1 - t0;
+}
+template <int MODE>
+static void col_case(const char* name) {
+  double *in, *out;
+  unsigned long long* cyc;
+  CK(hipMalloc(&in, 64 * 16 * 8));
+  CK(hipMalloc(&out, 64 * 8));
+  CK(hipMalloc(&cyc, 8));
+  std::vector<double> h(64 * 16);
+  for (int i = 0; i < 64 * 16; ++i) h[i] = (i % 17 == 0) ? 4.0 : 0.01 * ((i * 7) % 13);
+  CK(hipMemcpy(in, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+  unsigned long long best = ~0ull;
+  for (int rep = 0; rep < 3; ++rep) {
+    hipLaunchKernelGGL(k_col<MODE>, dim3(1), dim3(64), 0, 0, in, out, cyc);
+    CK(hipDeviceSynchronize());
+    unsigned long long c;
+    CK(hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost));
+    best = c < best ? c : best;
+  }
+  printf("column loop %-30s %.0f cycles per column\n", name, (double)best / 128.0);
+  hipFree(in);
+  hipFree(out);
+  hipFree(cyc);
+}
+
 template <int OP>
 static void lat_case(const char* name) {
   double* out;
@@ -111,7 +261,10 @@ static void lat_case(const char* name) {
   CK(hipDeviceSynchronize());
   unsigned long long c;
   CK(hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost));
-  printf("latency %-34s %.1f cycles per dependent op\n", name, (double)c / (8.0 * n));
+  if (OP >= 4)
+    printf("throughput %-31s %.1f cycles per op (8 independent chains)\n", name, (double)c / (32.0 * n));
+  else
+    printf("latency %-34s %.1f cycles per dependent op\n", name, (double)c / (8.0 * n));
   hipFree(out);
   hipFree(cyc);
 }
@@ -331,7 +484,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_db_stamps), sizeof(st)));
     const unsigned long long t0 = st[0][17];
     printf("stamps (cycles from the load barrier), wave 0: panel k end / Q_k end; wave 1, 2: step end / Q end\n");
-    for (int w : {0, 1, 2, 3, 5}) {
+    for (int w : {0, 1, 2, 3, 4, 5, 6, 7}) {
       printf("  w%d:", w);
       for (int i = 0; i < 17; ++i) printf(" %lld", (long long)(st[w][i] - t0));
       printf("\n");
@@ -344,7 +497,28 @@ int main(int argc, char** argv) {
   lat_case<1>("v_rsq_f64 + v_add_f64");
   lat_case<2>("v_readlane_b32 x2 + v_mul_f64");
   lat_case<3>("v_mul_f64");
+  lat_case<4>("v_fma_f64");
+  lat_case<5>("v_fmac_f64_dpp row_newbcast");
+  lat_case<6>("v_readlane_b32 x2 + v_mul_f64");
+  lat_case<7>("v_rsq_f64");
+  col_case<0>("as db_panel");
+  col_case<1>("without updates s >= q+2");
+  col_case<2>("without the 1/sqrt chain");
+  col_case<3>("neither");
   panel_case(dL[1], dU[1], dcyc, 256);
+  {
+    double* sink;
+    CK(hipMalloc(&sink, 256 * DNTH * 8));
+    for (int rep = 0; rep < 2; ++rep) {
+      contend_case<0>(dL[1], dU[1], dcyc, sink, 256, "nothing");
+      contend_case<1>(dL[1], dU[1], dcyc, sink, 256, "FP64 MFMA chains");
+      contend_case<2>(dL[1], dU[1], dcyc, sink, 256, "FP64 v_fma chains");
+      contend_case<3>(dL[1], dU[1], dcyc, sink, 256, "LDS reads");
+      contend_case<4>(dL[1], dU[1], dcyc, sink, 256, "MFMA, not wave 4");
+      contend_case<5>(dL[1], dU[1], dcyc, sink, 256, "MFMA, wave 4 only");
+    }
+    hipFree(sink);
+  }
   mfma_case<8>(1);
   mfma_case<8>(2);
   mfma_case<8>(4);
