@@ -278,21 +278,19 @@ __device__ __forceinline__ bool db_panel(double* lds, int k, double* __restrict_
   for (int c = 0; c < 16; ++c) x[c] = src[c];
   bool bad = false;
   // Column q: pivot from lane q, 1/sqrt by v_rsq + Newton, scale, then the rank-1 update of every
-  // later entry s of the lane's row with L(s, q) by v_readlane, in column order (each entry takes
-  // its updates q = 0, 1, .. in sequence, as a right-looking potrf does: an exactly singular
-  // block then ends with the same pivot rounding as LAPACK's column order, tests/test_gpu.py::
-  // test_not_positive_definite_raises_like_numpy).
-#ifndef GPF_PANEL_DPP
-#define GPF_PANEL_DPP 1  // (probe A/B only; removed once measured)
-#endif
-#if GPF_PANEL_DPP
-  // (r5) The updates s >= q+2 take L(s, q) through DPP instead of v_readlane: m of lanes 0..15 is
-  // copied to the other three rows of 16 lanes (two permlane swaps per 32-bit half), and each
-  // entry is then one v_fmac_f64 whose first operand is row_newbcast:s of that copy — lane s of
-  // the lane's own row, i.e. L(s, q) in every row — in place of two v_readlane, the SGPR hazard
-  // wait and a v_fma. The column was VALU-issue bound (~60 instructions, 426 cycles). The entry
-  // q+1 (the next pivot's) keeps the v_readlane: it is on the pivot chain. Bitwise the same
-  // products and sums.
+  // later entry s of the lane's row with L(s, q), in column order (each entry takes its updates
+  // q = 0, 1, .. in sequence, as a right-looking potrf does: an exactly singular block then ends
+  // with the same pivot rounding as LAPACK's column order, tests/test_gpu.py::
+  // test_not_positive_definite_raises_like_numpy). The entry q+1 (the next pivot's, on the chain)
+  // takes L(q+1, q) by v_readlane; the entries s >= q+2 by DPP: m of lanes 0..15 is copied to the
+  // other three rows of 16 lanes (two permlane swaps per 32-bit half), and each entry is one
+  // v_fmac_f64 whose first operand is row_newbcast:s of that copy — lane s of the lane's own row,
+  // i.e. L(s, q) in every row — in place of two v_readlane, the SGPR hazard wait and a v_fma.
+  // Measured per column on wave 0 alone (probe, profiles/r5/f128_*.txt): 299 cycles with the
+  // selects gone and the loads batched; the register-only column loop is 187, its pivot chain alone
+  // 124. Rejected: the pivot chain's 1/sqrt interleaved with the updates by scheduling barriers
+  // (465 vs 426 at the time), one column deferred through an LDS broadcast buffer (439-441), the
+  // chain on uniform values one step ahead (456-460; with one Newton step 439-443).
   double inv;
   {
     const double p0 = readlane_f64(x[0], 0);
@@ -312,59 +310,6 @@ __device__ __forceinline__ bool db_panel(double* lds, int k, double* __restrict_
       db_fmac_bcast_from<2>(q, x, row0_to_rows(m), m);
     }
   }
-#else
-  // Software-pipelined (r5): the entry s = q+1 is updated first, the next pivot read from it, and
-  // the 7 dependent steps of its 1/sqrt (v_rsq, two Newton steps) are interleaved one by one with
-  // the remaining updates of column q, each group fenced by a scheduling barrier (a wave issues in
-  // order: with the chain after the updates, as the compiler placed it, a column cost the issue of
-  // all its ~50 VALU instructions plus the chain's latency, 426 cycles; profiles/r5/
-  // f128_panel_variants.txt). Same operations in the same order per value: bitwise unchanged.
-  // (Rejected, same probe: one column deferred through an LDS broadcast buffer 439-441 cycles per
-  // column, and it reordered the updates; the pivot chain on uniform values one step ahead 456-460;
-  // that with one Newton step 439-443; uniform chain + LDS buffer 436-440.)
-  double inv;
-  {
-    const double p0 = readlane_f64(x[0], 0);
-    bad = !(p0 > 0.0);
-    inv = rsqrt_nr(p0);
-  }
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const double m = (arow && r < q) ? 0.0 : x[q] * inv;
-    x[q] = m;
-    if (q == 15) break;
-    x[q + 1] = fma(-m, readlane_f64(m, q + 1), x[q + 1]);
-    const double pn = readlane_f64(x[q + 1], q + 1);
-    bad = bad | !(pn > 0.0);
-    int s = q + 2;
-    auto upd = [&](int n) {  // the next n entries of column q's update (compile-time s)
-#pragma unroll
-      for (int i = 0; i < n; ++i)
-        if (s < 16) {
-          x[s] = fma(-m, readlane_f64(m, s), x[s]);
-          ++s;
-        }
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    __builtin_amdgcn_sched_barrier(0);
-    double y = __builtin_amdgcn_rsq(pn);  // (rsqrt_nr's operations, in its order)
-    const double h = 0.5 * pn;
-    upd(1);
-    double hy = h * y;
-    upd(1);
-    double t = fma(-hy, y, 0.5);
-    upd(1);
-    y = fma(y, t, y);
-    upd(1);
-    hy = h * y;
-    upd(1);
-    t = fma(-hy, y, 0.5);
-    upd(1);
-    y = fma(y, t, y);
-    upd(16);
-    inv = y;
-  }
-#endif
   // (the diagonal row's own entries right of its pivot took updates with m = L(q, q): not stored)
   if (arow) {
     double* gl = Lt + (size_t)(16 * k + r) * ld + 16 * k;
