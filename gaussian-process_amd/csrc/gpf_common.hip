@@ -252,8 +252,11 @@ __device__ __forceinline__ void dl_row_offsets(int lane, uint32_t (&o)[4]) {
 // ds_read immediates; the global sources are a scalar chunk base plus a fixed 32-bit per-lane
 // byte offset (the saddr form of global_load_lds). Wave layout of the 128-tiles: all 128 rows
 // (8 row blocks) x one 16-column slab, so a k-step is 8 A reads, 1 B read and 8 MFMAs.
-template <bool NN, bool NEG>
+// NS: LDS stages (2: double-buffered, the default; 3-4 for one-workgroup-per-CU launches, where
+// the next chunk's transfer has less time behind one chunk of MFMAs than two workgroups give it)
+template <bool NN, bool NEG, int NS = 2>
 struct DenseRun {
+  static_assert(NS >= 2 && NS <= 4, "DenseRun stages");
   static constexpr int MBR = Geo<128>::MBR;  // 8
   static_assert(Geo<128>::MBC == 1 && Geo<128>::WR == 1, "128-tile wave layout: all rows x one column slab");
   uint32_t la[4], lb[4];  // LDS read offsets (bytes) per k-step: A rows, B^T rows (!NN) / B (NN, [0] only)
@@ -322,10 +325,30 @@ struct DenseRun {
   template <int BUF, int M0>
   __device__ __forceinline__ void chunk(Acc<128>& acc, const double* Ap, const double* Bp, int ldb, int t, int nch,
                                         double* smem) const {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // chunk t's transfers done; chunks t+1 .. t+NS-2 (4 transfers each per wave) may be in flight
+    if constexpr (NS == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (t + NS - 2 < nch) {
+        if constexpr (NS == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
     __syncthreads();
-    if (t + 1 < nch) issue<1 - BUF>(Ap, Bp, ldb, t + 1, smem);
+    if (t + NS - 1 < nch) issue<(BUF + NS - 1) % NS>(Ap, Bp, ldb, t + NS - 1, smem);
     mma<BUF, M0>(acc, smem);
+  }
+  template <int M0>
+  __device__ __forceinline__ void chunk_rt(int b, Acc<128>& acc, const double* Ap, const double* Bp, int ldb, int t,
+                                           int nch, double* smem) const {
+    switch (b) {
+      case 0: chunk<0, M0>(acc, Ap, Bp, ldb, t, nch, smem); break;
+      case 1: chunk<1 % NS, M0>(acc, Ap, Bp, ldb, t, nch, smem); break;
+      case 2: chunk<2 % NS, M0>(acc, Ap, Bp, ldb, t, nch, smem); break;
+      default: chunk<3 % NS, M0>(acc, Ap, Bp, ldb, t, nch, smem); break;
+    }
   }
 
   // chunks [t0, t1) with one MFMA pattern (row blocks mi >= M0; M0 = MBR keeps only the
@@ -334,13 +357,27 @@ struct DenseRun {
   __device__ __forceinline__ void run(Acc<128>& acc, const double* Ap, const double* Bp, int ldb, int t0, int t1,
                                       int nch, double* smem) const {
     int t = t0;
-    if (t < t1 && (t & 1)) chunk<1, M0>(acc, Ap, Bp, ldb, t++, nch, smem);
+    if constexpr (NS == 2) {
+      if (t < t1 && (t & 1)) chunk<1, M0>(acc, Ap, Bp, ldb, t++, nch, smem);
 #pragma unroll 1
-    for (; t + 1 < t1; t += 2) {
-      chunk<0, M0>(acc, Ap, Bp, ldb, t, nch, smem);
-      chunk<1, M0>(acc, Ap, Bp, ldb, t + 1, nch, smem);
+      for (; t + 1 < t1; t += 2) {
+        chunk<0, M0>(acc, Ap, Bp, ldb, t, nch, smem);
+        chunk<1, M0>(acc, Ap, Bp, ldb, t + 1, nch, smem);
+      }
+      if (t < t1) chunk<0, M0>(acc, Ap, Bp, ldb, t, nch, smem);
+    } else {
+#pragma unroll 1
+      for (; t < t1 && t % NS != 0; ++t) chunk_rt<M0>(t % NS, acc, Ap, Bp, ldb, t, nch, smem);
+#pragma unroll 1
+      for (; t + NS - 1 < t1; t += NS) {
+        chunk<0, M0>(acc, Ap, Bp, ldb, t, nch, smem);
+        chunk<1, M0>(acc, Ap, Bp, ldb, t + 1, nch, smem);
+        chunk<2 % NS, M0>(acc, Ap, Bp, ldb, t + 2, nch, smem);
+        if constexpr (NS == 4) chunk<3, M0>(acc, Ap, Bp, ldb, t + 3, nch, smem);
+      }
+#pragma unroll 1
+      for (; t < t1; ++t) chunk_rt<M0>(t % NS, acc, Ap, Bp, ldb, t, nch, smem);
     }
-    if (t < t1) chunk<0, M0>(acc, Ap, Bp, ldb, t, nch, smem);
   }
 };
 
@@ -350,7 +387,7 @@ struct DenseRun {
 // pattern each. Each run is its own straight-line loop (one pattern per loop keeps the register
 // allocation of the dense loop); exactly the MFMAs tri_live admits are issued, so results are
 // bitwise those of per-block skipping. Every wave still passes one barrier per chunk.
-template <bool NN, bool NEG = false, int TRI = TRI_NONE>
+template <bool NN, bool NEG = false, int TRI = TRI_NONE, int NS = 2>
 __device__ __forceinline__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
                                int ldb, int K, double* smem, const Quad<128>& qd) {
   const int nch = K / DL_KC;
@@ -358,8 +395,13 @@ __device__ __forceinline__ void gemm_stream_dl(Acc<128>& acc, const double* __re
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const double* Ar = uniform_ptr(Ap);  // scalar bases
   const double* Br = uniform_ptr(Bp);
-  const DenseRun<NN, NEG> dr(qd, lda, ldb, wave);
+  const DenseRun<NN, NEG, NS> dr(qd, lda, ldb, wave);
   dr.template issue<0>(Ar, Br, ldb, 0, smem);
+  if constexpr (NS >= 3) {  // the first NS-1 chunks in flight
+    if (nch > 1) dr.template issue<1>(Ar, Br, ldb, 1, smem);
+    if constexpr (NS >= 4)
+      if (nch > 2) dr.template issue<2>(Ar, Br, ldb, 2, smem);
+  }
   // Drain every outstanding vector-memory op here (the chunk-0 transfers, which the first chunk
   // waits for anyway, and e.g. an accumulator seed loaded just before) through the builtin, so
   // that the compiler's wait bookkeeping sees them done: otherwise it keeps an s_waitcnt for the

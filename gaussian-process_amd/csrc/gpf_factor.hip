@@ -102,14 +102,20 @@ enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2, ROLE_DIAG = 3, ROLE_SYRK =
 // piece — the critical tile's included — does about the same work, instead of a fixed number of
 // pieces per tile (which gave the deepest tiles the longest pieces: the critical tile's GEMM, not
 // the diagonal factor, ended the launch). At most SPLIT_MAXS pieces (the reduction tree's bound).
+// (r5) At least SPLIT_MINP pieces per tile: the flat finish (flat_piece) spreads a tile's
+// triangular multiply and diagonal-block update over its pieces' CUs, so the shallow tiles of the
+// first launches (J = 0: no GEMM at all) no longer finish on one CU each (launch 0: ~77 us, the
+// diagonal factor ~40 of it). Pieces past the depth add zero partials.
 constexpr int SPLIT_MAXS = 32;
+constexpr int SPLIT_MINP = 4;
 __host__ __device__ __forceinline__ int split_all_chunks(int J, int w, int nt) {
   const int nL = nt - 1 - J;
   return (w < nL ? J : J - (w - nL)) * (T / DL_KC);  // L tile: depth 128J; U tile K: 128(J-K)
 }
 __host__ __device__ __forceinline__ int split_all_pieces(int J, int w, int nt, int tgt) {
   const int ch = split_all_chunks(J, w, nt);
-  const int s = ch <= 0 ? 1 : (ch + tgt - 1) / tgt;
+  int s = ch <= 0 ? 1 : (ch + tgt - 1) / tgt;
+  s = s < SPLIT_MINP ? SPLIT_MINP : s;
   return s > SPLIT_MAXS ? SPLIT_MAXS : s;
 }
 
@@ -223,8 +229,10 @@ __device__ __forceinline__ unsigned long long realtime() {
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
   return t;
 }
-#define GPF_PHASE(k) \
-  if (tid == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N) g_wg_phase[J][blockIdx.x][k] = realtime()
+// (r5: the latest wave's end of the phase: lane 0 of every wave that reaches it, atomic max)
+#define GPF_PHASE(k)                                                                                   \
+  if ((tid & 63) == 0 && J < WG_TRACE_J && blockIdx.x < WG_TRACE_N)                                  \
+  __hip_atomic_fetch_max(&g_wg_phase[J][blockIdx.x][k], realtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
 #else
 #define GPF_PHASE(k)
 #endif
@@ -494,7 +502,15 @@ __host__ __device__ __forceinline__ int split_cnt_stride(int nt) {  // counter w
 // also the region of slab s)
 __device__ __forceinline__ int region_slab(int r) { return r < 4 ? r : 11 - r; }
 
-// Bounded wave-level wait for *c >= n, then an agent-scope acquire; true: timed out (info bit 2).
+// The flat finish's hand-offs read what other workgroups stored write-through (sc1) with loads
+// that bypass L1 and L2 (sc0 sc1: from memory), after a relaxed poll of the counter, instead of an
+// agent-scope acquire: that acquire invalidates the XCD's L2, and ~1000 waiting waves per launch
+// issuing it thrashed the L2s of every XCD — the diagonal-update phase alone took ~25 us in the
+// first launches (same box, prediction factorisation 2.44-2.57 -> 2.15-2.25 ms; profiles/r5/
+// ab_flat_bypass.txt, predict_trace_bypass.txt). The data each reader needs was drained to memory
+// before the counter moved (s_waitcnt vmcnt(0) after the write-through stores).
+constexpr int FLAT_LD = 17;  // buffer-load cache policy of the flat finish's hand-off reads: sc0 | sc1
+// Bounded wave-level wait for *c >= n (the reads after it use FLAT_LD); true: timed out (info bit 2).
 __device__ __forceinline__ bool wave_wait(const unsigned* c, unsigned n, int* info, int spins) {
   int k = 0;
   while ((unsigned)__builtin_amdgcn_readfirstlane(
@@ -505,7 +521,7 @@ __device__ __forceinline__ bool wave_wait(const unsigned* c, unsigned n, int* in
     }
     __builtin_amdgcn_s_sleep(2);
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("" ::: "memory");  // (no acquire: the reads that follow bypass the caches, FLAT_LD)
   return false;
 }
 
@@ -521,7 +537,7 @@ __device__ __forceinline__ bool group_wait(const unsigned* c, unsigned n, int* i
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("" ::: "memory");  // (no acquire: FLAT_LD reads)
     *sflag = late;
   }
   __syncthreads();
@@ -540,7 +556,7 @@ __device__ __forceinline__ void flat_reduce_unit(double* pt, int np, int u) {
     u4v q[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i)
-      if (i0 + i < np) q[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, (i0 + i) * (T * T * 8) + u * 1024, 0);
+      if (i0 + i < np) q[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, (i0 + i) * (T * T * 8) + u * 1024, FLAT_LD);
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       if (i0 + i < np) {
@@ -559,7 +575,7 @@ __device__ __forceinline__ void flat_load_region(Acc<T>& acc, const double* pt, 
   for (int mi = 0; mi < Acc<T>::MBR; ++mi)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const d2 v = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, r * NODE_WAVE + (2 * mi + h) * 1024, 0));
+      const d2 v = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, r * NODE_WAVE + (2 * mi + h) * 1024, FLAT_LD));
       acc.v[mi][0][2 * h] = v.x;
       acc.v[mi][0][2 * h + 1] = v.y;
     }
@@ -580,43 +596,59 @@ __device__ __forceinline__ void flat_store_operand(const d4 (&o)[2], double* slo
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, d2{o[j][e], o[j][e + 1]}), ws, lane * 16,
                                              r * NODE_WAVE + (2 * (2 * P + j) + e / 2) * 1024, 16);  // write-through
 }
-__device__ __forceinline__ void flat_load_operand(double (&a)[32], const double* slot1, int r) {
+// 8 k-steps (t0 .. t0+7) of a slab's operands: 4 coalesced 16-B loads
+__device__ __forceinline__ void flat_load_operand8(double (&a)[8], const double* slot1, int r, int t0) {
   const int lane = threadIdx.x & 63;
   const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(slot1), 0, T * T * 8, 0x00020000);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const d2 v = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, r * NODE_WAVE + i * 1024, 0));
+  for (int i = 0; i < 4; ++i) {
+    const d2 v = __builtin_bit_cast(
+        d2, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, r * NODE_WAVE + (t0 / 2 + i) * 1024, FLAT_LD));
     a[2 * i] = v.x;
     a[2 * i + 1] = v.y;
   }
 }
 
 // Phase C: block (ib, jb) (ib >= jb) of A_II -= L_IJ L_IJ^T: 32 MFMAs, k = 4 t + (lane >> 4)
-// ascending, seeded with A_II (syrk_rows' operands and order per element).
+// ascending, seeded with A_II (syrk_rows' operands and order per element); the diagonal blocks
+// also y_I -= L_IJ z_J for their 16 rows (t ascending per lane, then the lane groups). The
+// operands stream in 4 batches of 8 k-steps, two in flight (32 k-steps of both operands at once
+// are 128 VGPRs: the compiler serialised their loads into several round trips).
 __device__ __forceinline__ void flat_syrk_block(double* Aii, size_t ld, const double* slot1, int ib, int jb, double* yi,
                                                 const double* zj) {
   const int lane = threadIdx.x & 63, g = lane >> 4, cl = lane & 15;
   double* cp = launder(Aii + (size_t)(16 * ib + g) * ld + 16 * jb + cl);
+  const int ra = region_slab(ib), rb = region_slab(jb);
+  const bool diag = ib == jb;
   d4 acc;
 #pragma unroll
   for (int r = 0; r < 4; ++r) acc[r] = cp[(size_t)(4 * r) * ld];
-  double a[32];
-  flat_load_operand(a, slot1, region_slab(ib));
-  if (ib == jb) {
+  const auto zs = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(zj), 0, T * 8, 0x00020000);
+  double yr = 0.0;
+  double a[2][8], b[2][8];
+  flat_load_operand8(a[0], slot1, ra, 0);
+  if (!diag) flat_load_operand8(b[0], slot1, rb, 0);
+  flat_load_operand8(a[1], slot1, ra, 8);
+  if (!diag) flat_load_operand8(b[1], slot1, rb, 8);
 #pragma unroll
-    for (int t = 0; t < 32; ++t) acc = mfma_neg_a(a[t], a[t], acc);
-    // y_I rows 16 ib + c: L(16 ib + c, k) z_k over k = 4 t + g ascending per lane, then the lane groups
-    const double* zg = launder(zj + g);
-    double yr = 0.0;
+  for (int q = 0; q < 4; ++q) {
+    const int u = q & 1;
 #pragma unroll
-    for (int t = 0; t < 32; ++t) yr = fma(a[t], zg[4 * t], yr);
+    for (int t = 0; t < 8; ++t) acc = mfma_neg_a(a[u][t], diag ? a[u][t] : b[u][t], acc);
+    if (diag) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        yr = fma(a[u][t], __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(zs, (4 * (8 * q + t) + g) * 8, 0, FLAT_LD)),
+                 yr);
+    }
+    if (q + 2 < 4) {
+      flat_load_operand8(a[u], slot1, ra, 8 * (q + 2));
+      if (!diag) flat_load_operand8(b[u], slot1, rb, 8 * (q + 2));
+    }
+  }
+  if (diag) {
     yr = sum_lane_groups(yr);
     if (g == 0) yi[16 * ib + cl] = yi[16 * ib + cl] - yr;
-  } else {
-    double b[32];
-    flat_load_operand(b, slot1, region_slab(jb));
-#pragma unroll
-    for (int t = 0; t < 32; ++t) acc = mfma_neg_a(a[t], b[t], acc);
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) cp[(size_t)(4 * r) * ld] = acc[r];
@@ -1126,11 +1158,12 @@ __global__ __launch_bounds__(NTHR) void k_fill_hash(double* __restrict__ p, long
   }
 }
 
+template <int NS>
 __global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_gemm_bench(int mode, int D, int Npad, int P,
                                                                                    const double* __restrict__ Lb,
                                                                                    double* __restrict__ C,
                                                                                    unsigned long long* clk) {
-  __shared__ __attribute__((aligned(16))) double smem[DL_STAGE];
+  __shared__ __attribute__((aligned(16))) double smem[NS * DL_BUF];
   __shared__ unsigned long long cs[2];
   const ClockSpan span(cs);
   span.start(clk);
@@ -1144,9 +1177,9 @@ __global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_gemm_bench(in
   Acc<T> acc;
   acc.zero();
   if (mode & 4)
-    gemm_stream_dl<true, false>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)w * T, Npad, D, smem, qd);
+    gemm_stream_dl<true, false, TRI_NONE, NS>(acc, Lp + (size_t)I * T * ld, Npad, Lp + (size_t)w * T, Npad, D, smem, qd);
   else
-    gemm_stream_dl<false, true>(acc, Lp + (size_t)J * T * ld, Npad, Lp + (size_t)I * T * ld, Npad, D, smem, qd);
+    gemm_stream_dl<false, true, TRI_NONE, NS>(acc, Lp + (size_t)J * T * ld, Npad, Lp + (size_t)I * T * ld, Npad, D, smem, qd);
   acc.store(qd, C + (size_t)b * T * T, T);
   span.stop(clk);
 }

@@ -1807,7 +1807,9 @@ int gpf_gemm_bench(gpf_ctx* c, int mode, int Npad, int P, int tiles, int D, int 
   const size_t n = (size_t)P * Npad * Npad;
   GPF_HIP(c, hipMalloc(&L, n * 8));
   GPF_HIP(c, hipMalloc(&C, (size_t)P * tiles * T * T * 8));
-  // mode bit 8: zero operands (rounds 1-3); otherwise hashed values in [-1, 1) (gpf::k_fill_hash)
+  // mode bit 8: zero operands (rounds 1-3); otherwise hashed values in [-1, 1) (gpf::k_fill_hash);
+  // bit 16 / 32: the 3- / 4-stage LDS pipeline (gpf::DenseRun NS) instead of 2
+  const auto kb = (mode & 32) ? gpf::k_gemm_bench<4> : (mode & 16) ? gpf::k_gemm_bench<3> : gpf::k_gemm_bench<2>;
   if (mode & 8)
     GPF_HIP(c, hipMemsetAsync(L, 0, n * 8, c->stream));
   else
@@ -1819,10 +1821,10 @@ int gpf_gemm_bench(gpf_ctx* c, int mode, int Npad, int P, int tiles, int D, int 
   unsigned long long* clk = nullptr;
   GPF_HIP(c, hipMalloc(&clk, 2 * sizeof(unsigned long long)));
   GPF_HIP(c, hipMemsetAsync(clk, 0, 2 * sizeof(unsigned long long), c->stream));
-  hipLaunchKernelGGL(gpf::k_gemm_bench, dim3(W), dim3(gpf::STEP_NTH), 0, c->stream, mode, D, Npad, P, L, C, nullptr);
+  hipLaunchKernelGGL(kb, dim3(W), dim3(gpf::STEP_NTH), 0, c->stream, mode, D, Npad, P, L, C, nullptr);
   GPF_HIP(c, hipEventRecord(a, c->stream));
   for (int i = 0; i < iters; ++i)
-    hipLaunchKernelGGL(gpf::k_gemm_bench, dim3(W), dim3(gpf::STEP_NTH), 0, c->stream, mode, D, Npad, P, L, C, clk);
+    hipLaunchKernelGGL(kb, dim3(W), dim3(gpf::STEP_NTH), 0, c->stream, mode, D, Npad, P, L, C, clk);
   GPF_HIP(c, hipEventRecord(b, c->stream));
   GPF_HIP(c, hipEventSynchronize(b));
   c->bench_sclk = read_clock(clk);

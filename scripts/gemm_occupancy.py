@@ -12,6 +12,10 @@ ctx = gpfit.Context(0)
 print("mfma peak probe:", round(ctx.mfma_peak(), 1), "TF/s")
 for depth in (256, 512, 2048):
     for P, tiles in ((32, 8), (64, 8)):
-        tf = max(ctx.gemm_bench(mode=0, npad=4096, particles=P, tiles=tiles, depth=depth, iters=5) for _ in range(3))
-        print(f"depth {depth:5d}  workgroups {P * tiles:4d} ({P * tiles // 256} per CU): {tf:6.1f} TF/s "
-              f"at {ctx.bench_clock():.0f} MHz")
+        for ns, mode in ((2, 0), (3, 16), (4, 32)):
+            if P * tiles > 256 and ns > 2:
+                continue  # (3-4 stages take one workgroup per CU)
+            tf = max(ctx.gemm_bench(mode=mode, npad=4096, particles=P, tiles=tiles, depth=depth, iters=5)
+                     for _ in range(3))
+            print(f"depth {depth:5d}  workgroups {P * tiles:4d} ({P * tiles // 256} per CU)  {ns} stages: "
+                  f"{tf:6.1f} TF/s at {ctx.bench_clock():.0f} MHz")

@@ -12,7 +12,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["GPFIT_LIB"] = os.path.join(ROOT, "gaussian-process_amd", "libgpfit_trace.so")
+os.environ["GPFIT_LIB"] = os.environ.get("TRACE_LIB", os.path.join(ROOT, "gaussian-process_amd", "libgpfit_trace.so"))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "gaussian-process_amd")]
 import gpfit  # noqa: E402
 

@@ -109,7 +109,9 @@ def test_default_plans_of_the_baseline_configs(env):
     assert bs["S"] == 1 and bs["Smax"] > 1 and bs["split_tiles"] > 0
     env({})
     one = gpfit.plan_check(1, 32)           # prediction: single particle, all tiles split
-    assert one["S"] > 1 and one["whole_tiles"] >= 31  # J = 0 has nothing to split
+    # every tile in at least SPLIT_MINP (4) pieces, J = 0's zero-depth tiles included (the flat
+    # finish spreads their triangular multiply and diagonal update over the pieces' CUs)
+    assert one["S"] > 1 and one["whole_tiles"] == 0
     # balanced pieces: every launch fits one workgroup per CU (255 + the diagonal workgroup),
     # and the critical tile of the deep launches gets the most pieces
     assert one["workgroups"] <= 32 * 256 and one["Smax"] > 8
