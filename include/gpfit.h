@@ -262,7 +262,8 @@ int gpf_bench_clock(gpf_ctx* ctx, double* mhz);
 /* Measurement hook: TF/s of the block-column GEMM core alone (no factorisation):
  * P particles' Npad x Npad matrices, `tiles` workgroups per particle, depth D, `iters`
  * timed launches; mode 0 = per-particle operands, mode 1 = one shared (L2-resident) pair; mode
- * bit 2 (4): U-tile-shaped operands; bit 3 (8): zero operands instead of hashed values in [-1, 1). */
+ * bit 2 (4): U-tile-shaped operands; bit 3 (8): zero operands instead of hashed values in [-1, 1);
+ * bit 4 (16) / bit 5 (32): the 3- / 4-stage LDS pipeline (one workgroup per CU). */
 int gpf_gemm_bench(gpf_ctx* ctx, int mode, int Npad, int P, int tiles, int D, int iters, double* tflops);
 
 #ifdef __cplusplus
