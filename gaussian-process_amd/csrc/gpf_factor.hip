@@ -473,19 +473,19 @@ __device__ __forceinline__ bool wait_diag(const int* flag, int J, int* info, int
 // single-particle prediction that was ~30 us of tree plus ~20 us of one-CU finish per launch, on
 // every launch's chain. Here the np pieces of a tile share all of it:
 //   A  every piece stores its partial to its slot (write-through, drained) and counts in (c[0]);
-//   R  once all np are in, the 8 np waves of the pieces sum the slots' 128 1-KiB units (slot
-//      order, so results are deterministic), 16 slots per round trip, into slot 0 in place, and
-//      count each unit in on its wave region's counter (c[1 + r]);
-//   T  the pieces 0..min(np,8)-1 load their regions' sums, wait for the diagonal block (U_JJ,
-//      z_J) and stage U_JJ; wave v of piece s finishes region r = s + np v (< 8): the triangular
-//      multiply, the stores and y_I (L tiles) or the column partials (U tiles); an L tile's wave
-//      also leaves its rows of L_IJ in slot 1 in the MFMA operand layout and counts in again;
+//   R  piece s < min(np, 8) owns the regions r = s + np k < 8 (at most 2: np >= SPLIT_MINP);
+//      once all np partials are in, its 8 waves sum those regions' 1-KiB units over the slots
+//      (slot order, so results are deterministic; 16 slots per round trip) into its LDS;
+//   T  the region's two waves take the sum from LDS, wait for the diagonal block (U_JJ, z_J),
+//      stage U_JJ and finish it: the triangular multiply (output row blocks split between the
+//      two), the stores and the column partials (U tiles), or, for an L tile, its rows of L_IJ
+//      also to slot 1 in the MFMA operand layout, then count in (c[1 + r], 2 per region);
 //   C  (L tiles) the 8 np waves take the 36 lower 16x16 blocks of A_II -= L_IJ L_IJ^T, block
 //      (ib, jb) as soon as the regions of slabs ib and jb are in: 32 MFMAs over k ascending with
-//      A_II as the seed — the per-element MFMA sequence of syrk_rows.
-// A tile of one piece (ONE: the early launches) runs the same phases T and C on its own
-// registers. r5, single-particle prediction N=4096: per launch ~70 us, of which the
-// finish after the diagonal block ~26 us (T ~10, C ~12; profiles/r5/predict_trace_*.txt).
+//      A_II as the seed — the per-element MFMA sequence of syrk_rows; the diagonal blocks also
+//      y_I -= L_IJ z_J for their rows.
+// The hand-off reads bypass the caches (FLAT_LD, below). r5 (profiles/r5/predict_trace_*.txt):
+// prediction N=4096, per launch 46-67 us of which the finish after the pieces' GEMMs ~20 us.
 // Every wait is bounded (`spins`; timeout: info bit 2, the wave or piece leaves). No wait can hold
 // the slots an awaited workgroup needs: the diagonal workgroups come first in the launch and wait
 // for nothing; the np <= SPLIT_MAXS pieces of a tile have consecutive workgroup ids, which the
@@ -493,8 +493,8 @@ __device__ __forceinline__ bool wait_diag(const int* flag, int J, int* info, int
 // 4 pieces of a tile — a stalled XCD (64 slots) would need all its slots taken by pieces of the
 // lowest incomplete tile. Counters: FLAT_CNT words per (particle, launch, tile), zeroed by the
 // factorisation's memset, never reused within it.
-constexpr int FLAT_CNT = 16;  // [0] partials stored; [1 + r]: units of region r summed (16), + 1 once an L tile's
-                              // region is finished (its phase-C operands stored)
+constexpr int FLAT_CNT = 16;  // [0] partials stored; [1 + r]: the waves that finished region r of an L tile
+                              // (its phase-C operands stored)
 __host__ __device__ __forceinline__ int split_cnt_stride(int nt) {  // counter words per split tile and particle
   return SPLIT_CNT > FLAT_CNT * nt ? SPLIT_CNT : FLAT_CNT * nt;
 }
@@ -546,9 +546,8 @@ __device__ __forceinline__ bool group_wait(const unsigned* c, unsigned n, int* i
 
 typedef unsigned u4v __attribute__((ext_vector_type(4)));
 
-// Phase R: unit u (bytes [1 KiB u, 1 KiB (u+1)) of a slot) summed over the np slots in slot order,
-// to slot 0 (write-through).
-__device__ __forceinline__ void flat_reduce_unit(double* pt, int np, int u) {
+// Unit u summed over the np slots in slot order (phase R, local): 16 slots per round trip.
+__device__ __forceinline__ d2 flat_sum_unit(const double* pt, int np, int u) {
   const int lane = threadIdx.x & 63;
   const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(pt), 0, np * T * T * 8, 0x00020000);
   d2 sum = {0.0, 0.0};
@@ -564,18 +563,16 @@ __device__ __forceinline__ void flat_reduce_unit(double* pt, int np, int u) {
         sum = (i0 + i == 0) ? v : sum + v;
       }
   }
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, sum), rs, lane * 16, u * 1024, 16);  // sc1: write-through
+  return sum;
 }
-
-// Phase T's operand: wave region r of slot 0 into the accumulator layout.
-__device__ __forceinline__ void flat_load_region(Acc<T>& acc, const double* pt, int r) {
+// A region's 16 summed units from LDS (1 KiB each, 16 B per lane) into the accumulator layout.
+__device__ __forceinline__ void flat_lds_region(Acc<T>& acc, const double* s) {
   const int lane = threadIdx.x & 63;
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(pt), 0, T * T * 8, 0x00020000);
 #pragma unroll
   for (int mi = 0; mi < Acc<T>::MBR; ++mi)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const d2 v = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, r * NODE_WAVE + (2 * mi + h) * 1024, FLAT_LD));
+      const d2 v = *reinterpret_cast<const d2*>(s + (2 * mi + h) * 128 + lane * 2);
       acc.v[mi][0][2 * h] = v.x;
       acc.v[mi][0][2 * h + 1] = v.y;
     }
@@ -655,7 +652,7 @@ __device__ __forceinline__ void flat_syrk_block(double* Aii, size_t ld, const do
 }
 
 // One piece (sidx of np) of tile w of launch J under the flat finish (see above); LT: an L tile.
-template <bool LT, bool ONE>
+template <bool LT>
 __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad, double* __restrict__ Lp,
                                         double* __restrict__ Up, double* __restrict__ yp, double* __restrict__ s2p,
                                         double* __restrict__ szp, int* __restrict__ info, int N,
@@ -671,64 +668,56 @@ __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   double* pt = part + (size_t)(p * (nt - 1) + w) * S2 * T * T;
   unsigned* ca = cnt + (size_t)p * (nt - 1) * split_cnt_stride(nt) + (size_t)(J * (nt - 1) + w) * FLAT_CNT;
-  // A: the partial (piece 0 of an L tile seeded with the covariance tile A_IJ^T). ONE (a tile of one
-  // piece, np = 1): the whole GEMM, kept in the registers — wave v's accumulators are region v.
+  // A: the partial (piece 0 of an L tile seeded with the covariance tile A_IJ^T)
   Acc<T> acc;
   if (LT)
     split_gemm<false, true, true>(acc, Lp + (size_t)J * T * ld, Npad, Lp + (size_t)I * T * ld, Npad, J * T / DL_KC,
                                   np, sidx, lds, qd, [&](Acc<T>& a) { cov_tile_acc(a, qd, x, lp, d, N, J, I, lds); });
-  else if (ONE) {  // (U_KK is lower triangular: the wave's first chunks add zeros, skipped)
-    acc.zero();
-    gemm_stream_dl<true, false, TRI_B_KGEC>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
-                                            Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T, lds, qd);
-  } else  // (the triangular first block runs dense: its upper part holds zeros)
+  else  // (the triangular first block runs dense: its upper part holds zeros)
     split_gemm<true, false, false>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
                                    Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T / DL_KC, np, sidx, lds, qd,
                                    [](Acc<T>&) {});
-  if (!ONE) {
-    store_node(acc, pt + (size_t)sidx * T * T, qd);
-    acc.zero();  // (dead until phase T reloads it: a constant, not 64 registers held across phase R)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's part of the partial drained
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(ca, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    GPF_PHASE(3);
-    if (group_wait(ca, (unsigned)np, info, spins, sflag)) return;
-    // R
-    for (int u = sidx * 8 + wave; u < 128; u += 8 * np) {
-      flat_reduce_unit(pt, np, u);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (qd.lane == 0) __hip_atomic_fetch_add(ca + 1 + (u >> 4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  GPF_PHASE(0);
-  // T (the region's sum is loaded before the wait for the diagonal block: its latency hides
-  // there). With np >= 4 two waves share a region (WPR = 2, on different SIMDs): the triangular
-  // multiply's output row blocks {0,1, 6,7} (P = 0, 3) and {2,3, 4,5} (P = 1, 2), 72 of its 144
-  // MFMAs each.
-  const int WPR = (!ONE && np >= 4) ? 2 : 1;
-  const int half = WPR == 2 ? (wave & 1) : -1;  // -1: every P
+  store_node(acc, pt + (size_t)sidx * T * T, qd);
+  acc.zero();  // (dead until phase T reloads it: a constant, not 64 registers held across phase R)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's part of the partial drained
+  __syncthreads();
+  if (tid == 0) __hip_atomic_fetch_add(ca, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  GPF_PHASE(3);
+  // T (with R): piece s < min(np, 8) finishes regions r = s + np k < 8 (nr of them). With np >= 4
+  // (always: SPLIT_MINP) two waves share a region (on different SIMDs): the triangular multiply's
+  // output row blocks {0,1, 6,7} (P = 0, 3) and {2,3, 4,5} (P = 1, 2), 72 of its 144 MFMAs each.
+  static_assert(SPLIT_MINP >= 4, "flat_piece: two waves per region, at most 2 regions per piece");
+  const int half = wave & 1;
+  const int r = sidx + np * (wave >> 1);  // the region this wave finishes (if < 8)
   double* slot1 = pt + (size_t)T * T;
   if (sidx < 8) {
-    double* zj = lds + STEP_ZJ;
-    const int r = sidx + np * (WPR == 2 ? (wave >> 1) : wave);  // the region this wave finishes
-    bool late = false;
-    if (!ONE && r < 8) {
-      late = wave_wait(ca + 1 + r, 16u, info, spins);
-      if (!late) flat_load_region(acc, pt, r);
+    if (group_wait(ca, (unsigned)np, info, spins, sflag)) return;
+    // R, local: the piece's 8 waves sum its regions' 16 1-KiB units each over the np slots (slot
+    // order) into LDS, where the region's two waves pick their operand up — no store, drain,
+    // counter and reload through memory between the reduction and the triangular multiply
+    const int nr = (8 - sidx + np - 1) / np;
+    for (int i = wave; i < 16 * nr; i += 8) {
+      const int k = i >> 4, j = i & 15;
+      const d2 sum = flat_sum_unit(pt, np, (sidx + np * k) * 16 + j);
+      *reinterpret_cast<d2*>(lds + k * 2048 + j * 128 + qd.lane * 2) = sum;
     }
-    if (wait_diag(dflag + p, J, info, spins, sflag)) return;  // U_JJ, z_J
+    __syncthreads();
+    GPF_PHASE(0);
+    if (r < 8) flat_lds_region(acc, lds + ((r - sidx) / np) * 2048);
+    double* zj = lds + STEP_ZJ;
+    if (wait_diag(dflag + p, J, info, spins, sflag)) return;  // U_JJ, z_J (its barrier: the region reads done)
     if (!LT && tid < T) zj[tid] = yp[J * T + tid];
     tri_to_lds(Up + (size_t)J * T * ld + (size_t)J * T, ld, lds);  // (its barrier also publishes z_J)
-    auto mine = [&](int P) { return half < 0 || (half == 0) == (P == 0 || P == 3); };
+    const bool outer = half == 0;  // this wave's output row blocks: P = 0, 3 (outer) or 1, 2
     const int cb = 16 * region_slab(r < 8 ? r : 0);
     if (LT) {
-      if (r < 8 && !late) {
+      if (r < 8) {
         // L_IJ^T = U_JJ D for the slab's 16 columns of D (rows cb.. of L_IJ); the rows also to slot 1
         // in the operand layout (y_I -= L_IJ z_J follows in phase C, from those operands)
         double* lrow = launder(Lp + (size_t)(I * T + cb + cl) * ld + (size_t)J * T + g);
 #pragma unroll
         for (int P = 0; P < 4; ++P) {
-          if (!mine(P)) continue;
+          if (outer != (P == 0 || P == 3)) continue;
           d4 o[2];
           switch (P) {
             case 0: trmm_acc<0, false>(o, acc, lds); break;
@@ -747,13 +736,13 @@ __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad
       }
     } else {
       // U_JK = -U_JJ W; the column partials of colsum(U^2) and U^T z: each wave's rows in P order,
-      // the 4 lane groups, then (WPR = 2) the two waves' sums, half 0's first
+      // the 4 lane groups, then the two waves' sums, half 0's first
       double a2 = 0.0, az = 0.0;
-      if (r < 8 && !late) {
+      if (r < 8) {
         double* ucol = launder(Up + (size_t)(J * T + g) * ld + (size_t)K * T + cb + cl);
 #pragma unroll
         for (int P = 0; P < 4; ++P) {
-          if (!mine(P)) continue;
+          if (outer != (P == 0 || P == 3)) continue;
           d4 o[2];
           switch (P) {
             case 0: trmm_acc<0, true>(o, acc, lds); break;
@@ -775,22 +764,16 @@ __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad
         a2 = sum_lane_groups(a2);
         az = sum_lane_groups(az);
       }
-      double* xs = lds + STEP_XS + 32 * (wave >> 1);  // (WPR = 2) half 1's sums for half 0
-      if (WPR == 2) {
-        if (half == 1 && g == 0) {
-          xs[2 * cl] = a2;
-          xs[2 * cl + 1] = az;
-        }
-        __syncthreads();  // (every wave of the piece: none has left since the diagonal wait)
+      double* xs = lds + STEP_XS + 32 * (wave >> 1);  // half 1's sums for half 0
+      if (half == 1 && g == 0) {
+        xs[2 * cl] = a2;
+        xs[2 * cl + 1] = az;
       }
-      if (r < 8 && !late && half <= 0 && g == 0) {
-        if (WPR == 2) {
-          a2 = a2 + xs[2 * cl];
-          az = az + xs[2 * cl + 1];
-        }
+      __syncthreads();  // (every wave of the piece: none has left since the diagonal wait)
+      if (r < 8 && half == 0 && g == 0) {
         const size_t poff = ((size_t)p * nt + J) * Npad + (size_t)K * T + cb + cl;
-        s2p[poff] = a2;
-        szp[poff] = az;
+        s2p[poff] = a2 + xs[2 * cl];
+        szp[poff] = az + xs[2 * cl + 1];
       }
     }
   }
@@ -798,7 +781,7 @@ __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad
   if (!LT) return;
   // C (block b = ib (ib + 1) / 2 + jb waits for the regions of slabs ib and jb only; the diagonal
   // blocks also apply y_I -= L_IJ z_J for their slab's rows, from the same operands)
-  const unsigned ready = (ONE ? 0u : 16u) + (unsigned)WPR;
+  const unsigned ready = 2u;  // the region's two waves
   double* Aii = Lp + (size_t)I * T * ld + (size_t)I * T;
   for (int b = sidx * 8 + wave; b < 36; b += 8 * np) {
     int ib = 0;
@@ -889,17 +872,12 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
     static_assert(ED, "the all-tile split runs with the early diagonal factor (host: early_diag)");
     // (every tile of the launch: the single-piece ones, ROLE_WHOLE, finish the same way)
     const int np = split_all_pieces(J, w, nt, S);
-#define GPF_FLAT(lt, one)                                                                                          \
-  flat_piece<lt, one>(J, w, p, nt, Npad, Lp, Up, yp, s2p, szp, info + p, N, x, ls + (size_t)p * d, d, np, sidx, S2, \
-                      part, cnt, sflag, dflag, spins, lds)
-    if (w < nL) {
-      if (role == ROLE_PIECE) GPF_FLAT(true, false);
-      else GPF_FLAT(true, true);
-    } else {
-      if (role == ROLE_PIECE) GPF_FLAT(false, false);
-      else GPF_FLAT(false, true);
-    }
-#undef GPF_FLAT
+if (w < nL)
+      flat_piece<true>(J, w, p, nt, Npad, Lp, Up, yp, s2p, szp, info + p, N, x, ls + (size_t)p * d, d, np, sidx, S2, part,
+                       cnt, sflag, dflag, spins, lds);
+    else
+      flat_piece<false>(J, w, p, nt, Npad, Lp, Up, yp, s2p, szp, info + p, N, x, ls + (size_t)p * d, d, np, sidx, S2, part,
+                        cnt, sflag, dflag, spins, lds);
     return;
   }
   const Quad<T> qd;
