@@ -73,7 +73,9 @@ __host__ __device__ __forceinline__ void step_tile(int b, int P, int ntl, int gr
   p = (gi * grp + (r - w * gs)) * 8 + xcd;
 }
 
-enum { SPLIT_NONE = 0, SPLIT_ALL = 1, SPLIT_CRIT = 2 };
+// (r5: the critical-tile split SPLIT_CRIT = 2 of rounds 1-4 — off by default since round 2 and
+// slower again on B in r5, profiles/r5/ab_split_crit_B.txt — and its reduction tree were removed.)
+enum { SPLIT_NONE = 0, SPLIT_ALL = 1 };
 enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2, ROLE_DIAG = 3, ROLE_SYRK = 4, ROLE_LA = 5 };
 
 // Early diagonal factor (k_step<SPLIT, ED = 1>; the host chooses it for launches that leave
@@ -122,7 +124,7 @@ __host__ __device__ __forceinline__ int split_all_pieces(int J, int w, int nt, i
 // Workgroup b of a k_step<SPLIT> launch (grid: [P diagonal workgroups if ed] + [P SYRK workgroups
 // if sy] + P * sum_w split_all_pieces(J, w, nt, S) for SPLIT_ALL (tiles in order w = 0, 1, ..:
 // the critical tile first, then the L tiles, then the U tiles deepest first; pieces particle-
-// fastest), P*(nt-1) + P*(S-1) for SPLIT_CRIT, P*(nt-1) otherwise): its
+// fastest), P*(nt-1) otherwise): its
 // particle p, tile w, split index sidx, and whether it factors the diagonal block (ROLE_DIAG,
 // w = -1), reduces the next diagonal block (ROLE_SYRK, w = -1), runs the whole tile, one depth
 // range (piece sidx of S) of it, or nothing. The kernel and the host-side plan check
@@ -190,20 +192,10 @@ __host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt,
     p = b % P;
     sidx = b / P;  // (< np for every dispatched workgroup: gpf_plan_check)
     return np > 1 ? ROLE_PIECE : ROLE_WHOLE;
-  } else if (SPLIT == SPLIT_CRIT && b < P * S) {  // the S pieces of the critical tiles
-    p = b % P;
-    w = 0;
-    sidx = b / P;
   } else {  // particle-fastest order (grp = 0) puts the critical tiles w = 0 at b < P
-    step_tile(b - (SPLIT == SPLIT_CRIT ? P * (S - 1) : 0), P, nt - 1, grp, p, w);
+    step_tile(b, P, nt - 1, grp, p, w);
   }
-  const bool ltile = w < nt - 1 - J;
-  if (ltile) {
-    // L tiles split their depth-128J GEMM (only with the K tiles fused into k_step)
-    if (SPLIT == SPLIT_CRIT && w == 0 && J > 0) return ROLE_PIECE;
-    return (SPLIT != SPLIT_NONE && sidx > 0) ? ROLE_IDLE : ROLE_WHOLE;  // nothing to split at J = 0
-  }
-  return (SPLIT == SPLIT_CRIT && sidx > 0) ? ROLE_IDLE : ROLE_WHOLE;  // U tiles never split in CRIT
+  return ROLE_WHOLE;
 }
 
 // LDS of a k_step workgroup (doubles): the GEMM stages (DL_STAGE), the diagonal factor
@@ -289,45 +281,10 @@ __device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, con
 }
 
 // ----------------------------------------------------------------------------
-// Split-K for launches with few tiles (a single particle: the prediction path, or small
-// swarms): the streamed GEMM of a tile is cut into S depth ranges, one workgroup ("piece")
-// each, and the S partial products are summed by a binary tree of hand-offs: at level l the
-// pieces pair up by node (c = s >> l, sibling c ^ 1); each takes a ticket on the pair's counter;
-// the first to arrive stores its node sum to the node's slot, raises the pair's ready flag and
-// leaves; the second waits for that flag (the first is running: it took its ticket), adds the
-// sibling's slot and carries the pair up; the last one standing holds the whole sum in its
-// accumulators and finishes the tile. Per level the chain (the second arriver) pays a ticket and
-// a 128 KiB read, not also a store and its drain (round 3: the tree sits on the prediction's
-// critical path once the pieces are balanced). IEEE addition commutes, so a node's sum does not
-// depend on which sibling arrived last: results are deterministic.
-// Hand-off (the memory-model argument): node sums are stored write-through (agent-scope relaxed
-// atomic stores, `sc1`: the line goes to memory, no L2 write-back fence, which on gfx950 would
-// write back every dirty line of the XCD's L2 — ~10-100 us here), every wave drains them
-// (s_waitcnt vmcnt(0)) before the barrier that precedes the ready flag, and the second arriver
-// does an agent-scope acquire (L1/L2 invalidate) after seeing the flag, before reading the
-// sibling's slot, which may have been written from another XCD. The second arriver resets the
-// pair's ticket and flag for the next launch. The wait is bounded like wait_diag (`spins`; on
-// timeout info gets bit 2 and the piece gives up, so the host reports the error).
-// seed(acc) (SEEDED: piece 0 only) starts piece 0's accumulator instead of zero: the L tiles seed
-// it with their covariance tile A_IJ, so the finisher does not compute it after the pieces, on
-// the critical path; piece 0 takes SEED_CH fewer chunks for it (r4: the seed cost it ~11 us,
-// and as the carrier of every level it reached, the whole tree waited for it).
-// (r4) Node sums are kept in the accumulators' own layout (wave, register pair, lane: 16-B
-// accesses, 1 KiB per wave instruction) instead of the row-major tile (8-B accesses): nothing but
-// the tree reads the slots. Prediction factor 2.99 -> 2.78-2.83 ms with both
-// (profiles/r4/ab_split_tree.txt).
-// ----------------------------------------------------------------------------
-// (A radix-4 tree — groups of up to 4 nodes, the last arriver forming ((n0 + n1) + (n2 + n3)),
-// bitwise these sums with half the levels — measured slower: factor 3.45 -> 3.73 ms, the
-// carrier's three 128 KiB reads per level cost more than the saved hand-offs;
-// profiles/r3s2/ab_split_tree_radix.txt.)
-// (sc1 loads of the sibling's node sum in place of the acquire: within noise; 4 or 8 row blocks of
-// it read per scheduling group instead of 2: slower; profiles/r4/ab_split_tree.txt.)
-constexpr int SEED_CH = 4;     // split_part: chunks of GEMM piece 0's covariance seed stands for
-constexpr int TREE_BATCH = 2;  // row blocks of the sibling's node sum read per scheduling group
-constexpr int SPLIT_TREE = 80;              // tickets per split tile: pair (level l < 5, pair k < 16) at l * 16 + k
-constexpr int SPLIT_CNT = 2 * SPLIT_TREE;   // + the pairs' ready flags at SPLIT_TREE + l * 16 + k
-
+// Split-K pieces (SPLIT_ALL): piece 0 of an L tile seeds its partial with the covariance tile A_IJ
+// (the unsplit path's accumulator seed) and takes SEED_CH fewer chunks for it, so that it ends its
+// GEMM with the others (r4: the seed cost it ~11 us).
+constexpr int SEED_CH = 4;  // chunks of GEMM piece 0's covariance seed stands for
 // One piece's partial GEMM: piece boundaries over nch + e chunks, the first e of them standing
 // for piece 0's seed (its covariance tile costs about SEED_CH chunks of GEMM), so that the seeded
 // piece ends its GEMM with the others.
@@ -368,78 +325,6 @@ __device__ __forceinline__ void store_node(const Acc<T>& acc, double* slot, cons
         __builtin_amdgcn_raw_buffer_store_b128(q4, ws, qd.lane * 16, wb + ((mi * Acc<T>::MBC + ni) * 2 + h) * 1024,
                                                16);  // sc1: write-through
       }
-}
-
-template <bool NN, bool NEG, bool SEEDED = false, typename Seed>
-__device__ __forceinline__ bool split_part(Acc<T>& acc, const double* Ap, int lda, const double* Bp, int ldb, int nch, int S,
-                           int s, double* __restrict__ pt, unsigned* __restrict__ ct, double* smem,
-                           const Quad<T>& qd, int* flag, int* info, int spins, Seed seed, int J) {
-  split_gemm<NN, NEG, SEEDED>(acc, Ap, lda, Bp, ldb, nch, S, s, smem, qd, seed);
-#ifdef GPF_WG_TRACE
-  {
-    const int tid = threadIdx.x;
-    GPF_PHASE(3);  // (trace build) this piece's GEMM done, before the reduction tree
-  }
-#else
-  (void)J;
-#endif
-  for (int l = 0; (1 << l) < S; ++l) {
-    const int c = s >> l, sib = c ^ 1;
-    if ((sib << l) >= S) continue;  // no sibling range at this level: go up alone
-    unsigned* tk = ct + l * 16 + (c >> 1);
-    unsigned* rdy = ct + SPLIT_TREE + l * 16 + (c >> 1);
-    __syncthreads();  // (the previous level's reads of *flag are done)
-    if (threadIdx.x == 0) *flag = (int)__hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (*flag == 0) {  // first: publish the node sum, then the sibling carries the pair on
-      store_node(acc, pt + (size_t)(c << l) * T * T, qd);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its part of the node sum
-      __syncthreads();
-      if (threadIdx.x == 0) __hip_atomic_store(rdy, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-    __syncthreads();  // (every wave has read *flag)
-    if (threadIdx.x == 0) {
-      int n = 0, late = 0;
-      while (__hip_atomic_load(rdy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-        if (n++ >= spins) {
-          __hip_atomic_fetch_or(info, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          late = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      if (!late) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        __hip_atomic_store(rdy, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      *flag = late;
-    }
-    __syncthreads();
-    if (*flag) return false;  // timed out: the host reports it
-    // the sibling's node sum through a buffer descriptor: one 32-bit per-lane offset and the
-    // element displacements in soffset (64-bit per-element addresses were hoisted out of the tree
-    // loop and spilled)
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(pt + (size_t)(sib << l) * T * T), 0, T * T * 8,
-                                                      0x00020000);
-    const int wb = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * NODE_WAVE;
-#pragma unroll
-    for (int mi = 0; mi < Acc<T>::MBR; ++mi) {
-#pragma unroll
-      for (int ni = 0; ni < Acc<T>::MBC; ++ni)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const auto q4 = __builtin_amdgcn_raw_buffer_load_b128(rs, qd.lane * 16, wb + ((mi * Acc<T>::MBC + ni) * 2 + h) * 1024, 0);
-          const unsigned long long u0 = (unsigned long long)q4[0] | ((unsigned long long)q4[1] << 32),
-                                   u1 = (unsigned long long)q4[2] | ((unsigned long long)q4[3] << 32);
-          acc.v[mi][ni][2 * h] = acc.v[mi][ni][2 * h] + __builtin_bit_cast(double, u0);
-          acc.v[mi][ni][2 * h + 1] = acc.v[mi][ni][2 * h + 1] + __builtin_bit_cast(double, u1);
-        }
-      if ((mi % TREE_BATCH) == TREE_BATCH - 1) __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  return true;
 }
 
 // Consumer side of the early diagonal factor: wait until the launch's diagonal workgroup of this
@@ -496,7 +381,7 @@ __device__ __forceinline__ bool wait_diag(const int* flag, int J, int* info, int
 constexpr int FLAT_CNT = 16;  // [0] partials stored; [1 + r]: the waves that finished region r of an L tile
                               // (its phase-C operands stored)
 __host__ __device__ __forceinline__ int split_cnt_stride(int nt) {  // counter words per split tile and particle
-  return SPLIT_CNT > FLAT_CNT * nt ? SPLIT_CNT : FLAT_CNT * nt;
+  return FLAT_CNT * nt;
 }
 // Quad<128>::cb / 16 of wave r: the column slab held in wave region r of a slot (an involution, so
 // also the region of slab s)
@@ -893,16 +778,7 @@ if (w < nL)
     Acc<T> acc;
     // D = C^T = A_JI - L_J,<J L_I,<J^T (accumulator seeded with the covariance tile, A operand
     // negated through the MFMA modifier)
-    if (SPLIT == SPLIT_CRIT && role == ROLE_PIECE) {
-      // split-K: partial GEMMs, the last workgroup to arrive finishes the tile; piece 0 seeds
-      // its partial with the covariance tile (the unsplit path's accumulator seed)
-      double* pt = part + (size_t)(p * (nt - 1) + w) * S2 * T * T;
-      if (!split_part<false, true, true>(acc, Lp + (size_t)J * T * ld, Npad, Lp + (size_t)I * T * ld, Npad,
-                                         J * T / DL_KC, S, sidx, pt, cnt + (size_t)(p * (nt - 1) + w) * split_cnt_stride(nt), lds,
-                                         qd, sflag, info + p, spins,
-                                         [&](Acc<T>& a) { cov_tile_acc(a, qd, x, lp, d, N, J, I, lds); }, J))
-        return;  // (the finisher's accumulators hold D)
-    } else if (SPLIT == SPLIT_NONE && ED && (la & 2) && I == J + 1) {
+    if (SPLIT == SPLIT_NONE && ED && (la & 2) && I == J + 1) {
       // look-ahead seed: launch J-1 left this tile's GEMM over its first la_chunks(J-1) chunks (cov
       // seed included); the rest follows — the same MFMAs in the same order
       const int k0 = la_chunks(J - 1) * DL_KC;  // where launch J-1's look-ahead stopped
@@ -1013,10 +889,9 @@ if (w < nL)
   }
 }
 
-// SPLIT: SPLIT_ALL cuts every tile (launches with few tiles), SPLIT_CRIT only the critical-path
-// tile I = J+1 of each particle (launches that leave slots idle: its S pieces are dispatched
-// first, ahead of the unsplit tiles); SPLIT_NONE carries no split code at all, so its register
-// allocation is that of the plain schedule.
+// SPLIT: SPLIT_ALL cuts every tile (launches with few tiles; always with the early diagonal
+// factor, ED = 1); SPLIT_NONE carries no split code at all, so its register allocation is that of
+// the plain schedule.
 template <int SPLIT, int ED>
 __global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_step(int J, int nt, int Npad, double* __restrict__ Lb,
                                                   double* __restrict__ Ub, double* __restrict__ yb,

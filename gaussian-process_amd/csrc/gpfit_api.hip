@@ -343,7 +343,7 @@ static int step_group(int pc) {
 }
 
 // Split-K factor of the block-column launches: launches with at most 64 tiles (a single
-// particle: the prediction path) cut every tile's GEMM into S depth ranges (gpf::split_part), S
+// particle: the prediction path) cut every tile's GEMM into S depth ranges (gpf::flat_piece), S
 // filling ~512 workgroup slots. Measured (profiles/r1/split_k_ab.txt): single-particle factor at
 // N=4096 11.3 -> 9.9 ms with S=16 (7.4 ms since the partials are stored write-through, with no
 // release fence); config B (224 tiles, S=2) 21.3k -> 14.3k evals/s with the fence, hence the
@@ -451,33 +451,6 @@ static int wait_spins() {
   return n;
 }
 
-// Critical-tile split of block-column launch J (gpf::SPLIT_CRIT), for launches that leave
-// workgroup slots idle (small N: the launch time is the latency of the tile I = J+1, which runs
-// the depth-128J GEMM, the look-ahead update and the next diagonal factor in sequence): that
-// tile's GEMM is cut into S depth ranges run by S workgroups dispatched ahead of the rest.
-// Needs the particle-fastest tile order (grp = 0). pc: the particles of all concurrent groups
-// (they share the 512 workgroup slots). Pieces of at least 16 16-deep chunks: shorter ones lose
-// more to the partial round trip than they save (A/B, profiles/r1/split_crit_ab.txt: N=1024
-// P=32 +2.4%, -5..-12% with 8-chunk pieces; N=2048 P=32 +9%). Off by default since the end of
-// round 2: with the early diagonal factor these launches wait for the diagonal block, not for
-// the critical tile's GEMM, and the pieces' hand-offs only cost (same box, profiles/r2/
-// split_crit_off_ab.txt: N=1024 P=32 +1.4% off, N=3072 P=16 +3.0% off, N=1536/2048 P=32 within
-// 0.6%). GPF_SPLIT_CRIT = maximum S (default 1 = off; 4 was the round-1 default),
-// GPF_SPLIT_CRIT_MIN = minimum chunks per piece.
-static int split_crit(int pc, int nt, int J, int grp, int S_all) {
-  // the last launch (J = nt-1) has no L tiles: its w = 0 is a U tile, which never splits
-  if (S_all > 1 || grp > 0 || J == 0 || J >= nt - 1 || nt < 4) return 1;
-  // + the diagonal and the SYRK workgroups
-  const int slots = 512, tiles = pc * (nt - 1) + (early_diag(pc, nt) ? pc : 0) + (defer_syrk() && J <= nt - 2 ? pc : 0);
-  int S = 1, minch = 16;
-  if (const char* s = getenv("GPF_SPLIT_CRIT")) S = std::max(1, std::min(32, atoi(s)));
-  if (const char* s = getenv("GPF_SPLIT_CRIT_MIN")) minch = std::max(2, atoi(s));
-  const int nch = J * T / gpf::DL_KC;
-  S = std::min(S, std::max(1, nch / minch));
-  while (S > 1 && tiles + pc * (S - 1) > slots) --S;
-  return S;
-}
-
 static int ensure_split(gpf_ctx* c, int tiles, int S) {
   const size_t pb = (size_t)tiles * S * T * T * 8, cb = (size_t)tiles * gpf::split_cnt_stride(c->nt) * 4;
   if (pb > c->part_cap) {
@@ -505,7 +478,7 @@ static int ensure_split(gpf_ctx* c, int tiles, int S) {
 // Split-K plan of a factorisation of pc particles: S (all tiles) and the largest factor any
 // launch uses; the partial buffers are sized for it. run_factor calls this before it forks
 // the group streams. The graph path (N <= 128 * GRAPH_NT_MAX) captures run_factor, but
-// split_k and split_crit never split below nt = 4, so nothing is allocated during a capture
+// split_k never splits below nt = 4, so nothing is allocated during a capture
 // (static_assert below).
 static void split_sizes(int pc, int nt, int& S, int& Smax) {
   const int ng = num_groups(pc, nt);
@@ -523,7 +496,6 @@ static void split_sizes(int pc, int nt, int& S, int& Smax) {
     }
     Smax = std::max(Smax, 2);
   }
-  for (int J = 1; S == 1 && J < nt; ++J) Smax = std::max(Smax, split_crit(pc, nt, J, step_group(gmax), S));
 }
 
 static int split_plan(gpf_ctx* c, int pc, int& S, int& Smax) {
@@ -558,17 +530,16 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
       l.p0 = (int)((long long)pc * g / ng);
       l.gc = (int)((long long)pc * (g + 1) / ng) - l.p0;
       l.grp = step_group(l.gc);
-      const int Sc = split_crit(pc, nt, J, l.grp, S);
-      l.S = S > 1 ? split_all_target(l.gc, nt, J) : Sc;
-      l.S2 = S > 1 ? Smax : l.S;
-      l.split = S > 1 ? gpf::SPLIT_ALL : Sc > 1 ? gpf::SPLIT_CRIT : gpf::SPLIT_NONE;
+      l.S = S > 1 ? split_all_target(l.gc, nt, J) : 1;
+      l.S2 = S > 1 ? Smax : 1;
+      l.split = S > 1 ? gpf::SPLIT_ALL : gpf::SPLIT_NONE;
       l.ed = ed ? 1 : 0;
       l.defer = (S == 1 && defer_syrk()) ? 1 : 0;  // the all-tile split keeps the per-tile look-ahead
       l.sy = (l.defer && J >= 1 && J <= nt - 2) ? 1 : 0;
       // look-ahead: launch J-1 of this group must have run unsplit too (its LA workgroups)
       const bool la_ok = look_ahead(pc, nt) && l.ed && l.split == gpf::SPLIT_NONE;
-      const bool prev_none = J >= 1 && (S > 1 ? false : split_crit(pc, nt, J - 1, l.grp, S) <= 1);
-      const bool next_none = S > 1 ? false : split_crit(pc, nt, J + 1, l.grp, S) <= 1;
+      const bool prev_none = J >= 1 && S == 1;
+      const bool next_none = S == 1;
       l.la = ((la_ok && next_none && J >= 1 && J <= nt - 3) ? 1 : 0) | ((la_ok && prev_none && J >= 2 && J <= nt - 2) ? 2 : 0);
       // reordered dispatch: only where the first 3 gc workgroups (the light U tiles, which wait for
       // the diagonal workgroups behind them, and the SYRK workgroups) fit the chip's CUs at once
@@ -577,7 +548,7 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
               3 * l.gc <= 256) ? 1 : 0;
       int nall = 0;
       for (int w = 0; S > 1 && w < nt - 1; ++w) nall += gpf::split_all_pieces(J, w, nt, l.S);
-      l.grid = (S > 1 ? l.gc * nall : l.gc * (nt - 1) + l.gc * (Sc - 1)) + (l.ed ? l.gc : 0) + (l.sy ? l.gc : 0) +
+      l.grid = (S > 1 ? l.gc * nall : l.gc * (nt - 1)) + (l.ed ? l.gc : 0) + (l.sy ? l.gc : 0) +
                ((l.la & 1) && !l.sy ? l.gc : 0);  // (with SYRK workgroups the look-ahead rides on them)
       // one set of partial slots per group: groups run concurrently
       l.part_off = (size_t)l.p0 * (nt - 1) * Smax * T * T;
@@ -709,9 +680,8 @@ static int run_factor(gpf_ctx* c, int pc) {
     double* partg = l.split != gpf::SPLIT_NONE ? c->d_part + l.part_off : nullptr;
     unsigned* cntg = l.split != gpf::SPLIT_NONE ? c->d_cnt + l.cnt_off : nullptr;
     if (l.split == gpf::SPLIT_ALL && !ed) return bad_arg(c, "internal: all-tile split without the early diagonal factor");
-    const auto kern = l.split == gpf::SPLIT_ALL    ? gpf::k_step<gpf::SPLIT_ALL, 1>
-                      : l.split == gpf::SPLIT_CRIT ? (ed ? gpf::k_step<gpf::SPLIT_CRIT, 1> : gpf::k_step<gpf::SPLIT_CRIT, 0>)
-                                                   : (ed ? gpf::k_step<gpf::SPLIT_NONE, 1> : gpf::k_step<gpf::SPLIT_NONE, 0>);
+    const auto kern = l.split == gpf::SPLIT_ALL ? gpf::k_step<gpf::SPLIT_ALL, 1>
+                                                : (ed ? gpf::k_step<gpf::SPLIT_NONE, 1> : gpf::k_step<gpf::SPLIT_NONE, 0>);
     const int rc = launch_on(c, st, PC_PANEL, fl * gc, [&] {
       hipLaunchKernelGGL(kern, dim3(l.grid), dim3(gpf::STEP_NTH), 0, st, l.J, nt, Np, c->d_L + (size_t)p0 * ld * ld,
                          c->d_U + (size_t)p0 * ld * ld, c->d_yb + (size_t)p0 * ld, c->d_s2p + (size_t)p0 * nt * ld,
@@ -1419,8 +1389,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
   for (const StepLaunch& l : plan) {
     if (l.gc <= 0 || l.p0 < 0 || l.p0 + l.gc > pc || l.g < 0 || l.g >= ng)
       return plan_fail(msg, msg_len, "J=%d: bad group range p0=%d gc=%d g=%d", l.J, l.p0, l.gc, l.g);
-    if (l.S < 1 || (l.split == gpf::SPLIT_CRIT && (l.S < 2 || l.S > Smax || l.S2 != l.S)) ||
-        (l.split == gpf::SPLIT_NONE && (l.S != 1 || l.S2 != 1)) || (l.split == gpf::SPLIT_ALL && l.S2 != Smax))
+    if (l.S < 1 || (l.split == gpf::SPLIT_NONE && (l.S != 1 || l.S2 != 1)) || (l.split == gpf::SPLIT_ALL && l.S2 != Smax))
       return plan_fail(msg, msg_len, "J=%d g=%d: split kind %d with S=%d S2=%d", l.J, l.g, l.split, l.S, l.S2);
     if (l.split != gpf::SPLIT_NONE && Smax < 2)
       return plan_fail(msg, msg_len, "J=%d g=%d: split launch without split-K buffers (Smax=%d)", l.J, l.g, Smax);
@@ -1457,10 +1426,9 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     for (unsigned b = 0; b < l.grid; ++b) {
       int p = -1, w = -1, sidx = -1;
       const int role =
-          l.split == gpf::SPLIT_ALL    ? gpf::step_decode<gpf::SPLIT_ALL>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, 0, 0, p, w, sidx)
-          : l.split == gpf::SPLIT_CRIT ? gpf::step_decode<gpf::SPLIT_CRIT>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.sy, 0, p, w, sidx)
-                                       : gpf::step_decode<gpf::SPLIT_NONE>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.sy,
-                                                                           (l.la & 1) && !l.sy, p, w, sidx, l.ro);
+          l.split == gpf::SPLIT_ALL ? gpf::step_decode<gpf::SPLIT_ALL>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, 0, 0, p, w, sidx)
+                                    : gpf::step_decode<gpf::SPLIT_NONE>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.sy,
+                                                                        (l.la & 1) && !l.sy, p, w, sidx, l.ro);
       if (role == gpf::ROLE_DIAG) {  // one diagonal workgroup per particle, ahead of every tile of the launch
         // (reordered: right behind the particles' light U tiles, which wait for it, and the SYRK workgroups)
         if (!l.ed || p < 0 || p >= l.gc || (unsigned)p + (l.ro ? 2 * l.gc : 0) != b || diag[p]++)
@@ -1489,13 +1457,11 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
         if (pieces_of(w) < 2) return plan_fail(msg, msg_len, "J=%d block %u is a piece of an unsplit tile", l.J, b);
         ++piece[(size_t)t * l.S2 + sidx];
         // slots as k_step addresses them: S2 per tile
-        // counters: the reduction tree's SPLIT_CNT words of the tile, or the flat finish's FLAT_CNT
-        // words of (particle, launch, tile) inside the particle's ntl * cstride (gpf::flat_piece)
+        // counters: the flat finish's FLAT_CNT words of (particle, launch, tile) inside the
+        // particle's ntl * cstride (gpf::flat_piece)
         const size_t off = l.part_off + ((size_t)t * l.S2 + sidx) * T * T;
-        const size_t ci = l.split == gpf::SPLIT_ALL
-                              ? l.cnt_off + (size_t)p * ntl * cstride + ((size_t)l.J * ntl + w) * gpf::FLAT_CNT
-                              : l.cnt_off + (size_t)t * cstride;
-        const size_t cn = l.split == gpf::SPLIT_ALL ? gpf::FLAT_CNT : gpf::SPLIT_CNT;
+        const size_t ci = l.cnt_off + (size_t)p * ntl * cstride + ((size_t)l.J * ntl + w) * gpf::FLAT_CNT;
+        const size_t cn = gpf::FLAT_CNT;
         if (off + (size_t)T * T > part_cap || ci + cn > cnt_cap || l.S2 > gpf::SPLIT_MAXS ||
             ci + cn > l.cnt_off + (size_t)(p + 1) * ntl * cstride)
           return plan_fail(msg, msg_len, "J=%d tile %d piece %d outside the split buffers (S=%d S2=%d)", l.J, t, sidx, l.S,
@@ -1507,12 +1473,6 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
       }
       ++wgs;
     }
-    // the split-K reduction tree (gpf::split_part): every pair of node ranges has its own counter
-    for (int lv = 0; l.split != gpf::SPLIT_NONE && (1 << lv) < l.S2; ++lv)
-      for (int cn = 0; (cn << lv) < l.S2; cn += 2)
-        if (((cn + 1) << lv) < l.S2 && lv * 16 + (cn >> 1) >= gpf::SPLIT_TREE)
-          return plan_fail(msg, msg_len, "J=%d: split factor %d needs more than %d tree counters", l.J, l.S2,
-                           gpf::SPLIT_TREE);
     for (int q = 0; q < l.gc; ++q) {
       if (diag[q] != l.ed) return plan_fail(msg, msg_len, "J=%d particle %d: %d diagonal workgroups", l.J, q, diag[q]);
       diag_wgs += diag[q];

@@ -211,7 +211,7 @@ const char* gpf_build_info(void);
 
 /* Host-only structural check of the k_step dispatch plan (needs no device and no context):
  * for a chunk of pc particles with nt block columns, under the current GPF_GROUPS /
- * GPF_SPLIT_K / GPF_SPLIT_CRIT / GPF_SPLIT_CRIT_MIN / GPF_STEP_GROUP environment, builds the
+ * GPF_SPLIT_K / GPF_STEP_GROUP environment, builds the
  * launch list run_factor issues and decodes every workgroup of every launch with the kernel's
  * own decoder (gpf::step_decode). Checks that every (block column, particle, tile) is computed
  * exactly once (one whole-tile workgroup, or all S depth pieces exactly once, whose S arrivals

@@ -523,44 +523,13 @@ def test_split_k_matches_unsplit_and_oracle(ctx, monkeypatch, split):
     assert _rel(m2[2], mo) < RTOL_MU_SD and _rel(s2[2], so) < RTOL_MU_SD
 
 
-@pytest.mark.parametrize("split", [3, 8])
-def test_critical_tile_split_matches_unsplit_and_oracle(ctx, monkeypatch, split):
-    """Critical-tile split (gpf::SPLIT_CRIT: only the tile I = J+1 of each particle is cut into
-    depth ranges, its pieces dispatched ahead of the unsplit tiles) against the unsplit path and
-    the oracle. GPF_SPLIT_CRIT forces its factor; GPF_SPLIT_K=1 keeps the all-tile split off."""
-    N, d = 1000, 2
-    rng = np.random.default_rng(12)
-    x = rng.uniform(size=(d, N))
-    y = np.cos(5 * x[0]) * x[1] + 0.1 * rng.standard_normal(N)
-    e = rng.uniform(0.05, 0.2, size=N)
-    s, ex = ref_cpu.sigma_grid()
-    lo, hi = ref_cpu.search_bounds(x)
-    P = rng.uniform(0.1, 0.5, size=(12, d))
-    ctx.set_data(x, y, e)
-    ctx.set_grid(s, ex, lo, hi)
-    monkeypatch.setenv("GPF_SPLIT_K", "1")
-    monkeypatch.setenv("GPF_SPLIT_CRIT", "1")
-    l1, m1, s1 = ctx.eval_batch(P, want_mu_sd=True)
-    monkeypatch.setenv("GPF_SPLIT_CRIT", str(split))
-    monkeypatch.setenv("GPF_SPLIT_CRIT_MIN", "2")  # short pieces too, so the forced factor is used
-    l2, m2, s2 = ctx.eval_batch(P, want_mu_sd=True)
-    l3, m3, s3 = ctx.eval_batch(P, want_mu_sd=True)
-    np.testing.assert_array_equal(m2, m3)  # deterministic: partials summed in slot order
-    np.testing.assert_array_equal(s2, s3)
-    assert _rel(m2, m1) < 1e-10 and _rel(s2, s1) < 1e-10
-    assert _rel(l2, l1) < RTOL_LOSS
-    for i in (0, 7, 11):
-        mo, so = ref_cpu.GP_train_identity(x, y, e, P[i])
-        assert _rel(m2[i], mo) < RTOL_MU_SD and _rel(s2[i], so) < RTOL_MU_SD
-
-
 @pytest.mark.parametrize("N,d", [(700, 2), (1920, 3)])
-def test_default_critical_split_live_counts(ctx, monkeypatch, N, d):
-    """The critical-tile split at its round-1 default (GPF_SPLIT_CRIT=4: on whenever a launch
-    leaves slots idle, up to the last block column, whose w = 0 tile is a U tile and must not be
-    duplicated; off by default since round 2) across changing live-particle counts (sentinels
-    never run; buffers grow between batches): deterministic, and within 1e-10 of the unsplit
-    path (GPF_SPLIT_CRIT=1, the default)."""
+def test_all_tile_split_live_counts(ctx, monkeypatch, N, d):
+    """The all-tile split with its flat finish (gpf::flat_piece) forced on a multi-particle batch
+    (GPF_SPLIT_K=2; by default it runs for launches of <= 64 tiles only) across changing
+    live-particle counts (sentinels never run; buffers grow between batches): more workgroups than
+    CUs (at least 4 pieces per tile), deterministic, and within 1e-10 of the unsplit path.
+    (r5: replaces the critical-tile split's test; that split was removed.)"""
     rng = np.random.default_rng(N + d)
     x = rng.uniform(size=(d, N))
     y = np.sin(3 * x[0]) + 0.1 * rng.standard_normal(N)
@@ -575,15 +544,16 @@ def test_default_critical_split_live_counts(ctx, monkeypatch, N, d):
     for m in masks:
         Q = P.copy()
         Q[m, 0] = hi[0] + 1.0  # sentinels: outside the box
-        monkeypatch.setenv("GPF_SPLIT_CRIT", "4")
-        g = ctx.eval_batch(Q)
+        monkeypatch.setenv("GPF_SPLIT_K", "2")
+        g, gm, gs = ctx.eval_batch(Q, want_mu_sd=True)
         np.testing.assert_array_equal(g, ctx.eval_batch(Q))  # deterministic
-        monkeypatch.setenv("GPF_SPLIT_CRIT", "1")
-        w = ctx.eval_batch(Q)
-        monkeypatch.delenv("GPF_SPLIT_CRIT", raising=False)
-        np.testing.assert_array_equal(w, ctx.eval_batch(Q))  # the default is the unsplit path
+        monkeypatch.setenv("GPF_SPLIT_K", "1")
+        w, wm, ws = ctx.eval_batch(Q, want_mu_sd=True)
+        monkeypatch.delenv("GPF_SPLIT_K", raising=False)
         assert np.all(g[m] == 1e13)
-        assert _rel(g, w) < 1e-10
+        live = ~m
+        assert _rel(gm[live], wm[live]) < 1e-10 and _rel(gs[live], ws[live]) < 1e-10
+        assert _rel(g[live], w[live]) < RTOL_LOSS
         got.append(g)
     np.testing.assert_array_equal(got[0], got[3])
 
@@ -938,7 +908,7 @@ def test_early_diagonal_factor_matches_fused(ctx, monkeypatch, N, d, P):
     """The early diagonal factor (k_step<SPLIT, 1>: block J factored by extra workgroups at the
     start of launch J and handed to the tiles through a flag) against the fused factor at the end
     of the previous launch's critical tile: the same arithmetic, so bitwise equal scores, mean
-    and sd, on the critical-split (N=1000) and unsplit paths. The all-tile split (one particle:
+    and sd, on the unsplit paths (N=1000, 2049). The all-tile split (one particle:
     the prediction path) always runs the early factor (its flat finish waits for the diagonal
     block inside the launch), so there GPF_EARLY_DIAG=0 must change nothing: the factor itself
     bitwise equal. The deferred diagonal update (one
@@ -956,7 +926,6 @@ def test_early_diagonal_factor_matches_fused(ctx, monkeypatch, N, d, P):
     ctx.set_grid(s, ex, lo, hi)
     Q = rng.uniform(0.1, 0.5, size=(P, d))
     out = {}
-    monkeypatch.setenv("GPF_SPLIT_CRIT", "4")  # the critical-split path (off by default since round 2)
     for mode, ed, defer in (("fused", "0", "1"), ("fused_lookahead", "0", "0"), ("ed", "1", "1"),
                             ("ed_lookahead", "1", "0")):
         monkeypatch.setenv("GPF_EARLY_DIAG", ed)

@@ -1,10 +1,10 @@
 """Host-side enumeration of the k_step dispatch plan (no GPU needed).
 
 gpf_plan_check (include/gpfit.h) builds the launch list run_factor issues (num_groups,
-split_k, split_crit, step_group and the grid sizing in csrc/gpfit_api.hip) and decodes every
+split_k, step_group and the grid sizing in csrc/gpfit_api.hip) and decodes every
 workgroup of every launch with the kernel's own decoder (gpf::step_decode). Every
 (block column, particle, tile) must be computed exactly once: one whole-tile workgroup, or
-all S depth pieces exactly once (S arrivals on a zeroed counter elect exactly one finisher);
+all S depth pieces exactly once (the flat finish's counters of that tile);
 pieces must stay inside the split-K buffers and concurrent particle groups must not share
 partial slots or counters. This is the structural guard for races like the v14 duplicate of
 the last block column's w = 0 tile.
@@ -23,13 +23,11 @@ ENVS = [
     {"GPF_GROUPS": "2"}, {"GPF_GROUPS": "3"}, {"GPF_GROUPS": "4"},
     {"GPF_SPLIT_K": "2"}, {"GPF_SPLIT_K": "7"}, {"GPF_SPLIT_K": "16"},
     {"GPF_SPLIT_K": "7", "GPF_GROUPS": "3"},
-    {"GPF_SPLIT_CRIT": "3"}, {"GPF_SPLIT_CRIT": "8", "GPF_SPLIT_CRIT_MIN": "2"},
-    {"GPF_SPLIT_CRIT": "8", "GPF_SPLIT_CRIT_MIN": "2", "GPF_GROUPS": "2"},
     {"GPF_STEP_GROUP": "1"}, {"GPF_STEP_GROUP": "2", "GPF_GROUPS": "2"},
     {"GPF_EARLY_DIAG": "1"}, {"GPF_EARLY_DIAG": "0"},
-    {"GPF_EARLY_DIAG": "1", "GPF_SPLIT_CRIT": "8", "GPF_SPLIT_CRIT_MIN": "2", "GPF_GROUPS": "3"},
+    {"GPF_EARLY_DIAG": "1", "GPF_GROUPS": "3"},
     {"GPF_DEFER_SYRK": "0"}, {"GPF_DEFER_SYRK": "0", "GPF_EARLY_DIAG": "1"},
-    {"GPF_DEFER_SYRK": "0", "GPF_EARLY_DIAG": "1", "GPF_SPLIT_CRIT": "8", "GPF_SPLIT_CRIT_MIN": "2", "GPF_GROUPS": "2"},
+    {"GPF_DEFER_SYRK": "0", "GPF_EARLY_DIAG": "1", "GPF_GROUPS": "2"},
     {"GPF_SPLIT_K_SLOTS": "512"}, {"GPF_SPLIT_K_SLOTS": "64", "GPF_SPLIT_K_MINCH": "1"},
     {"GPF_SPLIT_K": "3", "GPF_SPLIT_K_SLOTS": "1000", "GPF_SPLIT_K_MINCH": "1", "GPF_GROUPS": "2"},
     {"GPF_REORDER": "0"}, {"GPF_REORDER": "0", "GPF_EARLY_DIAG": "1"},  # r4: the reordered dispatch off
@@ -40,7 +38,7 @@ ENVS = [
 @pytest.fixture
 def env(monkeypatch):
     def apply(kv):
-        for k in ("GPF_GROUPS", "GPF_SPLIT_K", "GPF_SPLIT_CRIT", "GPF_SPLIT_CRIT_MIN", "GPF_STEP_GROUP", "GPF_EARLY_DIAG",
+        for k in ("GPF_GROUPS", "GPF_SPLIT_K", "GPF_STEP_GROUP", "GPF_EARLY_DIAG",
                   "GPF_DEFER_SYRK", "GPF_SPLIT_K_SLOTS", "GPF_SPLIT_K_MINCH", "GPF_PERSIST", "GPF_REORDER"):
             monkeypatch.delenv(k, raising=False)
         if kv and "GPF_PERSIST" not in kv:  # the launch-plan knobs: on the per-block-column launches
@@ -75,7 +73,7 @@ def test_every_tile_has_exactly_one_finisher(env, kv):
             assert st["syrk_workgroups"] == 0 or st["S"] == 1
             seen_split += st["split_tiles"] > 0
             seen_groups += st["groups"] > 1
-    if kv.get("GPF_SPLIT_K") or kv.get("GPF_SPLIT_CRIT") or not kv:
+    if kv.get("GPF_SPLIT_K") or not kv:
         assert seen_split, "the sweep never reached a split launch"
     if "GPF_GROUPS" in kv:
         assert seen_groups, "the sweep never reached a multi-group plan"
@@ -102,11 +100,8 @@ def test_default_plans_of_the_baseline_configs(env):
     e0 = gpfit.plan_check(16, 128)
     assert (e0["groups"], e0["diag_workgroups"], e0["syrk_workgroups"]) == (2, 0, 16 * 126)
     env({})
-    b = gpfit.plan_check(32, 8)             # config B: one group, no split (critical split off by default)
+    b = gpfit.plan_check(32, 8)             # config B: one group, no split
     assert b["groups"] == 1 and b["S"] == 1 and b["Smax"] == 1 and b["split_tiles"] == 0
-    env({"GPF_SPLIT_CRIT": "4"})            # ... and with the critical-tile split asked for
-    bs = gpfit.plan_check(32, 8)
-    assert bs["S"] == 1 and bs["Smax"] > 1 and bs["split_tiles"] > 0
     env({})
     one = gpfit.plan_check(1, 32)           # prediction: single particle, all tiles split
     # every tile in at least SPLIT_MINP (4) pieces, J = 0's zero-depth tiles included (the flat
