@@ -166,6 +166,8 @@ enum Tri : int {
   TRI_B_KGEC,   // B(k,c) = 0 for k < c   (B = U with U lower triangular in its first T rows)
   TRI_A_KLER,   // A(r,k) = 0 for k > r   (A = U lower triangular)
   TRI_C_LOWER,  // only C(r,c) with c <= r is ever read (symmetric rank-k update)
+  TRI_A_LAST,   // A's last 128 columns lower triangular by rows: A(r, K-128+c) = 0 for c > r
+                // (A = a row tile of U = L^-1 over columns [0, 128(t+1)): k_predict_vsq)
 };
 
 // does the 16x16x4 MFMA block (rows R0.., cols C0.., depth k..k+3) contribute?
@@ -417,6 +419,12 @@ __device__ __forceinline__ void gemm_stream_dl(Acc<128>& acc, const double* __re
     const int t1 = min(nch, slab);
     GPF_RUN(8, 0, t1);
     GPF_RUN(0, t1, nch);
+  } else if constexpr (TRI == TRI_A_LAST) {  // chunk c of the last 128 columns adds zeros to row blocks mi < c
+    // (at half-block granularity: the chunks c >= 4 run for mi >= 4 only; one run per chunk and M0
+    // spilled 12 VGPRs of the accumulators)
+    const int t0 = nch - 8;  // (K >= 128: at least one full block)
+    GPF_RUN(0, 0, t0 + 4);
+    GPF_RUN(4, t0 + 4, nch);
   } else {  // TRI_C_LOWER: only the row blocks mi >= slab of the output are ever read
     static_assert(TRI == TRI_C_LOWER, "known-zero pattern");
     switch (slab) {

@@ -496,8 +496,11 @@ __device__ __forceinline__ void flat_load_operand8(double (&a)[8], const double*
 // also y_I -= L_IJ z_J for their 16 rows (t ascending per lane, then the lane groups). The
 // operands stream in 4 batches of 8 k-steps, two in flight (32 k-steps of both operands at once
 // are 128 VGPRs: the compiler serialised their loads into several round trips).
-__device__ __forceinline__ void flat_syrk_block(double* Aii, size_t ld, const double* slot1, int ib, int jb, double* yi,
-                                                const double* zj) {
+// wait(): the block's regions are in (true: timed out — the block is abandoned); A_II's block,
+// which nothing else in the launch touches, is read before it, beside the wait.
+template <typename W>
+__device__ __forceinline__ bool flat_syrk_block(double* Aii, size_t ld, const double* slot1, int ib, int jb, double* yi,
+                                                const double* zj, W wait) {
   const int lane = threadIdx.x & 63, g = lane >> 4, cl = lane & 15;
   double* cp = launder(Aii + (size_t)(16 * ib + g) * ld + 16 * jb + cl);
   const int ra = region_slab(ib), rb = region_slab(jb);
@@ -505,6 +508,7 @@ __device__ __forceinline__ void flat_syrk_block(double* Aii, size_t ld, const do
   d4 acc;
 #pragma unroll
   for (int r = 0; r < 4; ++r) acc[r] = cp[(size_t)(4 * r) * ld];
+  if (wait()) return true;
   const auto zs = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(zj), 0, T * 8, 0x00020000);
   double yr = 0.0;
   double a[2][8], b[2][8];
@@ -534,6 +538,7 @@ __device__ __forceinline__ void flat_syrk_block(double* Aii, size_t ld, const do
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) cp[(size_t)(4 * r) * ld] = acc[r];
+  return false;
 }
 
 // One piece (sidx of np) of tile w of launch J under the flat finish (see above); LT: an L tile.
@@ -672,9 +677,11 @@ __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad
     int ib = 0;
     while ((ib + 1) * (ib + 2) / 2 <= b) ++ib;
     const int jb = b - ib * (ib + 1) / 2;
-    if (wave_wait(ca + 1 + region_slab(ib), ready, info, spins) || wave_wait(ca + 1 + region_slab(jb), ready, info, spins))
+    if (flat_syrk_block(Aii, ld, slot1, ib, jb, ib == jb ? yp + (size_t)I * T : nullptr, yp + (size_t)J * T, [&] {
+          return wave_wait(ca + 1 + region_slab(ib), ready, info, spins) ||
+                 wave_wait(ca + 1 + region_slab(jb), ready, info, spins);
+        }))
       return;
-    flat_syrk_block(Aii, ld, slot1, ib, jb, ib == jb ? yp + (size_t)I * T : nullptr, yp + (size_t)J * T);
   }
   GPF_PHASE(2);
 }

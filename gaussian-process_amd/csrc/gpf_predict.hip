@@ -28,8 +28,11 @@ __global__ __launch_bounds__(Geo<T>::NTH, 4) void k_predict_vsq(int Npad, const 
   const Quad<T> qd;
   Acc<T> acc;
   acc.zero();
-  // U is lower triangular: row tile t needs columns [0, (t+1) * 128)
-  gemm_stream_dl<true>(acc, U + (size_t)t * T * Npad, Npad, Ks + (size_t)q * T, ldks, (t + 1) * T, smem, qd);
+  // U is lower triangular: row tile t needs columns [0, (t+1) * 128), and in the last 128 of them
+  // row block mi only the chunks c <= mi add non-zeros (TRI_A_LAST skips the chunks c >= 4 for the
+  // row blocks mi < 4: 16 of the diagonal block's 64 chunk x row block MFMA groups, exact zeros; r5)
+  gemm_stream_dl<true, false, TRI_A_LAST>(acc, U + (size_t)t * T * Npad, Npad, Ks + (size_t)q * T, ldks, (t + 1) * T,
+                                          smem, qd);
   constexpr int MBR = Geo<T>::MBR;
   const double* zt = z + (size_t)t * T + (qd.lane >> 4);
   double half[2], zh[2];
