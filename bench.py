@@ -606,11 +606,13 @@ def main():
         achieved = fl / (prof["factor_wall_ms"] * 1e-3) / 1e12 if prof["factor_wall_ms"] > 0 else None
         timing = f"factorisation-phase wall over {groups} concurrent group streams (non-overlapping)"
     # practical ceiling: the same GEMM core alone on L-tile-shaped operands (gpf_gemm_bench,
-    # direct-to-LDS, N=4096-sized panels, depth 2048, 960 workgroups), on non-zero operand data
+    # direct-to-LDS, N=4096-sized panels, depth 1920, 1024 workgroups = two whole rounds of the
+    # 512 slots; r1-r5's 960 workgroups left 64 slots idle in the second round and read the core
+    # ~6% low per clock, profiles/r5/core_geometry.txt), on non-zero operand data
     # (r4: the MFMA's power depends on its operand bits — on zero operands the chip held ~2.39 GHz,
     # on real data ~2.09 GHz, profiles/r4/clock_probe_*.json), sustained for ~0.3 s so the clock
     # has settled (a 3-launch run starts below it)
-    core = ctx.gemm_bench(mode=2, npad=4096, particles=64, tiles=15, depth=2048, iters=300) \
+    core = ctx.gemm_bench(mode=2, npad=4096, particles=64, tiles=16, depth=1920, iters=300) \
         if (rank == 0 and N >= 2048) else None
     core_sclk = ctx.bench_clock() if core else None
     # this box's FP64 matrix ceiling: back-to-back independent v_mfma_f64_16x16x4 chains on every

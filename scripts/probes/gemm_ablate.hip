@@ -1,0 +1,164 @@
+// gemm_ablate.hip — where the streamed GEMM core (gpf_common.hip DenseRun, the k_step L-tile shape:
+// 128x128 output per 512-thread workgroup, 2 workgroups per CU, 16-deep chunks) loses its ~11% per
+// clock against the register-only MFMA loop. Each variant removes one part of the chunk loop:
+//   0  gemm_stream_dl itself
+//   1  the same loop written out here (sanity: must match 0)
+//   2  no global->LDS transfers (LDS holds the first two chunks; barrier and operand reads kept)
+//   3  no transfers, no barrier (operand reads + MFMAs only)
+//   4  transfers + barrier, no operand reads (operands read once before the loop)
+//   5  MFMAs only
+//   6  as 1 with the k-step's operands read one k-step ahead (two register sets)
+// Per variant: TF/s, the shader clock held (s_memtime over s_memrealtime) and the fraction of
+// 128 flop/CU/clk at that clock. Operands are hashed values in [-1, 1) (the clock depends on them).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -mllvm --amdgpu-mfma-vgpr-form \
+//     scripts/probes/gemm_ablate.hip -o gemm_ablate && ./gemm_ablate [tiles] [depth] [shared]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#include "../../gaussian-process_amd/csrc/gpf_common.hip"
+#include "../../gaussian-process_amd/csrc/gpf_factor.hip"
+
+#define CK(x)                                                                          \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) {                                                            \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                         \
+    }                                                                                  \
+  } while (0)
+
+using namespace gpf;
+using DR = DenseRun<false, true, 2>;
+
+// variant 6's chunk: operands of k-step s+1 read before the MFMAs of k-step s
+template <int BUF>
+__device__ __forceinline__ void mma_ahead(const DR& dr, Acc<128>& acc, const double* smem) {
+  const char* sb = (const char*)smem + BUF * DL_BUF * 8;
+  double a0[8], b0, a1[8], b1;
+  dr.reads<0>(sb, 0, a0, b0);
+  dr.reads<0>(sb, 1, a1, b1);
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) acc.v[mi][0] = mfma_neg_a(a0[mi], b0, acc.v[mi][0]);
+  dr.reads<0>(sb, 2, a0, b0);
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) acc.v[mi][0] = mfma_neg_a(a1[mi], b1, acc.v[mi][0]);
+  dr.reads<0>(sb, 3, a1, b1);
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) acc.v[mi][0] = mfma_neg_a(a0[mi], b0, acc.v[mi][0]);
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) acc.v[mi][0] = mfma_neg_a(a1[mi], b1, acc.v[mi][0]);
+}
+
+template <int V, int BUF>
+__device__ __forceinline__ void body(const DR& dr, Acc<128>& acc, const double* A, const double* B, int ld, int t,
+                                     int nch, double* smem, const double (&ra)[8], double rb) {
+  constexpr bool LOADS = V == 1 || V == 4 || V == 6, BAR = V == 1 || V == 2 || V == 4 || V == 6;
+  if (LOADS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (BAR) __syncthreads();
+  else asm volatile("" ::: "memory");  // (keeps the operand reads of a chunk in their chunk: no spills)
+  if (LOADS && t + 1 < nch) dr.issue<BUF ^ 1>(A, B, ld, t + 1, smem);
+  if constexpr (V == 4 || V == 5) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) acc.v[mi][0] = mfma_neg_a(ra[mi], rb, acc.v[mi][0]);
+  } else if constexpr (V == 6) {
+    mma_ahead<BUF>(dr, acc, smem);
+  } else {
+    dr.mma<BUF, 0>(acc, smem);
+  }
+}
+
+template <int V>
+__global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_abl(const double* __restrict__ L, int ld, int D,
+                                                                       int shared, double* __restrict__ C,
+                                                                       unsigned long long* clk) {
+  __shared__ __attribute__((aligned(16))) double smem[2 * DL_BUF];
+  __shared__ unsigned long long cs[2];
+  const ClockSpan span(cs);
+  span.start(clk);
+  const int b = blockIdx.x;
+  const double* A = uniform_ptr(L);
+  const double* B = uniform_ptr(L + (size_t)(shared ? 1 : 1 + b) * T * ld);
+  const Quad<T> qd;
+  Acc<T> acc;
+  acc.zero();
+  if constexpr (V == 0) {
+    gemm_stream_dl<false, true>(acc, A, ld, B, ld, D, smem, qd);
+  } else {
+    const int nch = D / DL_KC, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const DR dr(qd, ld, ld, wave);
+    dr.issue<0>(A, B, ld, 0, smem);
+    dr.issue<1>(A, B, ld, 1, smem);  // both buffers hold real operands (variants without transfers)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __syncthreads();
+    double ra[8], rb;
+    dr.reads<0>((const char*)smem, 0, ra, rb);
+#pragma unroll 1
+    for (int t = 0; t + 1 < nch; t += 2) {
+      body<V, 0>(dr, acc, A, B, ld, t, nch, smem, ra, rb);
+      body<V, 1>(dr, acc, A, B, ld, t + 1, nch, smem, ra, rb);
+    }
+    __syncthreads();
+  }
+  acc.store(qd, C + (size_t)b * T * T, T);
+  span.stop(clk);
+}
+
+template <int V>
+void run(const char* name, int W, int D, int shared, const double* L, int ld, double* C, unsigned long long* clk,
+         double mhz_ref) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  hipLaunchKernelGGL(k_abl<V>, dim3(W), dim3(STEP_NTH), 0, 0, L, ld, D, shared, C, nullptr);
+  CK(hipMemset(clk, 0, 16));
+  const int iters = 20;
+  CK(hipEventRecord(e0));
+  for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(k_abl<V>, dim3(W), dim3(STEP_NTH), 0, 0, L, ld, D, shared, C, clk);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  unsigned long long h[2];
+  CK(hipMemcpy(h, clk, 16, hipMemcpyDeviceToHost));
+  const double mhz = (double)h[0] / (double)h[1] * mhz_ref;
+  const double tf = 2.0 * T * T * (double)D * W * iters / (ms * 1e-3) / 1e12;
+  const double frac = tf * 1e12 / (128.0 * 256 * mhz * 1e6);
+  printf("%d %-44s %6.1f TF/s at %5.0f MHz = %.3f of 128 flop/CU/clk\n", V, name, tf, mhz, frac);
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+}
+
+int main(int argc, char** argv) {
+  const int W = argc > 1 ? atoi(argv[1]) : 1024, D = argc > 2 ? atoi(argv[2]) : 2048, shared = argc > 3 ? atoi(argv[3]) : 0;
+  if (D % 256 || D < 256 || W < 1 || W > 4096) {
+    fprintf(stderr, "bad args\n");
+    return 1;
+  }
+  const int ld = D, rows = (shared ? 2 : W + 1) * T;
+  double *L, *C;
+  unsigned long long* clk;
+  CK(hipMalloc(&L, (size_t)rows * ld * 8));
+  CK(hipMalloc(&C, (size_t)W * T * T * 8));
+  CK(hipMalloc(&clk, 16));
+  hipLaunchKernelGGL(k_fill_hash, dim3(4096), dim3(NTHR), 0, 0, L, (long long)rows * ld);
+  CK(hipDeviceSynchronize());
+  printf("tiles %d depth %d %s B panels\n", W, D, shared ? "one shared (L2-resident)" : "distinct (HBM)");
+  const double ref = 100.0;  // s_memrealtime: 100 MHz
+  run<0>("gemm_stream_dl", W, D, shared, L, ld, C, clk, ref);
+  run<1>("same loop here", W, D, shared, L, ld, C, clk, ref);
+  run<2>("no transfers", W, D, shared, L, ld, C, clk, ref);
+  run<3>("no transfers, no barrier", W, D, shared, L, ld, C, clk, ref);
+  run<4>("transfers + barrier, no operand reads", W, D, shared, L, ld, C, clk, ref);
+  run<5>("MFMAs only", W, D, shared, L, ld, C, clk, ref);
+  run<6>("as 1, operands read a k-step ahead", W, D, shared, L, ld, C, clk, ref);
+  run<0>("gemm_stream_dl again (the first run starts cold)", W, D, shared, L, ld, C, clk, ref);
+  CK(hipFree(L));
+  CK(hipFree(C));
+  CK(hipFree(clk));
+  printf("PROBE OK\n");
+  return 0;
+}
