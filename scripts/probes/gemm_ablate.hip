@@ -361,6 +361,12 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   printf("tiles %d depth %d %s B panels\n", W, D, shared ? "one shared (L2-resident)" : "distinct (HBM)");
   const double ref = 100.0;  // s_memrealtime: 100 MHz
+  if (getenv("ABL_PMC")) {  // (a short run for rocprofv3 --pmc: the single-output loop and the 16-wave pair only)
+    run<1>("same loop here", W, D, shared, L, ld, C, clk, ref);
+    run_dual(W, D, shared, L, ld, C, clk, ref, 16);
+    printf("PROBE OK\n");
+    return 0;
+  }
   run<0>("gemm_stream_dl", W, D, shared, L, ld, C, clk, ref);
   run<1>("same loop here", W, D, shared, L, ld, C, clk, ref);
   run<2>("no transfers", W, D, shared, L, ld, C, clk, ref);
