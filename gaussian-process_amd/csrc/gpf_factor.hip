@@ -206,6 +206,12 @@ constexpr int STEP_XS = STEP_ZJ + T;  // flat finish: the U-tile column sums one
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 constexpr int STEP_LDS = cmax(cmax(DL_STAGE, DB_LDS), cmax(STEP_XS + 64, 2 * DMAX * T + 2 * T));
 static_assert(STEP_LDS * 8 <= 80 * 1024, "two k_step workgroups per CU (160 KiB of LDS)");
+// k_step<SPLIT_ALL> (one workgroup per CU: the launch budget is the CU count): the flat finish's
+// reduction gets its own area behind the staged U_JJ, so U_JJ can be staged before the reduction
+// (flat_piece)
+constexpr int FLAT_RB = STEP_XS + 64;                 // 2 regions x 16 units x 128 doubles
+constexpr int STEP_LDS_FLAT = FLAT_RB + 2 * 2048;
+static_assert(STEP_LDS_FLAT >= STEP_LDS && STEP_LDS_FLAT * 8 <= 160 * 1024 && (FLAT_RB * 8) % 16 == 0, "flat LDS");
 constexpr int STEP_NTH = Geo<T>::NTH;     // 512 threads: 8 waves, 128x16 per wave
 static_assert(STEP_NTH == DNTH, "the fused diagonal runs on the step workgroup");
 
@@ -581,6 +587,21 @@ __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad
   const int r = sidx + np * (wave >> 1);  // the region this wave finishes (if < 8)
   double* slot1 = pt + (size_t)T * T;
   if (sidx < 8) {
+    double* zj = lds + STEP_ZJ;
+    // (r5) if the diagonal block is already published once this piece's partial is in (the deep
+    // launches: the diagonal factor ends before the GEMMs), U_JJ and z_J are staged while the other
+    // pieces' partials arrive, and the reduction goes to its own area (FLAT_RB); otherwise the
+    // reduction runs first, as it can before the diagonal block exists
+    if (threadIdx.x == 0) *sflag = __hip_atomic_load(dflag + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= J;
+    __syncthreads();
+    const bool early = *sflag != 0;
+    __syncthreads();  // (sflag is the waits' broadcast word)
+    double* rb = early ? lds + FLAT_RB : lds;
+    if (early) {
+      if (wait_diag(dflag + p, J, info, spins, sflag)) return;  // (published: one poll and the acquire)
+      if (!LT && tid < T) zj[tid] = yp[J * T + tid];
+      tri_to_lds(Up + (size_t)J * T * ld + (size_t)J * T, ld, lds);  // (its barrier also publishes z_J)
+    }
     if (group_wait(ca, (unsigned)np, info, spins, sflag)) return;
     // R, local: the piece's 8 waves sum its regions' 16 1-KiB units each over the np slots (slot
     // order) into LDS, where the region's two waves pick their operand up — no store, drain,
@@ -589,15 +610,16 @@ __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad
     for (int i = wave; i < 16 * nr; i += 8) {
       const int k = i >> 4, j = i & 15;
       const d2 sum = flat_sum_unit(pt, np, (sidx + np * k) * 16 + j);
-      *reinterpret_cast<d2*>(lds + k * 2048 + j * 128 + qd.lane * 2) = sum;
+      *reinterpret_cast<d2*>(rb + k * 2048 + j * 128 + qd.lane * 2) = sum;
     }
     __syncthreads();
     GPF_PHASE(0);
-    if (r < 8) flat_lds_region(acc, lds + ((r - sidx) / np) * 2048);
-    double* zj = lds + STEP_ZJ;
-    if (wait_diag(dflag + p, J, info, spins, sflag)) return;  // U_JJ, z_J (its barrier: the region reads done)
-    if (!LT && tid < T) zj[tid] = yp[J * T + tid];
-    tri_to_lds(Up + (size_t)J * T * ld + (size_t)J * T, ld, lds);  // (its barrier also publishes z_J)
+    if (r < 8) flat_lds_region(acc, rb + ((r - sidx) / np) * 2048);
+    if (!early) {
+      if (wait_diag(dflag + p, J, info, spins, sflag)) return;  // U_JJ, z_J (its barrier: the region reads done)
+      if (!LT && tid < T) zj[tid] = yp[J * T + tid];
+      tri_to_lds(Up + (size_t)J * T * ld + (size_t)J * T, ld, lds);  // (its barrier also publishes z_J)
+    }
     const bool outer = half == 0;  // this wave's output row blocks: P = 0, 3 (outer) or 1, 2
     const int cb = 16 * region_slab(r < 8 ? r : 0);
     if (LT) {
@@ -922,7 +944,7 @@ __global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_step(int J, i
     g_wg_trace[J][blockIdx.x][2] = ((unsigned long long)xcc << 32) | hw;
   }
 #endif
-  __shared__ __attribute__((aligned(16))) double lds[STEP_LDS];
+  __shared__ __attribute__((aligned(16))) double lds[SPLIT == SPLIT_ALL ? STEP_LDS_FLAT : STEP_LDS];
   __shared__ int sflag;
   int p, w, sidx;
   const int role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, SPLIT != SPLIT_ALL && sy,
