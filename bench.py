@@ -666,7 +666,12 @@ def main():
         ftf_min = -float(comm.allreduce([-ftf], op="max")[0])
     build_gbs = (prof["build_bytes"] / (prof["build_ms"] * 1e-3) / 1e9) if prof["build_ms"] > 0 else None
     breakdown = {k: prof[k] for k in ("panel_ms", "diag_ms", "build_ms", "loss_ms", "factor_wall_ms")}
-    breakdown["k_build_cov_GBps"] = build_gbs
+    # k_build_cov writes only the 128-wide diagonal blocks (3 nt 64x64 tiles per particle): the
+    # off-diagonal K tiles are generated inside k_step's accumulators (cov_tile_acc) and never
+    # written, so this is not a whole-K build rate
+    breakdown["k_build_cov_diag_blocks_GBps"] = build_gbs
+    breakdown["k_build_cov_scope"] = "diagonal 128-blocks only; off-diagonal K tiles are built inside k_step"
+
     breakdown["evals_on_gpu"] = prof["evals"]
 
     cpu = None

@@ -481,7 +481,9 @@ __device__ __forceinline__ void db_path_panel(double* lds, double* __restrict__ 
   }
   db_publish<WT>(yseg, lds, pub, pub_val);
   DB_STAMP(0, 16);
-  if (bad && threadIdx.x == 0 && *info == 0) *info = 1;  // (the pivots are wave-uniform)
+  // (the pivots are wave-uniform) an atomic OR: other workgroups of the launch may set the timeout
+  // bit of the same word concurrently (a plain read-modify-write could erase it)
+  if (bad && threadIdx.x == 0) __hip_atomic_fetch_or(info, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <bool WT, int k, int W>

@@ -676,8 +676,13 @@ __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad
         a2 = sum_lane_groups(a2);
         az = sum_lane_groups(az);
       }
-      double* xs = lds + STEP_XS + 32 * (wave >> 1);  // half 1's sums for half 0
-      if (half == 1 && g == 0) {
+      // half 1's sums for half 0: only the waves that finish a region (r < 8: pairs wave >> 1 <= 1,
+      // since np >= SPLIT_MINP >= 4) hand sums over, 32 doubles per pair inside the 64 of STEP_XS;
+      // the waves with r >= 8 must not store (pairs 2 and 3 wrote zeros into FLAT_RB,
+      // the early path's reduction area, racing with its reads)
+      static_assert(STEP_XS + 32 * ((8 + SPLIT_MINP - 1) / SPLIT_MINP) <= FLAT_RB, "flat finish: XS hand-over area");
+      double* xs = lds + STEP_XS + 32 * (wave >> 1);
+      if (r < 8 && half == 1 && g == 0) {
         xs[2 * cl] = a2;
         xs[2 * cl + 1] = az;
       }

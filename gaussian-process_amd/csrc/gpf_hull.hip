@@ -31,7 +31,12 @@ __device__ __forceinline__ double round_to_res(double v, double res, double p10)
   return s;
 }
 
-// Stepped points of gap k = (G[k], G[k+1]) (0 when they do not share a line).
+// Stepped points of gap k = (G[k], G[k+1]) (0 when they do not share a line). Every coordinate
+// evolves on its own (cur[j] = round_to_res(cur[j] + stride_j) per step) and only the fill axis
+// decides the step count, so the axis is stepped first (count pass: that alone) and the emit pass
+// then replays each other coordinate for the same count: the same arithmetic per coordinate in
+// the same order, with no per-lane coordinate array (r6: the DMAX-double array lived in scratch,
+// 272 B per lane; VERDICT r5 hygiene).
 template <bool EMIT>
 __device__ __forceinline__ int64_t hull_gap(const double* __restrict__ G, int64_t k, const HullDims& hd,
                                             double* __restrict__ out) {
@@ -40,18 +45,24 @@ __device__ __forceinline__ int64_t hull_gap(const double* __restrict__ G, int64_
   const double* b = a + d;
   for (int j = 0; j < d; ++j)
     if (j != ax && !(a[j] == b[j])) return 0;
-  double cur[DMAX];
-  for (int j = 0; j < d; ++j) cur[j] = a[j];
+  double c = a[ax];
+  const double end = b[ax], rax = hd.res[ax], pax = hd.p10[ax];
   int64_t s = 0;
-  while (cur[ax] < b[ax] && s < HULL_MAX_STEPS) {
-    for (int j = 0; j < d; ++j) {
-      const double stride = (j == ax) ? hd.res[j] : 0.0;
-      cur[j] = round_to_res(cur[j] + stride, hd.res[j], hd.p10[j]);
-    }
-    if (EMIT)
-      for (int j = 0; j < d; ++j) out[s * d + j] = cur[j];
+  while (c < end && s < HULL_MAX_STEPS) {
+    c = round_to_res(c + rax, rax, pax);
+    if (EMIT) out[s * d + ax] = c;
     ++s;
   }
+  if (EMIT)
+    for (int j = 0; j < d; ++j) {
+      if (j == ax) continue;
+      double v = a[j];
+      const double r = hd.res[j], q = hd.p10[j];
+      for (int64_t t = 0; t < s; ++t) {
+        v = round_to_res(v + 0.0, r, q);
+        out[t * d + j] = v;
+      }
+    }
   return s;
 }
 

@@ -10,6 +10,10 @@
 //   6  as 1 with the k-step's operands read one k-step ahead (two register sets)
 //   7  two outputs per workgroup sharing the streamed B panel, one workgroup per CU (k_dual)
 //   8  the same on a 16-wave workgroup: one output per 8 waves, 4 waves per SIMD (k_dual16)
+//   9  r6: single-output 8-wave workgroups, 2 per CU, in pairs that share the B panel through the
+//      XCD's L2 (workgroups b and b + 8: the dispatcher deals ids round-robin over the 8 XCDs, so
+//      both sit on one XCD and start together), against A panels J and J+1 (k_pair2)
+//  10  the same pairs placed on different XCDs (b and b + 1): no L2 sharing (control)
 // Per variant: TF/s, the shader clock held (s_memtime over s_memrealtime) and the fraction of
 // 128 flop/CU/clk at that clock. Operands are hashed values in [-1, 1) (the clock depends on them).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -mllvm --amdgpu-mfma-vgpr-form \
@@ -290,6 +294,51 @@ __global__ __launch_bounds__(STEP_NTH, 2) void k_dual(const double* __restrict__
   span.stop(clk);
 }
 
+// variants 9/10: workgroup b computes output o of pair q against A panel o (row panel 0 or 1), B panel
+// 2 + q; XCD-local pairs (9: b, b + 8) or split pairs (10: b, b + 1)
+template <int XL>
+__global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_pair2(const double* __restrict__ L, int ld, int D,
+                                                                         double* __restrict__ C,
+                                                                         unsigned long long* clk) {
+  __shared__ __attribute__((aligned(16))) double smem[2 * DL_BUF];
+  __shared__ unsigned long long cs[2];
+  const ClockSpan span(cs);
+  span.start(clk);
+  const int b = blockIdx.x;
+  const int o = XL ? (b >> 3) & 1 : b & 1, q = XL ? (b >> 4) * 8 + (b & 7) : b >> 1;
+  const Quad<T> qd;
+  Acc<T> acc;
+  acc.zero();
+  gemm_stream_dl<false, true>(acc, L + (size_t)o * T * ld, ld, L + (size_t)(2 + q) * T * ld, ld, D, smem, qd);
+  acc.store(qd, C + (size_t)b * T * T, T);
+  span.stop(clk);
+}
+
+template <int XL>
+void run_pair2(int W, int D, const double* L, int ld, double* C, unsigned long long* clk, double mhz_ref) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  hipLaunchKernelGGL(k_pair2<XL>, dim3(W), dim3(STEP_NTH), 0, 0, L, ld, D, C, nullptr);
+  CK(hipMemset(clk, 0, 16));
+  const int iters = 20;
+  CK(hipEventRecord(e0));
+  for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(k_pair2<XL>, dim3(W), dim3(STEP_NTH), 0, 0, L, ld, D, C, clk);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  unsigned long long h[2];
+  CK(hipMemcpy(h, clk, 16, hipMemcpyDeviceToHost));
+  const double mhz = (double)h[0] / (double)h[1] * mhz_ref;
+  const double tf = 2.0 * T * T * (double)D * W * iters / (ms * 1e-3) / 1e12;
+  printf("%d %-44s %6.1f TF/s at %5.0f MHz = %.3f of 128 flop/CU/clk\n", XL ? 9 : 10,
+         XL ? "pairs sharing B through the XCD's L2" : "pairs split over two XCDs (control)", tf, mhz,
+         tf * 1e12 / (128.0 * 256 * mhz * 1e6));
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+}
+
 template <int V>
 void run(const char* name, int W, int D, int shared, const double* L, int ld, double* C, unsigned long long* clk,
          double mhz_ref) {
@@ -351,6 +400,10 @@ int main(int argc, char** argv) {
     fprintf(stderr, "bad args\n");
     return 1;
   }
+  if (W % 16) {
+    fprintf(stderr, "tiles: a multiple of 16\n");
+    return 1;
+  }
   const int ld = D, rows = (shared ? 3 : W + 2) * T;
   double *L, *C;
   unsigned long long* clk;
@@ -364,6 +417,17 @@ int main(int argc, char** argv) {
   if (getenv("ABL_PMC")) {  // (a short run for rocprofv3 --pmc: the single-output loop and the 16-wave pair only)
     run<1>("same loop here", W, D, shared, L, ld, C, clk, ref);
     run_dual(W, D, shared, L, ld, C, clk, ref, 16);
+    if (W % 16 == 0) run_pair2<1>(W, D, L, ld, C, clk, ref);
+    printf("PROBE OK\n");
+    return 0;
+  }
+  if (getenv("ABL_PAIR")) {  // (r6: the L2-shared pairs against the single-output loop and the 16-wave pair)
+    for (int rep = 0; rep < 2; ++rep) {
+      run<1>("same loop here", W, D, shared, L, ld, C, clk, ref);
+      run_dual(W, D, shared, L, ld, C, clk, ref, 16);
+      run_pair2<1>(W, D, L, ld, C, clk, ref);
+      run_pair2<0>(W, D, L, ld, C, clk, ref);
+    }
     printf("PROBE OK\n");
     return 0;
   }

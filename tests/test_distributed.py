@@ -234,14 +234,32 @@ def _rccl_worker(rank, world, port, path, k, q):
            list(info["exchange"])))
 
 
+def _visible_gpus():
+    """GPUs the ranks could use, counted without importing torch or initialising HIP in the pytest
+    parent: the KFD topology's nodes with SIMDs (CPU nodes have none), narrowed by
+    HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES when set."""
+    import glob
+    n = 0
+    for f in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+        try:
+            props = dict(line.split()[:2] for line in open(f) if line.strip())
+        except (OSError, ValueError):
+            continue
+        n += int(props.get("simd_count", "0")) > 0
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([t for t in v.split(",") if t.strip()]))
+    return n
+
+
 @pytest.mark.gpu
 def test_rccl_sharded_swarm_multi_gpu():
     """RCCL with more than one rank: on a box with G >= 2 GPUs, min(G, 8) ranks,
     one per GPU, each scoring its rows with gpf_eval_batch_sharded and exchanging over RCCL
     (ncclAllReduce over xGMI); every rank's trajectory equals the single-rank GPU run bit for bit,
     every particle scored once, and the exchange timing is recorded. Skipped on one-GPU boxes."""
-    import torch
-    n = min(torch.cuda.device_count(), 8)
+    n = min(_visible_gpus(), 8)
     if n < 2:
         pytest.skip(f"{n} GPU visible: RCCL across ranks needs one GPU per rank")
     from conftest import GOLDEN

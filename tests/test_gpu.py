@@ -553,9 +553,52 @@ def test_all_tile_split_live_counts(ctx, monkeypatch, N, d):
         assert np.all(g[m] == 1e13)
         live = ~m
         assert _rel(gm[live], wm[live]) < 1e-10 and _rel(gs[live], ws[live]) < 1e-10
-        assert _rel(g[live], w[live]) < RTOL_LOSS
+        # the objective within 1e-10 of the unsplit path like mean/sd (no blanket 1e-8),
+        # unless a pull of the unsplit run sits at |pull| = 1, where the two correct fp64 runs may
+        # count one coverage point differently (assert_loss_or_ties bounds that difference)
+        for k in np.flatnonzero(live):
+            if abs(g[k] - w[k]) > 1e-10 * abs(w[k]):
+                assert_loss_or_ties(g[k], w[k], wm[k], ws[k], y, s, what=k)
         got.append(g)
     np.testing.assert_array_equal(got[0], got[3])
+
+
+@pytest.mark.parametrize("N", [2048, 4096])
+def test_single_particle_split_factor_tight(ctx, monkeypatch, N):
+    """The single-particle factorisation (the prediction's schedule: the all-tile split with the
+    flat finish, every tile cut into >= 4 pieces, deep launches up to nt = 32) against the unsplit
+    launches (GPF_SPLIT_K=1), factor by factor (the flat finish had no tight independent
+    check). The split sums each tile's partial products in slot order instead of one MFMA chain, so
+    the two differ by rounding only: L and U = L^-1 within 1e-11 of their largest entry (their
+    condition grows with N/e^2, ~1e5 here), z and alpha within 1e-10. The split run is repeated three
+    times and must be bitwise deterministic — a race in the finish (e.g. an LDS hand-over area
+    overwritten) shows up as a mismatch here."""
+    rng = np.random.default_rng(N)
+    d = 3
+    x = rng.uniform(size=(d, N))
+    y = np.sum(np.sin(2 * np.pi * x), axis=0) + 0.1 * rng.standard_normal(N)
+    e = rng.uniform(0.05, 0.2, size=N)
+    s, ex = ref_cpu.sigma_grid()
+    lo, hi = ref_cpu.search_bounds(x)
+    ctx.set_data(x, y, e)
+    ctx.set_grid(s, ex, lo, hi)
+    ls = np.array([0.3, 0.25, 0.4])
+    monkeypatch.delenv("GPF_SPLIT_K", raising=False)
+    runs = [ctx.debug_factor(ls) for _ in range(3)]
+    for r in runs[1:]:
+        for a, b in zip(runs[0], r):
+            np.testing.assert_array_equal(np.tril(a) if a.ndim == 2 else a, np.tril(b) if b.ndim == 2 else b)
+    monkeypatch.setenv("GPF_SPLIT_K", "1")
+    ref = ctx.debug_factor(ls)
+    monkeypatch.delenv("GPF_SPLIT_K")
+    for name, a, b in zip(("L", "U", "z", "alpha"), runs[0], ref):
+        if a.ndim == 2:
+            a, b = np.tril(a)[:N, :N], np.tril(b)[:N, :N]
+            err = np.max(np.abs(a - b)) / np.max(np.abs(b))
+            assert err < 1e-11, (name, err)
+        else:
+            a, b = a[:N], b[:N]
+            assert _rel(a, b) < 1e-10, (name, _rel(a, b))
 
 
 @pytest.mark.parametrize("N,d,hetero,seed", [(130, 1, False, 1), (383, 5, True, 2), (512, 2, True, 3),
