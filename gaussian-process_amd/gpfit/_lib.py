@@ -166,12 +166,15 @@ class Context:
             pass
 
     # -- error mapping: same exception types as the reference's numpy path --
-    def _check(self, rc, what):
+    def _check(self, rc, what, bad=None):
         if rc == GPF_OK:
             return
         msg = self.lib.gpf_last_error(self._h).decode(errors="replace")
         if rc == GPF_NOT_PD:
-            raise np.linalg.LinAlgError("Matrix is not positive definite")
+            err = np.linalg.LinAlgError("Matrix is not positive definite")
+            # the batch row of the first failing particle (gpf_eval_batch's bad_idx), or None
+            err.particle = None if bad is None or bad.value < 0 else int(bad.value)
+            raise err
         if rc == GPF_BAD_ARG:
             raise ValueError(f"{what}: {msg}")
         raise GPFitError(f"{what}: {msg}")
@@ -212,7 +215,7 @@ class Context:
         rc = self.lib.gpf_eval_batch(self._h, _ptr(P), n, _ptr(loss),
                                      _ptr(mu) if want_mu_sd else None,
                                      _ptr(sd) if want_mu_sd else None, ctypes.byref(bad))
-        self._check(rc, "gpf_eval_batch")
+        self._check(rc, "gpf_eval_batch", bad)
         return (loss, mu, sd) if want_mu_sd else loss
 
     def eval_batch_sharded(self, comm, positions):
@@ -225,7 +228,7 @@ class Context:
         loss = np.empty(P.shape[0])
         bad = ctypes.c_int(-1)
         rc = self.lib.gpf_eval_batch_sharded(self._h, comm.handle, _ptr(P), P.shape[0], _ptr(loss), ctypes.byref(bad))
-        self._check(rc, "gpf_eval_batch_sharded")
+        self._check(rc, "gpf_eval_batch_sharded", bad)
         return loss
 
     def synchronize(self):
