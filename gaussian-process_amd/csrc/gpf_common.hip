@@ -217,10 +217,17 @@ __device__ __forceinline__ void dl_load(const double* g, double* l) {
 // The same transfer in the saddr form: a wave-uniform 64-bit base in SGPRs plus a 32-bit per-lane
 // byte offset, so the streamed GEMMs keep one VGPR per transfer stream instead of forming a 64-bit
 // address per lane and transfer.
+template <bool NT = false>
 __device__ __forceinline__ void dl_load_s(const void* base, uint32_t off, double* l) {
   const uint32_t m = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)l;
-  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(base), "{m0}"(m) : "memory");
+  if constexpr (NT)  // non-temporal: a panel streamed once per launch does not evict the shared ones from L2
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt" ::"v"(off), "s"(base), "{m0}"(m) : "memory");
+  else
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(base), "{m0}"(m) : "memory");
 }
+#ifndef GPF_B_NT
+#define GPF_B_NT 0
+#endif
 
 // Slot swizzle of the [r][k] panels: k-pair kp of row r sits in slot kp ^ dl_sw(r). An MFMA
 // operand read takes 16 consecutive rows at one k per half-wave; rows r and r+8 share a bank
@@ -295,7 +302,7 @@ struct DenseRun {
     for (int u = 0; u < 2; ++u) {
       const int blk = blk0 + u;
       dl_load_s(Ac, ga[u], sbuf + blk * 8 * DL_KC);
-      dl_load_s(Bc, gb[u], sbuf + 128 * DL_KC + (NN ? blk * 128 : blk * 8 * DL_KC));
+      dl_load_s<GPF_B_NT != 0>(Bc, gb[u], sbuf + 128 * DL_KC + (NN ? blk * 128 : blk * 8 * DL_KC));
     }
   }
 

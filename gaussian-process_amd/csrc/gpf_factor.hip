@@ -76,7 +76,7 @@ __host__ __device__ __forceinline__ void step_tile(int b, int P, int ntl, int gr
 // (r5: the critical-tile split SPLIT_CRIT = 2 of rounds 1-4 — off by default since round 2 and
 // slower again on B in r5, profiles/r5/ab_split_crit_B.txt — and its reduction tree were removed.)
 enum { SPLIT_NONE = 0, SPLIT_ALL = 1 };
-enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2, ROLE_DIAG = 3, ROLE_SYRK = 4, ROLE_LA = 5 };
+enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2, ROLE_DIAG = 3, ROLE_SYRK = 4, ROLE_LA = 5, ROLE_PLA = 6, ROLE_SYRKP = 7 };
 
 // Early diagonal factor (k_step<SPLIT, ED = 1>; the host chooses it for launches that leave
 // workgroup slots idle): launch J starts with P extra workgroups that factor diagonal
@@ -197,6 +197,91 @@ __host__ __device__ __forceinline__ int step_decode(int b, int J, int P, int nt,
   }
   return ROLE_WHOLE;
 }
+
+// ----------------------------------------------------------------------------
+// Paired block columns (r6; k_step<SPLIT_NONE, 0>, the slot-bound launches of configs C/D; VERDICT r5
+// item 1). A left-looking launch streams every tile's B panel (row panel I of L for an L tile, column
+// panel K of U for a U tile) from HBM once per block column: ~2.4 GB per group launch at C, 16x the
+// compulsory stores, and the HBM stream costs the chip its clock (profiles/r5/gemm_ablate.txt: the
+// same GEMM loop holds 2.2 GHz streaming from HBM, 2.38 GHz on L2-resident panels). Block column J+1
+// needs the same panels over the same depth [0, J) plus one more 128-block, so the launches go in
+// pairs:
+//   lead J (pair = 1):    every tile of column J as before, and beside each tile of column J+1 that
+//                         exists already (L tiles I >= J+2, U tiles K < J) its GEMM over the columns
+//                         < J (ROLE_PLA: the covariance seed included), stored to a partial slot; the
+//                         SYRK workgroup of block J+1 as before, and a partial SYRK of block J+2 over
+//                         the same depth (ROLE_SYRKP, in place);
+//   follow J+1 (pair = 2): every tile loads its partial and runs the one remaining 128-deep block (the
+//                         columns of block J) before its finish; the critical tile applies blocks J
+//                         and J+1 to its diagonal block (the rest was ROLE_SYRKP's); no SYRK workgroups.
+// A tile's workgroup and its partner stream the same panel at the same time from one XCD (pair_decode),
+// so the panel is fetched into that XCD's L2 once: the probe (scripts/probes/gemm_ablate.hip,
+// profiles/r6/pair_*.txt) ran such pairs at 72.5-73.3 TF/s and 2.33-2.34 GHz against 68.6-68.7 TF/s
+// and 2.21-2.23 GHz for the single-output loop, at the same 0.95 per clock and with two ordinary
+// 8-wave workgroups per CU (the 16-wave two-output workgroup of round 5 held the clock too but lost
+// per clock, 0.93, and leaves its finishes without a co-resident workgroup). Every element sees the
+// same MFMAs in the same order as in the unpaired launches (a chain split at a chunk boundary with
+// an exact store and reload), so the factor is bitwise unchanged (test_paired_block_columns_bitwise).
+// ----------------------------------------------------------------------------
+// workgroups per particle of tile w's unit in a lead launch: the tile, its partner (w = 0: the SYRK
+// workgroup of block J+1; else the look-ahead partial), and for w = 1 when it is the L tile I = J+2
+// the partial SYRK of block J+2 (all three stream row panel J+2)
+__host__ __device__ __forceinline__ int pair_unit(int J, int w, int nt) { return (w == 1 && J + 2 <= nt - 1) ? 3 : 2; }
+__host__ __device__ __forceinline__ int pair_grid_per_particle(int J, int nt) {
+  int n = 0;
+  for (int w = 0; w < nt - 1; ++w) n += pair_unit(J, w, nt);
+  return n;
+}
+// Workgroup b of a lead launch (P a multiple of 8, w-major as step_tile's particle-fastest order):
+// per tile w, groups of 8 particles (one per XCD: b & 7 = p & 7), first the tile's own workgroups
+// (ROLE_WHOLE), then the partners of the same 8 particles — so a partner sits 8 (or 16) ids behind
+// its tile, on the same XCD, dispatched together with it (w = 0: the SYRK workgroups 8 ids ahead of
+// their critical tiles).
+__host__ __device__ __forceinline__ int pair_decode(int b, int J, int P, int nt, int& p, int& w, int* hout = nullptr) {
+  int base = 0;
+  for (w = 0; w < nt - 2; ++w) {
+    const int n = pair_unit(J, w, nt) * P;
+    if (b < base + n) break;
+    base += n;
+  }
+  const int u = pair_unit(J, w, nt), r = b - base, c = r / (8 * u), h = (r % (8 * u)) / 8;
+  p = 8 * c + (r & 7);
+  if (hout) *hout = h;
+  if (w == 0) {  // the SYRK workgroups ahead of their critical tiles, which wait for them (no wait can
+                 // then depend on a workgroup not yet dispatched)
+    if (h == 1) return ROLE_WHOLE;
+    w = -1;  // (as step_decode's SYRK workgroups)
+    return ROLE_SYRK;
+  }
+  if (h == 0) return ROLE_WHOLE;
+  return h == 1 ? ROLE_PLA : ROLE_SYRKP;
+}
+// Start synchronisation of a lead launch's partners (a performance hint, never a data dependency):
+// a tile's workgroup and its partner share their panel through the XCD's L2 only while they stream
+// it together, and the dispatcher starts a partner whenever a slot of its XCD frees — after the first
+// round of a launch partners drift apart by a finish phase or more. So every member h of a unit
+// stores the launch's tag (unique per factorisation and launch) into its word on arrival, and the
+// earlier-dispatched members wait until every later member of the unit has arrived. A waiting
+// workgroup waits only for the ids right behind it in its XCD's dispatch order, which are next for
+// that XCD's next free slot: the wait always ends. Bounded (~50 us); on timeout it just proceeds.
+constexpr int PAIR_HMAX = 3;
+__device__ __forceinline__ void pair_start_sync(int J, int u, int h, int p, int nt, int* pstart, int ptag) {
+  int* f = pstart + ((size_t)p * (nt - 1) + u) * PAIR_HMAX;
+  const int n = pair_unit(J, u, nt);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(f + h, ptag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = 0; k < 20000; ++k) {
+      bool all = true;
+      for (int j = h + 1; j < n; ++j) all = all && __hip_atomic_load(f + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ptag;
+      if (all) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+}
+
+// the partial slot of tile w' (follow-launch numbering; the lead's tile w + 1) of particle p
+__host__ __device__ __forceinline__ size_t pair_slot(int p, int wf, int nt) { return ((size_t)p * (nt - 1) + wf) * T * T; }
 
 // LDS of a k_step workgroup (doubles): the GEMM stages (DL_STAGE), the diagonal factor
 // (DB_LDS), the staged U_JJ of the triangular finishes (TRI_LDS) with z_J behind
@@ -763,6 +848,58 @@ __device__ __forceinline__ void la_item(int J, int p, int Npad, const double* __
   acc.store(qd, lab + la_slot(p, J), T);
 }
 
+// A partial from its slot in the accumulators' own layout (store_node's: wave w's 16 KiB, one 1 KiB
+// block per register pair and 16 B per lane), read back by the same wave layout: 16-B loads.
+__device__ __forceinline__ void load_node(Acc<T>& acc, const double* slot) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(slot), 0, T * T * 8, 0x00020000);
+  const int wb = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * NODE_WAVE, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int mi = 0; mi < Acc<T>::MBR; ++mi)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const d2 v = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, wb + (mi * 2 + h) * 1024, 0));
+      acc.v[mi][0][2 * h] = v.x;
+      acc.v[mi][0][2 * h + 1] = v.y;
+    }
+}
+
+// Lead launch J, ROLE_PLA: block column J+1's tile (the lead's tile w = w' + 1) over the columns < J,
+// the GEMM the follow launch would otherwise stream again — L tile I = J+1+w: the covariance seed
+// A_{J+1,I}^T (cov_tile_acc) minus L_{J+1,<J} L_{I,<J}^T; U tile K: L_{J+1,[K,J)} U_{[K,J),K} (its first
+// block triangular) — to the particle's slot w' (plain stores: the follow launch reads it after the
+// launch boundary).
+__device__ __forceinline__ void pla_item(int J, int w, int p, int nt, int Npad, const double* __restrict__ Lb,
+                                         const double* __restrict__ Ub, int N, const double* __restrict__ x,
+                                         const double* __restrict__ ls, int d, double* __restrict__ pb, double* lds) {
+  const size_t ld = (size_t)Npad;
+  const int nL = nt - 1 - J;
+  const double* Lp = Lb + (size_t)p * ld * ld;
+  const Quad<T> qd;
+  Acc<T> acc;
+  if (w < nL) {
+    const int I = J + 1 + w;
+    cov_tile_acc(acc, qd, x, ls + (size_t)p * d, d, N, J + 1, I, lds);
+    gemm_stream_dl<false, true>(acc, Lp + (size_t)(J + 1) * T * ld, Npad, Lp + (size_t)I * T * ld, Npad, J * T, lds, qd);
+  } else {
+    const int K = w - nL;
+    const double* Up = Ub + (size_t)p * ld * ld;
+    acc.zero();
+    gemm_stream_dl<true, false, TRI_B_KGEC>(acc, Lp + (size_t)(J + 1) * T * ld + (size_t)K * T, Npad,
+                                            Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T, lds, qd);
+  }
+  store_node(acc, pb + pair_slot(p, w - 1, nt), qd);
+}
+
+// Lead launch J, ROLE_SYRKP: A_{J+2,J+2} -= L_{J+2,<J} L_{J+2,<J}^T in place (plain stores; the follow
+// launch's critical tile continues with blocks J and J+1).
+__device__ __forceinline__ void syrkp_item(int J, int p, int Npad, double* __restrict__ Lb, double* lds) {
+  const size_t ld = (size_t)Npad;
+  const int I = J + 2;
+  double* Lp = Lb + (size_t)p * ld * ld;
+  const Quad<T> qd;
+  syrk_tile<false>(Lp + (size_t)I * T * ld + (size_t)I * T, ld, Lp + (size_t)I * T * ld, Npad, J * T, lds, qd);
+}
+
 // Tile w of block column J of particle p (the unit of work of k_step); role from step_decode.
 //   L tile (I = J+1+w):  D = A_IJ^T - L_J,<J L_I,<J^T  (the transposed panel C^T, so that each
 //                        wave holds all 128 k of the triangular multiply for its 16 rows of C)
@@ -779,9 +916,14 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
                                           const double* __restrict__ ls, int d, int S, int S2, int sidx,
                                           double* __restrict__ part, unsigned* __restrict__ cnt, int* sflag,
                                           const int* __restrict__ dflag, const int* __restrict__ yflag, int defer,
-                                          int spins, int la, const double* __restrict__ lab, double* lds) {
+                                          int spins, int la, const double* __restrict__ lab, int pair,
+                                          const double* __restrict__ pb, double* lds) {
   const int tid = threadIdx.x;
   const int nL = nt - 1 - J;
+  // (paired block columns exist only in the fused-diagonal schedule: the other instantiations keep
+  // their register allocation)
+  constexpr bool PAIRS = SPLIT == SPLIT_NONE && !ED;
+  const bool follow = PAIRS && pair == 2;
   const size_t ld = (size_t)Npad;
   if (SPLIT != SPLIT_NONE && role == ROLE_IDLE) return;
   double* Lp = Lb + (size_t)p * ld * ld;
@@ -823,6 +965,11 @@ if (w < nL)
       acc.load(qd, lab + la_slot(p, J - 1), T);
       gemm_stream_dl<false, true>(acc, Lp + (size_t)J * T * ld + k0, Npad, Lp + (size_t)I * T * ld + k0, Npad, J * T - k0,
                                   lds, qd);
+    } else if (follow) {
+      // follow launch: the lead's partial (seed and the columns < J-1), then block column J-1
+      load_node(acc, pb + pair_slot(p, w, nt));
+      gemm_stream_dl<false, true>(acc, Lp + (size_t)J * T * ld + (size_t)(J - 1) * T, Npad,
+                                  Lp + (size_t)I * T * ld + (size_t)(J - 1) * T, Npad, T, lds, qd);
     } else {
       cov_tile_acc(acc, qd, x, lp, d, N, J, I, lds);
       if (J > 0)
@@ -861,7 +1008,11 @@ if (w < nL)
     // look-ahead: A_II -= L_IJ L_IJ^T (the full tile; only its lower half is ever read). Deferred
     // (SPLIT_ALL never defers): only the critical tile, on top of the launch's SYRK workgroup's S.
     const bool defer_on = SPLIT != SPLIT_ALL && defer;
-    if (!defer_on || I == J + 1) {
+    if (follow && I == J + 1) {
+      // the lead's ROLE_SYRKP left A_II reduced over the columns < J-1: blocks J-1 and J remain (one
+      // 256-deep update, the chunks in the order the SYRK workgroup and this tile would run them)
+      syrk_tile<false>(Aii, ld, Aij - T, Npad, 2 * T, lds, qd);
+    } else if (!defer_on || I == J + 1) {
       if (defer_on && J > 0 && wait_diag(yflag + p, J, info + p, spins, sflag)) return;  // S published
       syrk_tile<false>(Aii, ld, Aij, Npad, T, lds, qd);
     }
@@ -877,9 +1028,16 @@ if (w < nL)
     double* Ujk = Up + (size_t)J * T * ld + (size_t)K * T;
     Acc<T> acc;
     // W = L_J,[K,J) U_[K,J),K (U_KK is lower triangular: the wave's first chunks add zeros)
-    acc.zero();
-    gemm_stream_dl<true, false, TRI_B_KGEC>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
-                                            Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T, lds, qd);
+    if (follow && K < J - 1) {
+      // follow launch: the lead's partial over [K, J-1), then block row J-1 of U's column panel K
+      load_node(acc, pb + pair_slot(p, w, nt));
+      gemm_stream_dl<true, false>(acc, Lp + (size_t)J * T * ld + (size_t)(J - 1) * T, Npad,
+                                  Up + (size_t)(J - 1) * T * ld + (size_t)K * T, Npad, T, lds, qd);
+    } else {
+      acc.zero();
+      gemm_stream_dl<true, false, TRI_B_KGEC>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
+                                              Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T, lds, qd);
+    }
     GPF_PHASE(0);
     if (ED && wait_diag(dflag + p, J, info + p, spins, sflag)) return;  // U_JJ, z_J (U tiles exist for J > 0 only)
     if (tid < T) zj[tid] = yp[J * T + tid];
@@ -935,7 +1093,9 @@ __global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_step(int J, i
                                                   int d, int S, int S2, double* __restrict__ part,
                                                   unsigned* __restrict__ cnt, int* __restrict__ dflag, int ed,
                                                   int* __restrict__ yflag, int defer, int sy, int spins, int la,
-                                                  double* __restrict__ lab, unsigned long long* __restrict__ clk) {
+                                                  double* __restrict__ lab, int pair, double* __restrict__ pb,
+                                                  int* __restrict__ pstart, int ptag,
+                                                  unsigned long long* __restrict__ clk) {
   const int tid = threadIdx.x;
   __shared__ unsigned long long sclk[2];
   const ClockSpan span(sclk);
@@ -951,10 +1111,14 @@ __global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_step(int J, i
 #endif
   __shared__ __attribute__((aligned(16))) double lds[SPLIT == SPLIT_ALL ? STEP_LDS_FLAT : STEP_LDS];
   __shared__ int sflag;
-  int p, w, sidx;
-  const int role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, SPLIT != SPLIT_ALL && sy,
-                                      SPLIT == SPLIT_NONE && ED && (la & 1) && !sy, p, w, sidx,
-                                      SPLIT == SPLIT_NONE && ED && (la & 32) != 0);
+  int p, w, sidx = 0;
+  constexpr bool PAIRS = SPLIT == SPLIT_NONE && !ED;
+  int uh = 0;
+  const int role = (PAIRS && pair == 1)
+                       ? pair_decode((int)blockIdx.x, J, P, nt, p, w, &uh)
+                       : step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, SPLIT != SPLIT_ALL && sy,
+                                            SPLIT == SPLIT_NONE && ED && (la & 1) && !sy, p, w, sidx,
+                                            SPLIT == SPLIT_NONE && ED && (la & 32) != 0);
 #ifdef GPF_CHECK
   // diagnostic build (-DGPF_CHECK): every index the workgroup derives its addresses from, checked
   // against the launch's extents before any access (an out-of-range role prints and does nothing)
@@ -963,7 +1127,10 @@ __global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_step(int J, i
     if (role == ROLE_SYRK) ok = ok && w == -1 && J >= 1 && J <= nt - 2 && yflag != nullptr;
     else if (role == ROLE_LA) ok = ok && w == -1 && J >= 1 && J + 2 < nt && lab != nullptr;
     else if (role == ROLE_DIAG) ok = ok && w == -1 && ED && dflag != nullptr;
-    else if (role != ROLE_IDLE) ok = ok && w >= 0 && w < nt - 1 && sidx >= 0 &&
+    else if (role == ROLE_PLA) ok = ok && PAIRS && pair == 1 && pb != nullptr && w >= 1 && w < nt - 1 && J >= 1 &&
+                                     (w >= nt - 1 - J || J + 1 + w < nt);
+    else if (role == ROLE_SYRKP) ok = ok && PAIRS && pair == 1 && w == 1 && J >= 1 && J + 2 <= nt - 1;
+    else if (role != ROLE_IDLE) ok = ok && w >= 0 && w < nt - 1 && sidx >= 0 && (pair != 2 || pb != nullptr) &&
                                      sidx < (SPLIT == SPLIT_ALL ? split_all_pieces(J, w, nt, S) : S) && sidx < S2 &&
                                      (role != ROLE_PIECE || (part != nullptr && cnt != nullptr && S > 1)) &&
                                      (w >= nt - 1 - J || J + 1 + w < nt) && (w < nt - 1 - J || w - (nt - 1 - J) < J);
@@ -975,7 +1142,12 @@ __global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_step(int J, i
     }
   }
 #endif
-  if (SPLIT != SPLIT_ALL && role == ROLE_SYRK) {
+  if (PAIRS && pair == 1 && pstart) pair_start_sync(J, role == ROLE_SYRK ? 0 : w, uh, p, nt, pstart, ptag);
+  if (PAIRS && role == ROLE_PLA) {
+    pla_item(J, w, p, nt, Npad, Lb, Ub, N, x, ls, d, pb, lds);
+  } else if (PAIRS && role == ROLE_SYRKP) {
+    syrkp_item(J, p, Npad, Lb, lds);
+  } else if (SPLIT != SPLIT_ALL && role == ROLE_SYRK) {
     syrk_item(J, p, Npad, Lb, yflag, lds);
     if (SPLIT == SPLIT_NONE && ED && (la & 1)) {  // the look-ahead rides on the SYRK workgroup (after its flag)
       __syncthreads();
@@ -995,7 +1167,7 @@ __global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_step(int J, i
                     dflag + p, J);
   } else {
     step_item<SPLIT, ED>(role, J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, S2, sidx, part, cnt, &sflag,
-                         dflag, yflag, defer, spins, la, lab, lds);
+                         dflag, yflag, defer, spins, la, lab, pair, pb, lds);
   }
   span.stop(clk);
 #ifdef GPF_WG_TRACE

@@ -84,6 +84,11 @@ struct gpf_ctx {
   size_t part_cap = 0, cnt_cap = 0;
   double* d_la = nullptr;      // look-ahead partials of the next critical tiles (gpf::la_item), one tile per particle
   size_t la_cap = 0;
+  double* d_pb = nullptr;      // paired block columns: the lead launch's partials, nt-1 tiles per particle (gpf::pair_slot)
+  size_t pb_cap = 0;
+  int* d_pstart = nullptr;     // ... and the partners' start words (gpf::pair_start_sync), PAIR_HMAX per tile
+  size_t pstart_cap = 0;
+  int fact_seq = 0;            // factorisations run (tags the start words)
   double* d_szp = nullptr;
   double* d_ls = nullptr;
   double* d_mu = nullptr;
@@ -253,6 +258,12 @@ static void free_work(gpf_ctx* c) {
   hipFree(c->d_la);
   c->d_la = nullptr;
   c->la_cap = 0;
+  hipFree(c->d_pb);
+  c->d_pb = nullptr;
+  c->pb_cap = 0;
+  hipFree(c->d_pstart);
+  c->d_pstart = nullptr;
+  c->pstart_cap = 0;
   c->d_L = c->d_U = c->d_yb = c->d_s2p = c->d_szp = c->d_ls = c->d_mu = c->d_sd = c->d_loss = nullptr;
   c->d_info = nullptr;
   c->d_hist = nullptr;
@@ -261,7 +272,9 @@ static void free_work(gpf_ctx* c) {
 
 static size_t bytes_per_particle(const gpf_ctx* c) {
   const size_t np = (size_t)c->Npad;
-  return 2 * np * np * 8 + (2 * (size_t)c->nt * np + 3 * np) * 8 + (size_t)(c->K + 1) * 4 + 64 * 8 + 8;
+  // (+ the paired block columns' partial slots, nt-1 tiles, allocated when a factorisation pairs)
+  return 2 * np * np * 8 + (2 * (size_t)c->nt * np + 3 * np) * 8 + (size_t)(c->K + 1) * 4 + 64 * 8 + 8 +
+         (size_t)std::max(c->nt - 1, 0) * T * T * 8;
 }
 
 // Chunk capacity from free HBM (GPF_MAX_CHUNK caps it, GPF_MEM_FRACTION scales the budget).
@@ -443,6 +456,17 @@ static bool reorder_on() {
   return on;
 }
 
+// Paired block columns (gpf::pair_decode; lead launch J streams each tile's panel once for block
+// columns J and J+1, the follow launch J+1 finishes from the partials) for the fused-diagonal
+// schedule without split: slot-bound launches (configs C, D) whose particle groups are multiples of 8
+// (one particle per XCD in every group of 8, so a tile and its partner share an XCD) and nt >= 4.
+// GPF_PAIR = 0/1 overrides.
+static bool pair_on() {
+  bool on = false;
+  if (const char* s = getenv("GPF_PAIR")) on = atoi(s) != 0;
+  return on;
+}
+
 // Bound of the early-diagonal hand-off spin (gpf::wait_diag, polls of ~1 us): ~2 s by default;
 // GPF_WAIT_SPINS lowers it to exercise the timeout report (tests/test_gpu.py).
 static int wait_spins() {
@@ -513,6 +537,7 @@ struct StepLaunch {
   int defer, sy;                        // deferred diagonal update; sy: gc SYRK workgroups follow
   int ro;  // reordered dispatch (gpf::step_decode ro): light U tiles, diagonal, other tiles, SYRK workgroups
   int la;  // look-ahead: bit 0: gc LA workgroups follow (gpf::la_item); bit 1: the critical tiles seed from launch J-1's
+  int pair;  // paired block columns: 1 lead launch (gpf::pair_decode), 2 follow launch (its tiles seed from the lead's partials)
   unsigned grid;
   size_t part_off, cnt_off;
 };
@@ -546,10 +571,15 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
       // and one group (a concurrent group's launch could hold the slots the waiters need)
       l.ro = (reorder_on() && ng == 1 && l.ed && l.sy && l.split == gpf::SPLIT_NONE && l.grp == 0 && J >= 1 &&
               3 * l.gc <= 256) ? 1 : 0;
+      // paired block columns: leads at odd J with a block column behind them, each followed by J+1
+      const bool pairs = pair_on() && !l.ed && S == 1 && l.defer && l.grp == 0 && l.gc % 8 == 0 && nt >= 4;
+      l.pair = pairs && (J & 1) && J + 1 <= nt - 1 ? 1 : (pairs && J >= 2 && !(J & 1) ? 2 : 0);
+      if (l.pair == 2) l.sy = 0;  // (the lead's partial SYRK and the critical tile reduce the diagonal block)
       int nall = 0;
       for (int w = 0; S > 1 && w < nt - 1; ++w) nall += gpf::split_all_pieces(J, w, nt, l.S);
       l.grid = (S > 1 ? l.gc * nall : l.gc * (nt - 1)) + (l.ed ? l.gc : 0) + (l.sy ? l.gc : 0) +
                ((l.la & 1) && !l.sy ? l.gc : 0);  // (with SYRK workgroups the look-ahead rides on them)
+      if (l.pair == 1) l.grid = (unsigned)(l.gc * gpf::pair_grid_per_particle(J, nt));
       // one set of partial slots per group: groups run concurrently
       l.part_off = (size_t)l.p0 * (nt - 1) * Smax * T * T;
       l.cnt_off = (size_t)l.p0 * (nt - 1) * gpf::split_cnt_stride(nt);
@@ -585,6 +615,17 @@ static int run_factor(gpf_ctx* c, int pc) {
       else fl += 2.0 * t3 * (J - (w - (nt - 1 - J)));
     }
     if (ed || J + 1 < nt) fl += (2.0 / 3.0) * t3;
+    return fl;
+  };
+  // paired block columns: the lead launch J also runs block column J+1's GEMMs over the columns < J
+  // (L tiles I >= J+2: depth 128J; U tiles K < J: depth 128(J-K), first block triangular), which the
+  // follow launch then does not
+  auto pla_flops = [&](int J) {
+    double fl = 0.0;
+    for (int w = 1; w < nt - 1; ++w) {
+      if (w < nt - 1 - J) fl += 2.0 * t3 * J;
+      else fl += 2.0 * t3 * (J - (w - (nt - 1 - J))) - t3;
+    }
     return fl;
   };
   // Split-K plan first: a (re)allocation of the arrival counters queues their zeroing memset on
@@ -660,8 +701,31 @@ static int run_factor(gpf_ctx* c, int pc) {
   // block-column launches (split-K for launches with few tiles, planned above)
   std::vector<StepLaunch> plan;
   step_plan(pc, nt, S, Smax, plan);
-  bool any_la = false;
-  for (const StepLaunch& l : plan) any_la = any_la || l.la != 0;
+  bool any_la = false, any_pair = false;
+  for (const StepLaunch& l : plan) {
+    any_la = any_la || l.la != 0;
+    any_pair = any_pair || l.pair != 0;
+  }
+  const size_t pb_bytes = (size_t)pc * (nt - 1) * T * T * 8;
+  if (any_pair && pb_bytes > c->pb_cap) {  // (nt >= 4: never under a graph capture)
+    clear_graphs(c);
+    hipFree(c->d_pb);
+    c->d_pb = nullptr;
+    c->pb_cap = 0;
+    GPF_HIP(c, hipMalloc(&c->d_pb, pb_bytes));
+    c->pb_cap = pb_bytes;
+  }
+  const size_t ps_bytes = (size_t)pc * (nt - 1) * gpf::PAIR_HMAX * 4;
+  if (any_pair && ps_bytes > c->pstart_cap) {
+    hipFree(c->d_pstart);
+    c->d_pstart = nullptr;
+    c->pstart_cap = 0;
+    GPF_HIP(c, hipMalloc(&c->d_pstart, ps_bytes));
+    GPF_HIP(c, hipMemset(c->d_pstart, 0, ps_bytes));  // (tags start at 1)
+    c->pstart_cap = ps_bytes;
+  }
+  const int seq = ++c->fact_seq & 0x7fffff;
+  const bool psync = getenv("GPF_PAIR_SYNC") == nullptr || atoi(getenv("GPF_PAIR_SYNC")) != 0;
   if (any_la && 2 * (size_t)pc * T * T * 8 > c->la_cap) {  // (never under a graph capture: nt >= 4 only)
     clear_graphs(c);
     hipFree(c->d_la);
@@ -673,7 +737,7 @@ static int run_factor(gpf_ctx* c, int pc) {
   // test hook: the critical tiles that seed from the look-ahead wait ~0.3 ms first (gpf::step_item)
   const int la_delay = (getenv("GPF_LA_DELAY_TEST") && atoi(getenv("GPF_LA_DELAY_TEST")) != 0) ? 4 : 0;
   for (const StepLaunch& l : plan) {
-    const double fl = step_flops(l.J);
+    const double fl = step_flops(l.J) + (l.pair == 1 ? pla_flops(l.J) : l.pair == 2 ? -pla_flops(l.J - 1) : 0.0);
     const int p0 = l.p0, gc = l.gc;
     hipStream_t st = (ng > 1) ? c->sub[l.g] : c->stream;
     // (every split launch gets its buffers: under SPLIT_ALL, l.S is chunks per piece, not a piece count)
@@ -689,7 +753,10 @@ static int run_factor(gpf_ctx* c, int pc) {
                          c->d_ls + (size_t)p0 * c->d, c->d, l.S, l.S2, partg, cntg, c->d_flag + p0, l.ed,
                          c->d_cflag + p0, l.defer, l.sy, spins,
                          l.la | ((l.la & 2) ? la_delay : 0) | (l.ro ? 32 : 0),
-                         l.la ? c->d_la + 2 * (size_t)p0 * T * T : nullptr, c->prof ? c->d_clk : nullptr);
+                         l.la ? c->d_la + 2 * (size_t)p0 * T * T : nullptr, l.pair,
+                         l.pair ? c->d_pb + gpf::pair_slot(p0, 0, nt) : nullptr,
+                         (l.pair == 1 && psync) ? c->d_pstart + (size_t)p0 * (nt - 1) * gpf::PAIR_HMAX : nullptr,
+                         (seq << 8) | l.J, c->prof ? c->d_clk : nullptr);
     });
     if (rc) return rc;
     total += fl * gc;
@@ -1362,6 +1429,7 @@ static int persist_check(int pc, int nt, long long* stats, char* msg, int msg_le
     stats[7] = 0;
     stats[8] = syrks;
     stats[9] = 1;
+    stats[10] = 0;
   }
   return GPF_OK;
 }
@@ -1383,7 +1451,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
   long long wgs = 0, whole_tiles = 0, split_tiles = 0;
   std::vector<int> whole, piece, diag, syrk;
   long long diag_wgs = 0, syrk_wgs = 0;
-  std::vector<int> la_prev(MAX_GROUPS, 0);
+  std::vector<int> la_prev(MAX_GROUPS, 0), pair_prev(MAX_GROUPS, 0), pairJ(MAX_GROUPS, -1);
   if ((int)plan.size() != (nt > 1 ? nt * ng : 0)) return plan_fail(msg, msg_len, "plan has %d launches, want %d",
                                                               (int)plan.size(), nt * ng);
   for (const StepLaunch& l : plan) {
@@ -1422,6 +1490,67 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     if (l.ro && (ng != 1 || !l.ed || !l.sy || l.split != gpf::SPLIT_NONE || l.grp != 0 || l.J < 1 || 3 * l.gc > 256 ||
                  l.grid != (unsigned)(l.gc * (nt - 1) + 2 * l.gc)))
       return plan_fail(msg, msg_len, "J=%d g=%d: reordered dispatch out of place", l.J, l.g);
+    // paired block columns: a lead launch (J odd, with a block column behind it, fused diagonal factor,
+    // deferred update, no split, groups of 8 particles) is followed on its stream by the follow
+    // launch J+1, and only there
+    if (l.pair && (l.ed || l.split != gpf::SPLIT_NONE || !l.defer || l.grp != 0 || l.gc % 8 != 0 || nt < 4 ||
+                   (l.pair == 1 && (!(l.J & 1) || l.J + 1 > nt - 1 || !l.sy)) ||
+                   (l.pair == 2 && (l.sy || pair_prev[l.g] != 1 || pairJ[l.g] != l.J - 1))))
+      return plan_fail(msg, msg_len, "J=%d g=%d: paired block column %d out of place", l.J, l.g, l.pair);
+    if (pair_prev[l.g] == 1 && l.pair != 2)
+      return plan_fail(msg, msg_len, "J=%d g=%d: the lead launch's partials left unused", l.J, l.g);
+    pair_prev[l.g] = l.pair;
+    pairJ[l.g] = l.J;
+    if (l.pair == 1) {
+      if (l.grid != (unsigned)(l.gc * gpf::pair_grid_per_particle(l.J, nt)))
+        return plan_fail(msg, msg_len, "J=%d g=%d: lead launch grid %u", l.J, l.g, l.grid);
+      std::vector<int> pla((size_t)tiles, 0), syp((size_t)l.gc, 0);
+      for (unsigned b = 0; b < l.grid; ++b) {
+        int p = -1, w = -1;
+        const int role = gpf::pair_decode((int)b, l.J, l.gc, nt, p, w);
+        if (p < 0 || p >= l.gc || (int)(b & 7) != (p & 7))
+          return plan_fail(msg, msg_len, "J=%d block %u: pair decode p=%d (its XCD is not the particle's)", l.J, b, p);
+        if (role != gpf::ROLE_WHOLE) {  // a partner: its tile's workgroup of the same particle 8 or 16 ids
+          // earlier (a SYRK workgroup: its critical tile, which waits for it, 8 ids later)
+          int p2 = -1, w2 = -1, ok = 0;
+          for (int k = 1; k <= 2 && !ok; ++k) {
+            const int b2 = role == gpf::ROLE_SYRK ? (int)b + 8 * k : (int)b - 8 * k;
+            ok = b2 >= 0 && b2 < (int)l.grid && gpf::pair_decode(b2, l.J, l.gc, nt, p2, w2) == gpf::ROLE_WHOLE &&
+                 p2 == p && w2 == (role == gpf::ROLE_SYRK ? 0 : w) && (role != gpf::ROLE_SYRK || k == 1);
+          }
+          if (!ok) return plan_fail(msg, msg_len, "J=%d block %u: partner (role %d) not beside its tile", l.J, b, role);
+        }
+        if (role == gpf::ROLE_SYRK) {
+          if (syrk[p]++) return plan_fail(msg, msg_len, "J=%d: duplicate SYRK workgroup p=%d", l.J, p);
+        } else if (role == gpf::ROLE_SYRKP) {
+          if (w != 1 || l.J + 2 > nt - 1 || syp[p]++)
+            return plan_fail(msg, msg_len, "J=%d: misplaced or duplicate partial SYRK p=%d", l.J, p);
+        } else if (role == gpf::ROLE_PLA) {
+          if (w < 1 || w >= ntl || pla[(size_t)p * ntl + w]++)
+            return plan_fail(msg, msg_len, "J=%d: misplaced or duplicate look-ahead partial p=%d w=%d", l.J, p, w);
+          if (gpf::pair_slot(p, w - 1, nt) + (size_t)T * T > (size_t)l.gc * ntl * T * T)
+            return plan_fail(msg, msg_len, "J=%d: partial slot outside the group's buffer", l.J);
+        } else if (role == gpf::ROLE_WHOLE) {
+          if (w < 0 || w >= ntl) return plan_fail(msg, msg_len, "J=%d block %u decodes out of range", l.J, b);
+          ++whole[(size_t)p * ntl + w];
+        } else {
+          return plan_fail(msg, msg_len, "J=%d block %u: role %d in a lead launch", l.J, b, role);
+        }
+        ++wgs;
+      }
+      for (int q = 0; q < l.gc; ++q) {
+        if (syrk[q] != 1 || syp[q] != (l.J + 2 <= nt - 1 ? 1 : 0))
+          return plan_fail(msg, msg_len, "J=%d particle %d: %d SYRK, %d partial SYRK workgroups", l.J, q, syrk[q], syp[q]);
+        syrk_wgs += 1;
+        for (int w = 0; w < ntl; ++w) {
+          if (whole[(size_t)q * ntl + w] != 1 || pla[(size_t)q * ntl + w] != (w >= 1 ? 1 : 0))
+            return plan_fail(msg, msg_len, "J=%d particle %d tile %d: %d runs, %d partials", l.J, q, w,
+                             whole[(size_t)q * ntl + w], pla[(size_t)q * ntl + w]);
+          ++whole_tiles;
+        }
+      }
+      continue;
+    }
     std::vector<int> lawg((size_t)l.gc, 0);
     for (unsigned b = 0; b < l.grid; ++b) {
       int p = -1, w = -1, sidx = -1;
@@ -1492,6 +1621,8 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
       else return plan_fail(msg, msg_len, "J=%d tile %d: %d whole runs and %d pieces", l.J, t, whole[t], np);
     }
   }
+  for (int g = 0; g < ng; ++g)
+    if (pair_prev[g] == 1) return plan_fail(msg, msg_len, "group %d ends with a lead launch", g);
   for (int a = 0; a < ng; ++a)
     for (int b2 = a + 1; b2 < ng; ++b2) {
       if (plo[a] < phi[a] && plo[b2] < phi[b2] && plo[a] < phi[b2] && plo[b2] < phi[a])
@@ -1509,7 +1640,10 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     stats[6] = ng;
     stats[7] = diag_wgs;
     stats[8] = syrk_wgs;
-    stats[9] = 0;
+    long long pairs = 0;
+    for (const StepLaunch& l : plan) pairs += l.pair == 1;
+    stats[9] = 0;      // not persistent
+    stats[10] = pairs;  // lead launches (paired block columns)
   }
   return GPF_OK;
 }

@@ -19,7 +19,7 @@ LIB_PATH = Path(os.environ.get("GPFIT_LIB", PKG_DIR / "libgpfit.so"))
 GPF_OK, GPF_NOT_PD, GPF_HIP_ERROR, GPF_BAD_ARG = 0, 1, 2, 3
 GPF_COMM_RCCL, GPF_COMM_HOST = 1, 2
 GPF_OP_SUM, GPF_OP_MAX = 0, 1
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int)
@@ -105,13 +105,13 @@ def plan_check(particles, nt):
     """Host-side check of the k_step dispatch plan (gpf_plan_check); raises AssertionError
     naming the first violation, else returns the stats dict. Reads the GPF_* environment."""
     lib = load_library()
-    stats = (ctypes.c_longlong * 10)()
+    stats = (ctypes.c_longlong * 11)()
     msg = ctypes.create_string_buffer(256)
     rc = lib.gpf_plan_check(int(particles), int(nt), stats, msg, 256)
     if rc != GPF_OK:
         raise AssertionError(f"plan_check(pc={particles}, nt={nt}): {msg.value.decode()}")
     keys = ("launches", "workgroups", "whole_tiles", "split_tiles", "S", "Smax", "groups", "diag_workgroups",
-            "syrk_workgroups", "persistent")
+            "syrk_workgroups", "persistent", "lead_launches")
     return dict(zip(keys, list(stats)))
 
 

@@ -43,7 +43,7 @@ extern "C" {
 #define GPF_HIP_ERROR 2
 #define GPF_BAD_ARG 3
 
-#define GPF_ABI_VERSION 1
+#define GPF_ABI_VERSION 2  /* 2 (r6): gpf_plan_check's stats carry 11 entries */
 
 typedef struct gpf_ctx gpf_ctx;
 
@@ -226,9 +226,14 @@ const char* gpf_build_info(void);
  * kernel's own decoder (gpf::p_decode): every (block column, particle, tile) exactly once, one
  * SYRK item per particle and block column 1 .. nt-2, and every item's inputs produced by items
  * earlier in its queue (what makes the persistent launch deadlock-free).
- * stats (nullable, 10 entries): launches, workgroups (persistent: items), whole tiles, split
+ * Paired block columns (GPF_PAIR; gpf::pair_decode): a lead launch J carries, per particle, every
+ * tile of column J once, its SYRK workgroup, one look-ahead partial per tile of column J+1 that
+ * exists (the tile's 8 or 16 ids behind, on the same XCD), and the partial SYRK of block J+2; it is
+ * followed on its stream by the follow launch J+1, whose tiles read those partials (slots inside
+ * the group's buffer).
+ * stats (nullable, 11 entries): launches, workgroups (persistent: items), whole tiles, split
  * tiles, S (all-tile split factor), largest split factor, particle groups, diagonal
- * workgroups, SYRK workgroups (items), persistent (0/1). Returns GPF_OK, or
+ * workgroups, SYRK workgroups (items), persistent (0/1), lead launches of paired block columns. Returns GPF_OK, or
  * GPF_BAD_ARG with a description of the first violation in msg. */
 int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len);
 

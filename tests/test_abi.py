@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_tile():
     import gpfit._lib as L
     lib = L.load_library()
-    assert lib.gpf_version() == L.ABI_VERSION == 1
+    assert lib.gpf_version() == L.ABI_VERSION == 2
     assert lib.gpf_tile() == 128
 
 

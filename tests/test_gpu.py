@@ -388,6 +388,47 @@ def test_not_pd_past_block3_in_prediction(ctx):
     assert _rel(mu, m0) < RTOL_MU_SD and _rel(sd, s0) < RTOL_MU_SD
 
 
+@pytest.mark.parametrize("N,d,P,groups,paired", [(4096, 3, 64, None, True), (4096, 3, 32, None, True),
+                                                  (3900, 2, 16, None, True), (512, 2, 8, None, True),
+                                                  (2048, 4, 24, "1", True), (2049, 3, 40, "2", False)])
+def test_paired_block_columns_bitwise(ctx, monkeypatch, N, d, P, groups, paired):
+    """Paired block columns (gpf::pair_decode; r6): the lead launch J runs block column J+1's GEMMs
+    over the columns < J beside the tiles that stream the same panels, the follow launch J+1 finishes
+    from those partials. Every element sees the same MFMAs in the same order (a chain split at a
+    chunk boundary with an exact store and reload), so scores, mean and sd are bitwise those of the
+    unpaired launches: C (64 particles, two groups), D's share, an odd block-column count (nt = 31),
+    the smallest paired nt (4), one group of 24, and 40 particles in two groups of 20 (not multiples
+    of 8: unpaired, same results). Deterministic over two runs."""
+    rng = np.random.default_rng(N + P)
+    x = rng.uniform(size=(d, N))
+    y = np.sum(np.sin(2 * np.pi * x), axis=0) + 0.1 * rng.standard_normal(N)
+    e = rng.uniform(0.05, 0.2, size=N)
+    s, ex = ref_cpu.sigma_grid()
+    lo, hi = ref_cpu.search_bounds(x)
+    ctx.set_data(x, y, e)
+    ctx.set_grid(s, ex, lo, hi)
+    Q = rng.uniform(0.1, 0.5, size=(P, d))
+    monkeypatch.setenv("GPF_PERSIST", "0")
+    monkeypatch.setenv("GPF_EARLY_DIAG", "0")  # (pairs run with the fused diagonal factor, unsplit)
+    monkeypatch.setenv("GPF_SPLIT_K", "1")
+    if groups:
+        monkeypatch.setenv("GPF_GROUPS", groups)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("GPF_PAIR", mode)
+        out[mode] = ctx.eval_batch(Q, want_mu_sd=True)
+    again = ctx.eval_batch(Q, want_mu_sd=True)
+    for a, b, c in zip(out["0"], out["1"], again):
+        np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(b, c)
+    import gpfit
+    st = gpfit.plan_check(P, (N + 127) // 128)
+    assert (st["lead_launches"] > 0) == paired, st
+    if N <= 2049:
+        mo, so = ref_cpu.GP_train_identity(x, y, e, Q[0])
+        assert _rel(out["1"][1][0], mo) < RTOL_MU_SD and _rel(out["1"][2][0], so) < RTOL_MU_SD
+
+
 def test_sentinels_never_reach_gpu_and_mix_with_live_particles(ctx, f2):
     x, y, e = f2["c0_x"], f2["c0_y"], f2["c0_e"]
     lo, hi = f2["c0_lo"], f2["c0_hi"]

@@ -32,6 +32,8 @@ ENVS = [
     {"GPF_SPLIT_K": "3", "GPF_SPLIT_K_SLOTS": "1000", "GPF_SPLIT_K_MINCH": "1", "GPF_GROUPS": "2"},
     {"GPF_REORDER": "0"}, {"GPF_REORDER": "0", "GPF_EARLY_DIAG": "1"},  # r4: the reordered dispatch off
     {"GPF_EARLY_DIAG": "1", "GPF_GROUPS": "2"},                         # reordered where it fits, two groups
+    {"GPF_PAIR": "1"}, {"GPF_PAIR": "1", "GPF_GROUPS": "1"},            # r6: paired block columns
+    {"GPF_PAIR": "1", "GPF_GROUPS": "3"}, {"GPF_PAIR": "1", "GPF_EARLY_DIAG": "0", "GPF_GROUPS": "1"},
 ]
 
 
@@ -39,7 +41,8 @@ ENVS = [
 def env(monkeypatch):
     def apply(kv):
         for k in ("GPF_GROUPS", "GPF_SPLIT_K", "GPF_STEP_GROUP", "GPF_EARLY_DIAG",
-                  "GPF_DEFER_SYRK", "GPF_SPLIT_K_SLOTS", "GPF_SPLIT_K_MINCH", "GPF_PERSIST", "GPF_REORDER"):
+                  "GPF_DEFER_SYRK", "GPF_SPLIT_K_SLOTS", "GPF_SPLIT_K_MINCH", "GPF_PERSIST", "GPF_REORDER",
+                  "GPF_PAIR"):
             monkeypatch.delenv(k, raising=False)
         if kv and "GPF_PERSIST" not in kv:  # the launch-plan knobs: on the per-block-column launches
             monkeypatch.setenv("GPF_PERSIST", "0")
@@ -51,7 +54,7 @@ def env(monkeypatch):
 @pytest.mark.parametrize("kv", ENVS, ids=lambda kv: ",".join(f"{k}={v}" for k, v in kv.items()) or "default")
 def test_every_tile_has_exactly_one_finisher(env, kv):
     env(kv)
-    seen_split = seen_groups = seen_persist = 0
+    seen_split = seen_groups = seen_persist = seen_pairs = 0
     for nt in NT:
         # all chunk sizes up to 64 at small nt; a spread at large nt (the check is O(pc nt^2))
         pcs = range(1, 65) if nt <= 33 else (1, 2, 7, 8, 15, 16, 17, 31, 32, 33, 63, 64)
@@ -69,16 +72,25 @@ def test_every_tile_has_exactly_one_finisher(env, kv):
             assert st["diag_workgroups"] in (0, pc * nt if nt > 1 else 0)
             # deferred diagonal update: one SYRK workgroup per particle in launches 1 .. nt-2,
             # except under the all-tile split (which keeps the per-tile look-ahead)
-            assert st["syrk_workgroups"] in (0, pc * max(0, nt - 2))
+            # (paired block columns: only the lead launches carry them; the follow launch's critical
+            # tile finishes the diagonal block the lead's partial SYRK started)
+            # (the C-side check counts them per launch: one per particle in every lead launch, none in a
+            # follow launch; groups whose size is not a multiple of 8 stay unpaired)
+            assert st["syrk_workgroups"] in (0, pc * max(0, nt - 2)) or st["lead_launches"] > 0
             assert st["syrk_workgroups"] == 0 or st["S"] == 1
             seen_split += st["split_tiles"] > 0
             seen_groups += st["groups"] > 1
+            seen_pairs += st["lead_launches"] > 0
+            if st["lead_launches"]:  # leads at odd J <= nt-2 in every paired group
+                assert st["lead_launches"] % ((nt - 1) // 2) == 0 and st["lead_launches"] <= st["groups"] * ((nt - 1) // 2)
     if kv.get("GPF_SPLIT_K") or not kv:
         assert seen_split, "the sweep never reached a split launch"
-    if "GPF_GROUPS" in kv:
+    if kv.get("GPF_GROUPS", "1") != "1":
         assert seen_groups, "the sweep never reached a multi-group plan"
     if not kv or kv.get("GPF_PERSIST") == "1":
         assert seen_persist, "the sweep never reached the persistent factorisation"
+    if kv.get("GPF_PAIR") == "1" and kv.get("GPF_EARLY_DIAG") != "1":
+        assert seen_pairs, "the sweep never reached a paired plan"
 
 
 def test_default_plans_of_the_baseline_configs(env):
