@@ -225,8 +225,12 @@ __device__ __forceinline__ void dl_load_s(const void* base, uint32_t off, double
   else
     asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(base), "{m0}"(m) : "memory");
 }
+// B panels streamed once per launch (the k_step tiles' row / column panels) load non-temporal, so
+// they stop evicting the launch's shared A panels (row panel J) from the XCD's L2: r6, same box,
+// config C 1360 -> 1387 evals/s, the clock 2136 -> 2177 MHz, FETCH 2.25 -> 2.01 GB per group launch
+// (profiles/r6/ab_b_nt.txt). -DGPF_B_NT=0 builds the default policy everywhere (A/B).
 #ifndef GPF_B_NT
-#define GPF_B_NT 0
+#define GPF_B_NT 1
 #endif
 
 // Slot swizzle of the [r][k] panels: k-pair kp of row r sits in slot kp ^ dl_sw(r). An MFMA
@@ -263,7 +267,7 @@ __device__ __forceinline__ void dl_row_offsets(int lane, uint32_t (&o)[4]) {
 // (8 row blocks) x one 16-column slab, so a k-step is 8 A reads, 1 B read and 8 MFMAs.
 // NS: LDS stages (2: double-buffered, the default; 3-4 for one-workgroup-per-CU launches, where
 // the next chunk's transfer has less time behind one chunk of MFMAs than two workgroups give it)
-template <bool NN, bool NEG, int NS = 2>
+template <bool NN, bool NEG, int NS = 2, bool BNT = true>
 struct DenseRun {
   static_assert(NS >= 2 && NS <= 4, "DenseRun stages");
   static constexpr int MBR = Geo<128>::MBR;  // 8
@@ -302,7 +306,7 @@ struct DenseRun {
     for (int u = 0; u < 2; ++u) {
       const int blk = blk0 + u;
       dl_load_s(Ac, ga[u], sbuf + blk * 8 * DL_KC);
-      dl_load_s<GPF_B_NT != 0>(Bc, gb[u], sbuf + 128 * DL_KC + (NN ? blk * 128 : blk * 8 * DL_KC));
+      dl_load_s<BNT && GPF_B_NT != 0>(Bc, gb[u], sbuf + 128 * DL_KC + (NN ? blk * 128 : blk * 8 * DL_KC));
     }
   }
 
@@ -396,7 +400,8 @@ struct DenseRun {
 // pattern each. Each run is its own straight-line loop (one pattern per loop keeps the register
 // allocation of the dense loop); exactly the MFMAs tri_live admits are issued, so results are
 // bitwise those of per-block skipping. Every wave still passes one barrier per chunk.
-template <bool NN, bool NEG = false, int TRI = TRI_NONE, int NS = 2>
+// BNT: the B panel loads non-temporal (a panel read once per launch; GPF_B_NT)
+template <bool NN, bool NEG = false, int TRI = TRI_NONE, int NS = 2, bool BNT = true>
 __device__ __forceinline__ void gemm_stream_dl(Acc<128>& acc, const double* __restrict__ Ap, int lda, const double* __restrict__ Bp,
                                int ldb, int K, double* smem, const Quad<128>& qd) {
   const int nch = K / DL_KC;
@@ -404,7 +409,7 @@ __device__ __forceinline__ void gemm_stream_dl(Acc<128>& acc, const double* __re
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const double* Ar = uniform_ptr(Ap);  // scalar bases
   const double* Br = uniform_ptr(Bp);
-  const DenseRun<NN, NEG, NS> dr(qd, lda, ldb, wave);
+  const DenseRun<NN, NEG, NS, BNT> dr(qd, lda, ldb, wave);
   dr.template issue<0>(Ar, Br, ldb, 0, smem);
   if constexpr (NS >= 3) {  // the first NS-1 chunks in flight
     if (nch > 1) dr.template issue<1>(Ar, Br, ldb, 1, smem);

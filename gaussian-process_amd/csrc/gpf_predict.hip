@@ -6,6 +6,9 @@
 #pragma once
 #include "gpf_common.hip"
 
+#ifndef GPF_VSQ_BNT
+#define GPF_VSQ_BNT 0  // (K_s column tiles are re-read by every row tile: default cache policy)
+#endif
 namespace gpf {
 
 // Row tile t of V = U K_s (GP_func.py:38: v = solve(L, K_s), with U = L^-1), reduced per column
@@ -31,7 +34,7 @@ __global__ __launch_bounds__(Geo<T>::NTH, 4) void k_predict_vsq(int Npad, const 
   // U is lower triangular: row tile t needs columns [0, (t+1) * 128), and in the last 128 of them
   // row block mi only the chunks c <= mi add non-zeros (TRI_A_LAST skips the chunks c >= 4 for the
   // row blocks mi < 4: 16 of the diagonal block's 64 chunk x row block MFMA groups, exact zeros; r5)
-  gemm_stream_dl<true, false, TRI_A_LAST>(acc, U + (size_t)t * T * Npad, Npad, Ks + (size_t)q * T, ldks, (t + 1) * T,
+  gemm_stream_dl<true, false, TRI_A_LAST, 2, GPF_VSQ_BNT != 0>(acc, U + (size_t)t * T * Npad, Npad, Ks + (size_t)q * T, ldks, (t + 1) * T,
                                           smem, qd);
   constexpr int MBR = Geo<T>::MBR;
   const double* zt = z + (size_t)t * T + (qd.lane >> 4);
