@@ -76,7 +76,8 @@ __host__ __device__ __forceinline__ void step_tile(int b, int P, int ntl, int gr
 // (r5: the critical-tile split SPLIT_CRIT = 2 of rounds 1-4 — off by default since round 2 and
 // slower again on B in r5, profiles/r5/ab_split_crit_B.txt — and its reduction tree were removed.)
 enum { SPLIT_NONE = 0, SPLIT_ALL = 1 };
-enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2, ROLE_DIAG = 3, ROLE_SYRK = 4, ROLE_LA = 5, ROLE_PLA = 6, ROLE_SYRKP = 7 };
+enum { ROLE_IDLE = 0, ROLE_WHOLE = 1, ROLE_PIECE = 2, ROLE_DIAG = 3, ROLE_SYRK = 4, ROLE_LA = 5, ROLE_PLA = 6, ROLE_SYRKP = 7,
+       ROLE_LPIECE = 8 };
 
 // Early diagonal factor (k_step<SPLIT, ED = 1>; the host chooses it for launches that leave
 // workgroup slots idle): launch J starts with P extra workgroups that factor diagonal
@@ -282,6 +283,59 @@ __device__ __forceinline__ void pair_start_sync(int J, int u, int h, int p, int 
 
 // the partial slot of tile w' (follow-launch numbering; the lead's tile w + 1) of particle p
 __host__ __device__ __forceinline__ size_t pair_slot(int p, int wf, int nt) { return ((size_t)p * (nt - 1) + wf) * T * T; }
+
+// ----------------------------------------------------------------------------
+// All-tile look-ahead in pieces (r6; k_step<SPLIT_NONE, 1>: the early-diagonal launches of config B,
+// fewer tiles than workgroup slots). There a launch lasts as long as its longest
+// item: from J = 3 the deep non-critical tiles, one depth-128J GEMM on one CU each (~95 us at J = 5,
+// against ~60 us of work per CU; profiles/r5/crit_B_r5.txt). Here launch J (J >= 1) also runs, in
+// pieces of at most LALL_PB 128-blocks each (ROLE_LPIECE), every GEMM of launch J+1 over the columns
+// that are final before launch J — column J+1's L tiles I >= J+2 over [0, J) (covariance seed in
+// piece 0), its U tiles K < J over [K, J), and the diagonal update of block J+2 over [0, J) — to
+// partial slots; launch J+1's tiles and SYRK workgroup then sum their item's partials in piece
+// order, run the one remaining 128-block (the columns of block J) and finish as before. Every item
+// of a launch is then at most LALL_PB blocks of GEMM (or one block plus a finish), and the launch's
+// chain is the diagonal factor and the critical tile's finish. The partials of launch J go to parity
+// J & 1 of the buffer, so launch J+1 reads one half while it writes the other. Deterministic; the sum
+// of partials rounds differently from one MFMA chain (within 1e-12 of the unsplit factor,
+// test_all_tile_lookahead_pieces).
+constexpr int LALL_PB = 2;
+// (the look-ahead launches pass P and the slots per particle packed in k_step's ptag)
+__host__ __device__ __forceinline__ int lall_tag(int P, int smax) { return (P << 16) | smax; }
+__host__ __device__ __forceinline__ int P_of(int tag) { return tag >> 16; }
+__host__ __device__ __forceinline__ int smax_of(int tag) { return tag & 0xffff; }
+__host__ __device__ __forceinline__ int lall_items(int J, int nt) {  // items launch J produces, per particle
+  return J < 1 || J + 1 > nt - 1 ? 0 : (nt - 2 - J) + J + (J + 2 <= nt - 1 ? 1 : 0);
+}
+__host__ __device__ __forceinline__ int lall_depth(int J, int it, int nt) {  // in 128-blocks
+  const int nLc = nt - 2 - J;
+  return it < nLc ? J : it < nLc + J ? J - (it - nLc) : J;
+}
+__host__ __device__ __forceinline__ int lall_np(int J, int it, int nt) { return (lall_depth(J, it, nt) + LALL_PB - 1) / LALL_PB; }
+__host__ __device__ __forceinline__ int lall_off(int J, int it, int nt) {
+  int o = 0;
+  for (int i = 0; i < it; ++i) o += lall_np(J, i, nt);
+  return o;
+}
+__host__ __device__ __forceinline__ int lall_total(int J, int nt) { return lall_off(J, lall_items(J, nt), nt); }
+// slot of piece s of item it produced by launch J for particle p (P particles in the group, smax slots
+// per particle and parity)
+__host__ __device__ __forceinline__ size_t lall_slot(int J, int it, int s, int p, int P, int nt, int smax) {
+  return ((size_t)((J & 1) * P + p) * smax + lall_off(J, it, nt) + s) * T * T;
+}
+// Workgroup b of a look-ahead launch past its diagonal, SYRK and tile workgroups (r = b - those): piece
+// s of item it of particle p (items in order, their pieces in order, particles fastest)
+__host__ __device__ __forceinline__ void lall_decode(int r, int J, int P, int nt, int& p, int& it, int& s) {
+  p = r % P;
+  int q = r / P;
+  const int ni = lall_items(J, nt);
+  for (it = 0; it < ni - 1; ++it) {
+    const int n = lall_np(J, it, nt);
+    if (q < n) break;
+    q -= n;
+  }
+  s = q;
+}
 
 // LDS of a k_step workgroup (doubles): the GEMM stages (DL_STAGE), the diagonal factor
 // (DB_LDS), the staged U_JJ of the triangular finishes (TRI_LDS) with z_J behind
@@ -900,6 +954,80 @@ __device__ __forceinline__ void syrkp_item(int J, int p, int Npad, double* __res
   syrk_tile<false>(Lp + (size_t)I * T * ld + (size_t)I * T, ld, Lp + (size_t)I * T * ld, Npad, J * T, lds, qd);
 }
 
+// acc += a partial in store_node's layout (its 16-B units added as they arrive: no second accumulator set)
+__device__ __forceinline__ void add_node(Acc<T>& acc, const double* slot) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(slot), 0, T * T * 8, 0x00020000);
+  const int wb = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * NODE_WAVE, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int mi = 0; mi < Acc<T>::MBR; ++mi)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const d2 v = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, wb + (mi * 2 + h) * 1024, 0));
+      acc.v[mi][0][2 * h] = acc.v[mi][0][2 * h] + v.x;
+      acc.v[mi][0][2 * h + 1] = acc.v[mi][0][2 * h + 1] + v.y;
+    }
+}
+// the summed partials of item it (launch J-1's pieces, in piece order)
+__device__ __forceinline__ void lall_seed(Acc<T>& acc, const double* lb, int J, int it, int p, int P, int nt, int smax) {
+  const int np = lall_np(J - 1, it, nt);
+  const double* s0 = lb + lall_slot(J - 1, it, 0, p, P, nt, smax);
+  load_node(acc, s0);
+  for (int s = 1; s < np; ++s) add_node(acc, s0 + (size_t)s * T * T);
+}
+
+// ROLE_LPIECE: piece s of item it of launch J (see lall_items)
+__device__ __forceinline__ void lall_piece(int J, int it, int s, int p, int P, int nt, int Npad, const double* __restrict__ Lb,
+                                           const double* __restrict__ Ub, int N, const double* __restrict__ x,
+                                           const double* __restrict__ ls, int d, double* __restrict__ lb, int smax,
+                                           double* lds) {
+  const size_t ld = (size_t)Npad;
+  const int nLc = nt - 2 - J, depth = lall_depth(J, it, nt);
+  const int b0 = s * LALL_PB, nb = min(LALL_PB, depth - b0);
+  const double* Lp = Lb + (size_t)p * ld * ld;
+  const Quad<T> qd;
+  Acc<T> acc;
+  if (it < nLc) {  // L tile I of column J+1: (A_{J+1,I} seed) - L_{J+1,[b0,b0+nb)} L_{I,[b0,b0+nb)}^T
+    const int I = J + 2 + it;
+    if (s == 0) cov_tile_acc(acc, qd, x, ls + (size_t)p * d, d, N, J + 1, I, lds);
+    else acc.zero();
+    gemm_stream_dl<false, true>(acc, Lp + (size_t)(J + 1) * T * ld + (size_t)b0 * T, Npad,
+                                Lp + (size_t)I * T * ld + (size_t)b0 * T, Npad, nb * T, lds, qd);
+  } else if (it < nLc + J) {  // U tile K: L_{J+1,K+[b0,b0+nb)} U_{K+[b0,b0+nb),K} (U_KK lower triangular)
+    const int K = it - nLc;
+    const double* Up = Ub + (size_t)p * ld * ld;
+    const double* A = Lp + (size_t)(J + 1) * T * ld + (size_t)(K + b0) * T;
+    const double* B = Up + (size_t)(K + b0) * T * ld + (size_t)K * T;
+    acc.zero();
+    if (s == 0) gemm_stream_dl<true, false, TRI_B_KGEC>(acc, A, Npad, B, Npad, nb * T, lds, qd);
+    else gemm_stream_dl<true, false>(acc, A, Npad, B, Npad, nb * T, lds, qd);
+  } else {  // the diagonal update of block J+2 (lower part; piece 0 seeded with A_{J+2,J+2})
+    const double* Ar = Lp + (size_t)(J + 2) * T * ld + (size_t)b0 * T;
+    if (s == 0) acc.load(qd, Lp + (size_t)(J + 2) * T * ld + (size_t)(J + 2) * T, ld);
+    else acc.zero();
+    gemm_stream_dl<false, true, TRI_C_LOWER>(acc, Ar, Npad, Ar, Npad, nb * T, lds, qd);
+  }
+  store_node(acc, lb + lall_slot(J, it, s, p, P, nt, smax), qd);
+}
+
+// SYRK workgroup of a look-ahead launch J >= 2: S = A_{J+1,J+1} - L_{J+1,<J} L_{J+1,<J}^T from launch
+// J-1's pieces over [0, J-1) (item nt-2) plus block column J-1, published like syrk_item's.
+__device__ __forceinline__ void lall_syrk_item(int J, int p, int P, int nt, int Npad, double* __restrict__ Lb,
+                                               int* __restrict__ yflag, const double* __restrict__ lb, int smax,
+                                               double* lds) {
+  const size_t ld = (size_t)Npad;
+  const int I = J + 1;
+  double* Lp = Lb + (size_t)p * ld * ld;
+  const Quad<T> qd;
+  Acc<T> acc;
+  lall_seed(acc, lb, J, nt - 2, p, P, nt, smax);
+  const double* Ar = Lp + (size_t)I * T * ld + (size_t)(J - 1) * T;
+  gemm_stream_dl<false, true, TRI_C_LOWER>(acc, Ar, Npad, Ar, Npad, T, lds, qd);
+  acc.store_wt(qd, Lp + (size_t)I * T * ld + (size_t)I * T, ld);  // (the upper half rewrites A's own values)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(yflag + p, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Tile w of block column J of particle p (the unit of work of k_step); role from step_decode.
 //   L tile (I = J+1+w):  D = A_IJ^T - L_J,<J L_I,<J^T  (the transposed panel C^T, so that each
 //                        wave holds all 128 k of the triangular multiply for its 16 rows of C)
@@ -917,13 +1045,16 @@ __device__ __forceinline__ void step_item(int role, int J, int w, int p, int nt,
                                           double* __restrict__ part, unsigned* __restrict__ cnt, int* sflag,
                                           const int* __restrict__ dflag, const int* __restrict__ yflag, int defer,
                                           int spins, int la, const double* __restrict__ lab, int pair,
-                                          const double* __restrict__ pb, double* lds) {
+                                          const double* __restrict__ pb, int ptag, double* lds) {
   const int tid = threadIdx.x;
   const int nL = nt - 1 - J;
   // (paired block columns exist only in the fused-diagonal schedule: the other instantiations keep
   // their register allocation)
   constexpr bool PAIRS = SPLIT == SPLIT_NONE && !ED;
   const bool follow = PAIRS && pair == 2;
+  // all-tile look-ahead (early-diagonal launches): this launch's tiles seed from launch J-1's pieces
+  constexpr bool LALL = SPLIT == SPLIT_NONE && ED;
+  const bool lseed = LALL && (pair & 2) && J >= 2;
   const size_t ld = (size_t)Npad;
   if (SPLIT != SPLIT_NONE && role == ROLE_IDLE) return;
   double* Lp = Lb + (size_t)p * ld * ld;
@@ -965,6 +1096,11 @@ if (w < nL)
       acc.load(qd, lab + la_slot(p, J - 1), T);
       gemm_stream_dl<false, true>(acc, Lp + (size_t)J * T * ld + k0, Npad, Lp + (size_t)I * T * ld + k0, Npad, J * T - k0,
                                   lds, qd);
+    } else if (lseed) {
+      // the pieces of launch J-1 (seed and the columns < J-1), then block column J-1
+      lall_seed(acc, pb, J, w, p, P_of(ptag), nt, smax_of(ptag));
+      gemm_stream_dl<false, true>(acc, Lp + (size_t)J * T * ld + (size_t)(J - 1) * T, Npad,
+                                  Lp + (size_t)I * T * ld + (size_t)(J - 1) * T, Npad, T, lds, qd);
     } else if (follow) {
       // follow launch: the lead's partial (seed and the columns < J-1), then block column J-1
       load_node(acc, pb + pair_slot(p, w, nt));
@@ -1028,7 +1164,11 @@ if (w < nL)
     double* Ujk = Up + (size_t)J * T * ld + (size_t)K * T;
     Acc<T> acc;
     // W = L_J,[K,J) U_[K,J),K (U_KK is lower triangular: the wave's first chunks add zeros)
-    if (follow && K < J - 1) {
+    if (lseed && K < J - 1) {
+      lall_seed(acc, pb, J, w, p, P_of(ptag), nt, smax_of(ptag));
+      gemm_stream_dl<true, false>(acc, Lp + (size_t)J * T * ld + (size_t)(J - 1) * T, Npad,
+                                  Up + (size_t)(J - 1) * T * ld + (size_t)K * T, Npad, T, lds, qd);
+    } else if (follow && K < J - 1) {
       // follow launch: the lead's partial over [K, J-1), then block row J-1 of U's column panel K
       load_node(acc, pb + pair_slot(p, w, nt));
       gemm_stream_dl<true, false>(acc, Lp + (size_t)J * T * ld + (size_t)(J - 1) * T, Npad,
@@ -1113,12 +1253,22 @@ __global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_step(int J, i
   __shared__ int sflag;
   int p, w, sidx = 0;
   constexpr bool PAIRS = SPLIT == SPLIT_NONE && !ED;
-  int uh = 0;
-  const int role = (PAIRS && pair == 1)
-                       ? pair_decode((int)blockIdx.x, J, P, nt, p, w, &uh)
-                       : step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, SPLIT != SPLIT_ALL && sy,
-                                            SPLIT == SPLIT_NONE && ED && (la & 1) && !sy, p, w, sidx,
-                                            SPLIT == SPLIT_NONE && ED && (la & 32) != 0);
+  int uh = 0, lit = -1;
+  constexpr bool LALL = SPLIT == SPLIT_NONE && ED;
+  // look-ahead launches: the pieces follow the diagonal, SYRK and tile workgroups (lall_decode)
+  const int nstd = (ED && ed ? P : 0) + (SPLIT != SPLIT_ALL && sy ? P : 0) + P * (nt - 1);
+  int role;
+  if (PAIRS && pair == 1) {
+    role = pair_decode((int)blockIdx.x, J, P, nt, p, w, &uh);
+  } else if (LALL && (pair & 1) && (int)blockIdx.x >= nstd) {
+    lall_decode((int)blockIdx.x - nstd, J, P, nt, p, lit, sidx);
+    w = -1;
+    role = ROLE_LPIECE;
+  } else {
+    role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, SPLIT != SPLIT_ALL && sy,
+                              SPLIT == SPLIT_NONE && ED && (la & 1) && !sy, p, w, sidx,
+                              SPLIT == SPLIT_NONE && ED && (la & 32) != 0);
+  }
 #ifdef GPF_CHECK
   // diagnostic build (-DGPF_CHECK): every index the workgroup derives its addresses from, checked
   // against the launch's extents before any access (an out-of-range role prints and does nothing)
@@ -1130,6 +1280,9 @@ __global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_step(int J, i
     else if (role == ROLE_PLA) ok = ok && PAIRS && pair == 1 && pb != nullptr && w >= 1 && w < nt - 1 && J >= 1 &&
                                      (w >= nt - 1 - J || J + 1 + w < nt);
     else if (role == ROLE_SYRKP) ok = ok && PAIRS && pair == 1 && w == 1 && J >= 1 && J + 2 <= nt - 1;
+    else if (role == ROLE_LPIECE) ok = ok && LALL && pb != nullptr && lit >= 0 && lit < lall_items(J, nt) && sidx >= 0 &&
+                                       sidx < lall_np(J, lit, nt) && P_of(ptag) == P &&
+                                       lall_off(J, lit, nt) + sidx < smax_of(ptag);
     else if (role != ROLE_IDLE) ok = ok && w >= 0 && w < nt - 1 && sidx >= 0 && (pair != 2 || pb != nullptr) &&
                                      sidx < (SPLIT == SPLIT_ALL ? split_all_pieces(J, w, nt, S) : S) && sidx < S2 &&
                                      (role != ROLE_PIECE || (part != nullptr && cnt != nullptr && S > 1)) &&
@@ -1143,7 +1296,11 @@ __global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_step(int J, i
   }
 #endif
   if (PAIRS && pair == 1 && pstart) pair_start_sync(J, role == ROLE_SYRK ? 0 : w, uh, p, nt, pstart, ptag);
-  if (PAIRS && role == ROLE_PLA) {
+  if (LALL && role == ROLE_LPIECE) {
+    lall_piece(J, lit, sidx, p, P, nt, Npad, Lb, Ub, N, x, ls, d, pb, smax_of(ptag), lds);
+  } else if (LALL && role == ROLE_SYRK && (pair & 2) && J >= 2) {
+    lall_syrk_item(J, p, P, nt, Npad, Lb, yflag, pb, smax_of(ptag), lds);
+  } else if (PAIRS && role == ROLE_PLA) {
     pla_item(J, w, p, nt, Npad, Lb, Ub, N, x, ls, d, pb, lds);
   } else if (PAIRS && role == ROLE_SYRKP) {
     syrkp_item(J, p, Npad, Lb, lds);
@@ -1167,7 +1324,7 @@ __global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_step(int J, i
                     dflag + p, J);
   } else {
     step_item<SPLIT, ED>(role, J, w, p, nt, Npad, Lb, Ub, yb, s2p, szp, info, N, x, ls, d, S, S2, sidx, part, cnt, &sflag,
-                         dflag, yflag, defer, spins, la, lab, pair, pb, lds);
+                         dflag, yflag, defer, spins, la, lab, pair, pb, ptag, lds);
   }
   span.stop(clk);
 #ifdef GPF_WG_TRACE

@@ -88,6 +88,8 @@ struct gpf_ctx {
   size_t pb_cap = 0;
   int* d_pstart = nullptr;     // ... and the partners' start words (gpf::pair_start_sync), PAIR_HMAX per tile
   size_t pstart_cap = 0;
+  double* d_lb = nullptr;      // all-tile look-ahead pieces (gpf::lall_slot): two parities x particles x smax slots
+  size_t lb_cap = 0;
   int fact_seq = 0;            // factorisations run (tags the start words)
   double* d_szp = nullptr;
   double* d_ls = nullptr;
@@ -264,6 +266,9 @@ static void free_work(gpf_ctx* c) {
   hipFree(c->d_pstart);
   c->d_pstart = nullptr;
   c->pstart_cap = 0;
+  hipFree(c->d_lb);
+  c->d_lb = nullptr;
+  c->lb_cap = 0;
   c->d_L = c->d_U = c->d_yb = c->d_s2p = c->d_szp = c->d_ls = c->d_mu = c->d_sd = c->d_loss = nullptr;
   c->d_info = nullptr;
   c->d_hist = nullptr;
@@ -467,6 +472,22 @@ static bool pair_on() {
   return on;
 }
 
+// All-tile look-ahead in pieces (gpf::lall_decode) for the early-diagonal launches without split
+// (config B: fewer tiles than workgroup slots, launches bound by their deepest tile). GPF_LA_ALL =
+// 0/1 overrides. It replaces the critical-tile look-ahead (GPF_LOOKAHEAD) and the reordered dispatch.
+static bool lall_on() {
+  bool on = false;
+  if (const char* s = getenv("GPF_LA_ALL")) on = atoi(s) != 0;
+  return on;
+}
+// (the pieces per particle and launch grow as nt J / 2: the look-ahead is for short factorisations)
+constexpr int LALL_NT_MAX = 32;
+static int lall_smax(int nt) {
+  int m = 1;
+  for (int J = 0; J < nt; ++J) m = std::max(m, gpf::lall_total(J, nt));
+  return m;
+}
+
 // Bound of the early-diagonal hand-off spin (gpf::wait_diag, polls of ~1 us): ~2 s by default;
 // GPF_WAIT_SPINS lowers it to exercise the timeout report (tests/test_gpu.py).
 static int wait_spins() {
@@ -474,6 +495,10 @@ static int wait_spins() {
   if (const char* s = getenv("GPF_WAIT_SPINS")) n = std::max(0, atoi(s));
   return n;
 }
+
+// Dynamic LDS that keeps a k_step launch at one workgroup per CU (its static LDS plus this exceeds
+// half of the CU's 160 KiB): GPF_STEP_1PERCU = 1 for every unsplit early-diagonal launch (A/B knob).
+static unsigned one_per_cu_lds(const struct StepLaunch& l);
 
 static int ensure_split(gpf_ctx* c, int tiles, int S) {
   const size_t pb = (size_t)tiles * S * T * T * 8, cb = (size_t)tiles * gpf::split_cnt_stride(c->nt) * 4;
@@ -542,6 +567,12 @@ struct StepLaunch {
   size_t part_off, cnt_off;
 };
 
+static unsigned one_per_cu_lds(const StepLaunch& l) {
+  const int on = getenv("GPF_STEP_1PERCU") ? atoi(getenv("GPF_STEP_1PERCU")) : 0;
+  if (!on || !l.ed || l.split != gpf::SPLIT_NONE) return 0;
+  return (unsigned)(82 * 1024 - gpf::STEP_LDS * 8);  // > 80 KiB in all: one per CU
+}
+
 static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& out) {
   out.clear();
   const int ng = num_groups(pc, nt);
@@ -580,6 +611,14 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
       l.grid = (S > 1 ? l.gc * nall : l.gc * (nt - 1)) + (l.ed ? l.gc : 0) + (l.sy ? l.gc : 0) +
                ((l.la & 1) && !l.sy ? l.gc : 0);  // (with SYRK workgroups the look-ahead rides on them)
       if (l.pair == 1) l.grid = (unsigned)(l.gc * gpf::pair_grid_per_particle(J, nt));
+      // all-tile look-ahead (early-diagonal launches): bit 0 this launch produces pieces for J+1, bit 1
+      // its tiles and SYRK workgroup consume launch J-1's
+      if (lall_on() && l.ed && S == 1 && l.defer && nt >= 4 && nt <= LALL_NT_MAX) {
+        l.pair = (gpf::lall_items(J, nt) > 0 ? 1 : 0) | (J >= 2 ? 2 : 0);
+        l.la = 0;
+        l.ro = 0;
+        l.grid = (unsigned)(l.gc * (nt - 1) + l.gc + (l.sy ? l.gc : 0) + l.gc * gpf::lall_total(J, nt));
+      }
       // one set of partial slots per group: groups run concurrently
       l.part_off = (size_t)l.p0 * (nt - 1) * Smax * T * T;
       l.cnt_off = (size_t)l.p0 * (nt - 1) * gpf::split_cnt_stride(nt);
@@ -704,7 +743,7 @@ static int run_factor(gpf_ctx* c, int pc) {
   bool any_la = false, any_pair = false;
   for (const StepLaunch& l : plan) {
     any_la = any_la || l.la != 0;
-    any_pair = any_pair || l.pair != 0;
+    any_pair = any_pair || (!l.ed && l.pair != 0);
   }
   const size_t pb_bytes = (size_t)pc * (nt - 1) * T * T * 8;
   if (any_pair && pb_bytes > c->pb_cap) {  // (nt >= 4: never under a graph capture)
@@ -724,6 +763,18 @@ static int run_factor(gpf_ctx* c, int pc) {
     GPF_HIP(c, hipMemset(c->d_pstart, 0, ps_bytes));  // (tags start at 1)
     c->pstart_cap = ps_bytes;
   }
+  bool any_lall = false;
+  for (const StepLaunch& l : plan) any_lall = any_lall || (l.ed && l.pair != 0);
+  const int smax = lall_smax(nt);
+  const size_t lb_bytes = (size_t)2 * pc * smax * T * T * 8;
+  if (any_lall && lb_bytes > c->lb_cap) {
+    clear_graphs(c);
+    hipFree(c->d_lb);
+    c->d_lb = nullptr;
+    c->lb_cap = 0;
+    GPF_HIP(c, hipMalloc(&c->d_lb, lb_bytes));
+    c->lb_cap = lb_bytes;
+  }
   const int seq = ++c->fact_seq & 0x7fffff;
   const bool psync = getenv("GPF_PAIR_SYNC") == nullptr || atoi(getenv("GPF_PAIR_SYNC")) != 0;
   if (any_la && 2 * (size_t)pc * T * T * 8 > c->la_cap) {  // (never under a graph capture: nt >= 4 only)
@@ -737,7 +788,9 @@ static int run_factor(gpf_ctx* c, int pc) {
   // test hook: the critical tiles that seed from the look-ahead wait ~0.3 ms first (gpf::step_item)
   const int la_delay = (getenv("GPF_LA_DELAY_TEST") && atoi(getenv("GPF_LA_DELAY_TEST")) != 0) ? 4 : 0;
   for (const StepLaunch& l : plan) {
-    const double fl = step_flops(l.J) + (l.pair == 1 ? pla_flops(l.J) : l.pair == 2 ? -pla_flops(l.J - 1) : 0.0);
+    // (paired columns: lead 1, follow 2; look-ahead pieces: bit 0 produces for J+1, bit 1 consumes J-1's —
+    // either way the GEMMs over the columns < J of block column J+1's tiles move one launch earlier)
+    const double fl = step_flops(l.J) + ((l.pair & 1) ? pla_flops(l.J) : 0.0) - ((l.pair & 2) ? pla_flops(l.J - 1) : 0.0);
     const int p0 = l.p0, gc = l.gc;
     hipStream_t st = (ng > 1) ? c->sub[l.g] : c->stream;
     // (every split launch gets its buffers: under SPLIT_ALL, l.S is chunks per piece, not a piece count)
@@ -747,16 +800,17 @@ static int run_factor(gpf_ctx* c, int pc) {
     const auto kern = l.split == gpf::SPLIT_ALL ? gpf::k_step<gpf::SPLIT_ALL, 1>
                                                 : (ed ? gpf::k_step<gpf::SPLIT_NONE, 1> : gpf::k_step<gpf::SPLIT_NONE, 0>);
     const int rc = launch_on(c, st, PC_PANEL, fl * gc, [&] {
-      hipLaunchKernelGGL(kern, dim3(l.grid), dim3(gpf::STEP_NTH), 0, st, l.J, nt, Np, c->d_L + (size_t)p0 * ld * ld,
+      hipLaunchKernelGGL(kern, dim3(l.grid), dim3(gpf::STEP_NTH), one_per_cu_lds(l), st, l.J, nt, Np, c->d_L + (size_t)p0 * ld * ld,
                          c->d_U + (size_t)p0 * ld * ld, c->d_yb + (size_t)p0 * ld, c->d_s2p + (size_t)p0 * nt * ld,
                          c->d_szp + (size_t)p0 * nt * ld, c->d_info + p0, gc, l.grp, N, c->d_x,
                          c->d_ls + (size_t)p0 * c->d, c->d, l.S, l.S2, partg, cntg, c->d_flag + p0, l.ed,
                          c->d_cflag + p0, l.defer, l.sy, spins,
                          l.la | ((l.la & 2) ? la_delay : 0) | (l.ro ? 32 : 0),
                          l.la ? c->d_la + 2 * (size_t)p0 * T * T : nullptr, l.pair,
-                         l.pair ? c->d_pb + gpf::pair_slot(p0, 0, nt) : nullptr,
-                         (l.pair == 1 && psync) ? c->d_pstart + (size_t)p0 * (nt - 1) * gpf::PAIR_HMAX : nullptr,
-                         (seq << 8) | l.J, c->prof ? c->d_clk : nullptr);
+                         l.pair ? (l.ed ? c->d_lb + (size_t)2 * p0 * smax * T * T : c->d_pb + gpf::pair_slot(p0, 0, nt))
+                                : nullptr,
+                         (!l.ed && l.pair == 1 && psync) ? c->d_pstart + (size_t)p0 * (nt - 1) * gpf::PAIR_HMAX : nullptr,
+                         l.ed ? gpf::lall_tag(gc, smax) : (seq << 8) | l.J, c->prof ? c->d_clk : nullptr);
     });
     if (rc) return rc;
     total += fl * gc;
@@ -1451,7 +1505,8 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
   long long wgs = 0, whole_tiles = 0, split_tiles = 0;
   std::vector<int> whole, piece, diag, syrk;
   long long diag_wgs = 0, syrk_wgs = 0;
-  std::vector<int> la_prev(MAX_GROUPS, 0), pair_prev(MAX_GROUPS, 0), pairJ(MAX_GROUPS, -1);
+  std::vector<int> la_prev(MAX_GROUPS, 0), pair_prev(MAX_GROUPS, 0), pairJ(MAX_GROUPS, -1), lall_prev(MAX_GROUPS, 0);
+  const int lsmax = lall_smax(nt);
   if ((int)plan.size() != (nt > 1 ? nt * ng : 0)) return plan_fail(msg, msg_len, "plan has %d launches, want %d",
                                                               (int)plan.size(), nt * ng);
   for (const StepLaunch& l : plan) {
@@ -1493,15 +1548,25 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     // paired block columns: a lead launch (J odd, with a block column behind it, fused diagonal factor,
     // deferred update, no split, groups of 8 particles) is followed on its stream by the follow
     // launch J+1, and only there
-    if (l.pair && (l.ed || l.split != gpf::SPLIT_NONE || !l.defer || l.grp != 0 || l.gc % 8 != 0 || nt < 4 ||
+    // all-tile look-ahead (early-diagonal launches, l.pair bits): pieces only from J >= 1 with a block
+    // column behind, consumed by the next launch of the same group (which reads the other parity)
+    if (l.ed && l.pair) {
+      if (l.split != gpf::SPLIT_NONE || !l.defer || l.la || l.ro || nt < 4 || ((l.pair & 1) && gpf::lall_items(l.J, nt) == 0) ||
+          ((l.pair & 2) && (l.J < 2 || !(lall_prev[l.g] & 1) || pairJ[l.g] != l.J - 1)))
+        return plan_fail(msg, msg_len, "J=%d g=%d: look-ahead pieces %d out of place", l.J, l.g, l.pair);
+    }
+    if ((lall_prev[l.g] & 1) && !(l.ed && (l.pair & 2)))
+      return plan_fail(msg, msg_len, "J=%d g=%d: launch J-1's look-ahead pieces left unused", l.J, l.g);
+    lall_prev[l.g] = l.ed ? l.pair : 0;
+    if (!l.ed && l.pair && (l.split != gpf::SPLIT_NONE || !l.defer || l.grp != 0 || l.gc % 8 != 0 || nt < 4 ||
                    (l.pair == 1 && (!(l.J & 1) || l.J + 1 > nt - 1 || !l.sy)) ||
                    (l.pair == 2 && (l.sy || pair_prev[l.g] != 1 || pairJ[l.g] != l.J - 1))))
       return plan_fail(msg, msg_len, "J=%d g=%d: paired block column %d out of place", l.J, l.g, l.pair);
     if (pair_prev[l.g] == 1 && l.pair != 2)
       return plan_fail(msg, msg_len, "J=%d g=%d: the lead launch's partials left unused", l.J, l.g);
-    pair_prev[l.g] = l.pair;
+    pair_prev[l.g] = l.ed ? 0 : l.pair;
     pairJ[l.g] = l.J;
-    if (l.pair == 1) {
+    if (!l.ed && l.pair == 1) {
       if (l.grid != (unsigned)(l.gc * gpf::pair_grid_per_particle(l.J, nt)))
         return plan_fail(msg, msg_len, "J=%d g=%d: lead launch grid %u", l.J, l.g, l.grid);
       std::vector<int> pla((size_t)tiles, 0), syp((size_t)l.gc, 0);
@@ -1552,8 +1617,27 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
       continue;
     }
     std::vector<int> lawg((size_t)l.gc, 0);
+    const int nstd = (l.ed ? l.gc : 0) + (l.sy ? l.gc : 0) + l.gc * ntl;
+    std::vector<int> lpc;
+    if (l.ed && (l.pair & 1)) {
+      if (l.grid != (unsigned)(nstd + l.gc * gpf::lall_total(l.J, nt)))
+        return plan_fail(msg, msg_len, "J=%d g=%d: look-ahead launch grid %u", l.J, l.g, l.grid);
+      lpc.assign((size_t)l.gc * lsmax, 0);
+    }
     for (unsigned b = 0; b < l.grid; ++b) {
       int p = -1, w = -1, sidx = -1;
+      if (l.ed && (l.pair & 1) && (int)b >= nstd) {  // a look-ahead piece: every (particle, item, piece) once
+        int it = -1;
+        gpf::lall_decode((int)b - nstd, l.J, l.gc, nt, p, it, sidx);
+        if (p < 0 || p >= l.gc || it < 0 || it >= gpf::lall_items(l.J, nt) || sidx < 0 || sidx >= gpf::lall_np(l.J, it, nt))
+          return plan_fail(msg, msg_len, "J=%d block %u: look-ahead piece decodes out of range", l.J, b);
+        const int o = gpf::lall_off(l.J, it, nt) + sidx;
+        if (o >= lsmax || gpf::lall_slot(l.J, it, sidx, p, l.gc, nt, lsmax) + (size_t)T * T > (size_t)2 * l.gc * lsmax * T * T ||
+            lpc[(size_t)p * lsmax + o]++)
+          return plan_fail(msg, msg_len, "J=%d block %u: look-ahead piece slot %d duplicate or outside", l.J, b, o);
+        ++wgs;
+        continue;
+      }
       const int role =
           l.split == gpf::SPLIT_ALL ? gpf::step_decode<gpf::SPLIT_ALL>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, 0, 0, p, w, sidx)
                                     : gpf::step_decode<gpf::SPLIT_NONE>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.sy,
@@ -1602,6 +1686,10 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
       }
       ++wgs;
     }
+    for (size_t i = 0; i < lpc.size(); ++i)
+      if ((int)(i % lsmax) < gpf::lall_total(l.J, nt) && lpc[i] != 1)
+        return plan_fail(msg, msg_len, "J=%d particle %d: look-ahead piece %d run %d times", l.J, (int)(i / lsmax),
+                         (int)(i % lsmax), lpc[i]);
     for (int q = 0; q < l.gc; ++q) {
       if (diag[q] != l.ed) return plan_fail(msg, msg_len, "J=%d particle %d: %d diagonal workgroups", l.J, q, diag[q]);
       diag_wgs += diag[q];
@@ -1622,7 +1710,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     }
   }
   for (int g = 0; g < ng; ++g)
-    if (pair_prev[g] == 1) return plan_fail(msg, msg_len, "group %d ends with a lead launch", g);
+    if (pair_prev[g] == 1 || (lall_prev[g] & 1)) return plan_fail(msg, msg_len, "group %d ends with unused partials", g);
   for (int a = 0; a < ng; ++a)
     for (int b2 = a + 1; b2 < ng; ++b2) {
       if (plo[a] < phi[a] && plo[b2] < phi[b2] && plo[a] < phi[b2] && plo[b2] < phi[a])
@@ -1641,7 +1729,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     stats[7] = diag_wgs;
     stats[8] = syrk_wgs;
     long long pairs = 0;
-    for (const StepLaunch& l : plan) pairs += l.pair == 1;
+    for (const StepLaunch& l : plan) pairs += !l.ed && l.pair == 1;
     stats[9] = 0;      // not persistent
     stats[10] = pairs;  // lead launches (paired block columns)
   }

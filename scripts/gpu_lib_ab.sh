@@ -7,7 +7,7 @@ O=gpurun_out/${TAG:-libab}; mkdir -p $O
 LIBS=${LIBS:-"libgpfit.so"}
 if [ "${SEC:-0}" = 1 ]; then EXTRA="--pso-steps 0 --no-cpu --predict-points 10000 --no-hull --no-kmeans --psurf-rows 0";
 else EXTRA="--pso-steps 0 --no-cpu --predict-points 0 --no-hull --no-kmeans --psurf-rows 0 --no-secondary"; fi
-B="python bench.py --steps ${STEPS:-40} --warmup 2 $EXTRA"
+B="python bench.py --steps ${STEPS:-40} --warmup 2 $EXTRA ${BENCH_ARGS:-}"
 for rep in $(seq ${REPS:-2}); do
   for V in $LIBS; do
     L=${V%%:*}; E=""; [ "$V" != "$L" ] && E=$(echo ${V#*:} | tr ',' ' ')

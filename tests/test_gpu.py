@@ -429,6 +429,45 @@ def test_paired_block_columns_bitwise(ctx, monkeypatch, N, d, P, groups, paired)
         assert _rel(out["1"][1][0], mo) < RTOL_MU_SD and _rel(out["1"][2][0], so) < RTOL_MU_SD
 
 
+@pytest.mark.parametrize("N,d,P", [(1024, 2, 32), (2049, 3, 12), (700, 4, 5), (1024, 2, 64)])
+def test_all_tile_lookahead_pieces(ctx, monkeypatch, N, d, P):
+    """All-tile look-ahead in pieces (GPF_LA_ALL; gpf::lall_decode, r6): launch J runs every GEMM of
+    launch J+1 over the columns final before it, in pieces of <= 2 blocks, and launch J+1 sums them.
+    Against the launches without it (GPF_LA_ALL=0): the partial sums round differently from one MFMA
+    chain, so mean/sd within 1e-10 and the objective within 1e-10 or explained by threshold ties;
+    deterministic over two runs; and against the oracle's identity form. Shapes: config B (32
+    particles, nt = 8), nt = 17, nt = 6, and 64 particles (two groups, the piece buffer's parities
+    per group)."""
+    rng = np.random.default_rng(N * 7 + P)
+    x = rng.uniform(size=(d, N))
+    y = np.sum(np.sin(2 * np.pi * x), axis=0) + 0.1 * rng.standard_normal(N)
+    e = rng.uniform(0.05, 0.2, size=N)
+    s, ex = ref_cpu.sigma_grid()
+    lo, hi = ref_cpu.search_bounds(x)
+    ctx.set_data(x, y, e)
+    ctx.set_grid(s, ex, lo, hi)
+    Q = rng.uniform(0.1, 0.5, size=(P, d))
+    monkeypatch.setenv("GPF_EARLY_DIAG", "1")
+    monkeypatch.setenv("GPF_PERSIST", "0")
+    monkeypatch.setenv("GPF_SPLIT_K", "1")
+    monkeypatch.setenv("GPF_LA_ALL", "1")
+    import gpfit
+    st = gpfit.plan_check(P, (N + 127) // 128)
+    g, gm, gs = ctx.eval_batch(Q, want_mu_sd=True)
+    again = ctx.eval_batch(Q, want_mu_sd=True)
+    for a, b in zip((g, gm, gs), again):
+        np.testing.assert_array_equal(a, b)
+    monkeypatch.setenv("GPF_LA_ALL", "0")
+    w, wm, ws = ctx.eval_batch(Q, want_mu_sd=True)
+    assert st["workgroups"] > gpfit.plan_check(P, (N + 127) // 128)["workgroups"]  # the pieces ran
+    assert _rel(gm, wm) < 1e-10 and _rel(gs, ws) < 1e-10, (_rel(gm, wm), _rel(gs, ws))
+    for k in range(P):
+        if abs(g[k] - w[k]) > 1e-10 * abs(w[k]):
+            assert_loss_or_ties(g[k], w[k], wm[k], ws[k], y, s, what=k)
+    mo, so = ref_cpu.GP_train_identity(x, y, e, Q[0])
+    assert _rel(gm[0], mo) < RTOL_MU_SD and _rel(gs[0], so) < RTOL_MU_SD
+
+
 def test_sentinels_never_reach_gpu_and_mix_with_live_particles(ctx, f2):
     x, y, e = f2["c0_x"], f2["c0_y"], f2["c0_e"]
     lo, hi = f2["c0_lo"], f2["c0_hi"]
