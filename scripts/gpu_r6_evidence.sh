@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-5 evidence: rocprofv3 kernel stats + trace of the config-C bench and the PMC passes
+# Round-6 evidence: rocprofv3 kernel stats + trace of the config-C bench and the PMC passes
 # (FETCH_SIZE, WRITE_SIZE, MFMA busy) of its dominant kernel; then the same for the
 # single-particle prediction (scripts/predict_probe.py: k_step<SPLIT_ALL, 1>, the flat finish).
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/${TAG:-r5ev}; mkdir -p $O
+O=gpurun_out/${TAG:-r6ev}; mkdir -p $O
 B="python bench.py --steps 3 --warmup 1 --pso-steps 0 --no-cpu --predict-points 0 --no-hull --no-kmeans --psurf-rows 0 --no-secondary"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- $B > $O/prof.log 2>&1 || exit 4
 f=$(find $O/prof -name "*kernel_trace.csv" | head -1)
