@@ -299,10 +299,11 @@ __host__ __device__ __forceinline__ size_t pair_slot(int p, int wf, int nt) { re
 // J & 1 of the buffer, so launch J+1 reads one half while it writes the other. Deterministic; the sum
 // of partials rounds differently from one MFMA chain (within 1e-12 of the unsplit factor,
 // test_all_tile_lookahead_pieces).
-constexpr int LALL_PB = 2;
-// (the look-ahead launches pass P and the slots per particle packed in k_step's ptag)
-__host__ __device__ __forceinline__ int lall_tag(int P, int smax) { return (P << 16) | smax; }
-__host__ __device__ __forceinline__ int P_of(int tag) { return tag >> 16; }
+// (the look-ahead launches pass P, the piece size in blocks and the slots per particle packed in
+// k_step's ptag)
+__host__ __device__ __forceinline__ int lall_tag(int P, int pb, int smax) { return (pb << 28) | (P << 16) | smax; }
+__host__ __device__ __forceinline__ int P_of(int tag) { return (tag >> 16) & 0xfff; }
+__host__ __device__ __forceinline__ int pb_of(int tag) { return tag >> 28; }
 __host__ __device__ __forceinline__ int smax_of(int tag) { return tag & 0xffff; }
 __host__ __device__ __forceinline__ int lall_items(int J, int nt) {  // items launch J produces, per particle
   return J < 1 || J + 1 > nt - 1 ? 0 : (nt - 2 - J) + J + (J + 2 <= nt - 1 ? 1 : 0);
@@ -311,26 +312,26 @@ __host__ __device__ __forceinline__ int lall_depth(int J, int it, int nt) {  // 
   const int nLc = nt - 2 - J;
   return it < nLc ? J : it < nLc + J ? J - (it - nLc) : J;
 }
-__host__ __device__ __forceinline__ int lall_np(int J, int it, int nt) { return (lall_depth(J, it, nt) + LALL_PB - 1) / LALL_PB; }
-__host__ __device__ __forceinline__ int lall_off(int J, int it, int nt) {
+__host__ __device__ __forceinline__ int lall_np(int J, int it, int nt, int pb) { return (lall_depth(J, it, nt) + pb - 1) / pb; }
+__host__ __device__ __forceinline__ int lall_off(int J, int it, int nt, int pb) {
   int o = 0;
-  for (int i = 0; i < it; ++i) o += lall_np(J, i, nt);
+  for (int i = 0; i < it; ++i) o += lall_np(J, i, nt, pb);
   return o;
 }
-__host__ __device__ __forceinline__ int lall_total(int J, int nt) { return lall_off(J, lall_items(J, nt), nt); }
+__host__ __device__ __forceinline__ int lall_total(int J, int nt, int pb) { return lall_off(J, lall_items(J, nt), nt, pb); }
 // slot of piece s of item it produced by launch J for particle p (P particles in the group, smax slots
 // per particle and parity)
-__host__ __device__ __forceinline__ size_t lall_slot(int J, int it, int s, int p, int P, int nt, int smax) {
-  return ((size_t)((J & 1) * P + p) * smax + lall_off(J, it, nt) + s) * T * T;
+__host__ __device__ __forceinline__ size_t lall_slot(int J, int it, int s, int p, int P, int nt, int smax, int pb) {
+  return ((size_t)((J & 1) * P + p) * smax + lall_off(J, it, nt, pb) + s) * T * T;
 }
 // Workgroup b of a look-ahead launch past its diagonal, SYRK and tile workgroups (r = b - those): piece
 // s of item it of particle p (items in order, their pieces in order, particles fastest)
-__host__ __device__ __forceinline__ void lall_decode(int r, int J, int P, int nt, int& p, int& it, int& s) {
+__host__ __device__ __forceinline__ void lall_decode(int r, int J, int P, int nt, int pb, int& p, int& it, int& s) {
   p = r % P;
   int q = r / P;
   const int ni = lall_items(J, nt);
   for (it = 0; it < ni - 1; ++it) {
-    const int n = lall_np(J, it, nt);
+    const int n = lall_np(J, it, nt, pb);
     if (q < n) break;
     q -= n;
   }
@@ -954,6 +955,22 @@ __device__ __forceinline__ void syrkp_item(int J, int p, int Npad, double* __res
   syrk_tile<false>(Lp + (size_t)I * T * ld + (size_t)I * T, ld, Lp + (size_t)I * T * ld, Npad, J * T, lds, qd);
 }
 
+// Block layout of a look-ahead launch: [diagonal P][SYRK P] then the tiles and the pieces — tiles
+// first (pair bit 2 clear) or the pieces first (bit 2 set: the pieces wait for nothing, the tiles
+// for the diagonal block anyway). nstd = the diagonal, SYRK and tile workgroups.
+__host__ __device__ __forceinline__ int lall_head(int P, int nt, int nstd) { return nstd - P * (nt - 1); }
+__host__ __device__ __forceinline__ bool lall_is_piece(int b, int J, int P, int nt, int nstd, int bits, int tag) {
+  if (!(bits & 4)) return b >= nstd;
+  const int h = lall_head(P, nt, nstd);
+  return b >= h && b < h + P * lall_total(J, nt, pb_of(tag));
+}
+__host__ __device__ __forceinline__ int lall_piece_index(int b, int P, int nt, int nstd, int bits) {
+  return (bits & 4) ? b - lall_head(P, nt, nstd) : b - nstd;
+}
+// (pieces first: the block index step_decode sees for a diagonal, SYRK or tile workgroup)
+__host__ __device__ __forceinline__ int lall_tile_block(int b, int J, int P, int nt, int nstd, int tag) {
+  return b < lall_head(P, nt, nstd) ? b : b - P * lall_total(J, nt, pb_of(tag));
+}
 // acc += a partial in store_node's layout (its 16-B units added as they arrive: no second accumulator set)
 __device__ __forceinline__ void add_node(Acc<T>& acc, const double* slot) {
   const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(slot), 0, T * T * 8, 0x00020000);
@@ -968,21 +985,23 @@ __device__ __forceinline__ void add_node(Acc<T>& acc, const double* slot) {
     }
 }
 // the summed partials of item it (launch J-1's pieces, in piece order)
-__device__ __forceinline__ void lall_seed(Acc<T>& acc, const double* lb, int J, int it, int p, int P, int nt, int smax) {
-  const int np = lall_np(J - 1, it, nt);
-  const double* s0 = lb + lall_slot(J - 1, it, 0, p, P, nt, smax);
+__device__ __forceinline__ void lall_seed(Acc<T>& acc, const double* lb, int J, int it, int p, int tag, int nt) {
+  const int P = P_of(tag), smax = smax_of(tag), pb = pb_of(tag);
+  const int np = lall_np(J - 1, it, nt, pb);
+  const double* s0 = lb + lall_slot(J - 1, it, 0, p, P, nt, smax, pb);
   load_node(acc, s0);
   for (int s = 1; s < np; ++s) add_node(acc, s0 + (size_t)s * T * T);
 }
 
 // ROLE_LPIECE: piece s of item it of launch J (see lall_items)
-__device__ __forceinline__ void lall_piece(int J, int it, int s, int p, int P, int nt, int Npad, const double* __restrict__ Lb,
+__device__ __forceinline__ void lall_piece(int J, int it, int s, int p, int nt, int Npad, const double* __restrict__ Lb,
                                            const double* __restrict__ Ub, int N, const double* __restrict__ x,
-                                           const double* __restrict__ ls, int d, double* __restrict__ lb, int smax,
+                                           const double* __restrict__ ls, int d, double* __restrict__ lb, int tag,
                                            double* lds) {
   const size_t ld = (size_t)Npad;
+  const int pb = pb_of(tag);
   const int nLc = nt - 2 - J, depth = lall_depth(J, it, nt);
-  const int b0 = s * LALL_PB, nb = min(LALL_PB, depth - b0);
+  const int b0 = s * pb, nb = min(pb, depth - b0);
   const double* Lp = Lb + (size_t)p * ld * ld;
   const Quad<T> qd;
   Acc<T> acc;
@@ -1006,20 +1025,20 @@ __device__ __forceinline__ void lall_piece(int J, int it, int s, int p, int P, i
     else acc.zero();
     gemm_stream_dl<false, true, TRI_C_LOWER>(acc, Ar, Npad, Ar, Npad, nb * T, lds, qd);
   }
-  store_node(acc, lb + lall_slot(J, it, s, p, P, nt, smax), qd);
+  store_node(acc, lb + lall_slot(J, it, s, p, P_of(tag), nt, smax_of(tag), pb), qd);
 }
 
 // SYRK workgroup of a look-ahead launch J >= 2: S = A_{J+1,J+1} - L_{J+1,<J} L_{J+1,<J}^T from launch
 // J-1's pieces over [0, J-1) (item nt-2) plus block column J-1, published like syrk_item's.
-__device__ __forceinline__ void lall_syrk_item(int J, int p, int P, int nt, int Npad, double* __restrict__ Lb,
-                                               int* __restrict__ yflag, const double* __restrict__ lb, int smax,
+__device__ __forceinline__ void lall_syrk_item(int J, int p, int nt, int Npad, double* __restrict__ Lb,
+                                               int* __restrict__ yflag, const double* __restrict__ lb, int tag,
                                                double* lds) {
   const size_t ld = (size_t)Npad;
   const int I = J + 1;
   double* Lp = Lb + (size_t)p * ld * ld;
   const Quad<T> qd;
   Acc<T> acc;
-  lall_seed(acc, lb, J, nt - 2, p, P, nt, smax);
+  lall_seed(acc, lb, J, nt - 2, p, tag, nt);
   const double* Ar = Lp + (size_t)I * T * ld + (size_t)(J - 1) * T;
   gemm_stream_dl<false, true, TRI_C_LOWER>(acc, Ar, Npad, Ar, Npad, T, lds, qd);
   acc.store_wt(qd, Lp + (size_t)I * T * ld + (size_t)I * T, ld);  // (the upper half rewrites A's own values)
@@ -1098,7 +1117,7 @@ if (w < nL)
                                   lds, qd);
     } else if (lseed) {
       // the pieces of launch J-1 (seed and the columns < J-1), then block column J-1
-      lall_seed(acc, pb, J, w, p, P_of(ptag), nt, smax_of(ptag));
+      lall_seed(acc, pb, J, w, p, ptag, nt);
       gemm_stream_dl<false, true>(acc, Lp + (size_t)J * T * ld + (size_t)(J - 1) * T, Npad,
                                   Lp + (size_t)I * T * ld + (size_t)(J - 1) * T, Npad, T, lds, qd);
     } else if (follow) {
@@ -1165,7 +1184,7 @@ if (w < nL)
     Acc<T> acc;
     // W = L_J,[K,J) U_[K,J),K (U_KK is lower triangular: the wave's first chunks add zeros)
     if (lseed && K < J - 1) {
-      lall_seed(acc, pb, J, w, p, P_of(ptag), nt, smax_of(ptag));
+      lall_seed(acc, pb, J, w, p, ptag, nt);
       gemm_stream_dl<true, false>(acc, Lp + (size_t)J * T * ld + (size_t)(J - 1) * T, Npad,
                                   Up + (size_t)(J - 1) * T * ld + (size_t)K * T, Npad, T, lds, qd);
     } else if (follow && K < J - 1) {
@@ -1260,12 +1279,13 @@ __global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_step(int J, i
   int role;
   if (PAIRS && pair == 1) {
     role = pair_decode((int)blockIdx.x, J, P, nt, p, w, &uh);
-  } else if (LALL && (pair & 1) && (int)blockIdx.x >= nstd) {
-    lall_decode((int)blockIdx.x - nstd, J, P, nt, p, lit, sidx);
+  } else if (LALL && (pair & 1) && lall_is_piece((int)blockIdx.x, J, P, nt, nstd, pair, ptag)) {
+    lall_decode(lall_piece_index((int)blockIdx.x, P, nt, nstd, pair), J, P, nt, pb_of(ptag), p, lit, sidx);
     w = -1;
     role = ROLE_LPIECE;
   } else {
-    role = step_decode<SPLIT>((int)blockIdx.x, J, P, nt, grp, S, ED && ed, SPLIT != SPLIT_ALL && sy,
+    role = step_decode<SPLIT>(LALL && (pair & 5) == 5 ? lall_tile_block((int)blockIdx.x, J, P, nt, nstd, ptag) : (int)blockIdx.x, J,
+                              P, nt, grp, S, ED && ed, SPLIT != SPLIT_ALL && sy,
                               SPLIT == SPLIT_NONE && ED && (la & 1) && !sy, p, w, sidx,
                               SPLIT == SPLIT_NONE && ED && (la & 32) != 0);
   }
@@ -1281,8 +1301,8 @@ __global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_step(int J, i
                                      (w >= nt - 1 - J || J + 1 + w < nt);
     else if (role == ROLE_SYRKP) ok = ok && PAIRS && pair == 1 && w == 1 && J >= 1 && J + 2 <= nt - 1;
     else if (role == ROLE_LPIECE) ok = ok && LALL && pb != nullptr && lit >= 0 && lit < lall_items(J, nt) && sidx >= 0 &&
-                                       sidx < lall_np(J, lit, nt) && P_of(ptag) == P &&
-                                       lall_off(J, lit, nt) + sidx < smax_of(ptag);
+                                       sidx < lall_np(J, lit, nt, pb_of(ptag)) && P_of(ptag) == P &&
+                                       lall_off(J, lit, nt, pb_of(ptag)) + sidx < smax_of(ptag);
     else if (role != ROLE_IDLE) ok = ok && w >= 0 && w < nt - 1 && sidx >= 0 && (pair != 2 || pb != nullptr) &&
                                      sidx < (SPLIT == SPLIT_ALL ? split_all_pieces(J, w, nt, S) : S) && sidx < S2 &&
                                      (role != ROLE_PIECE || (part != nullptr && cnt != nullptr && S > 1)) &&
@@ -1297,9 +1317,9 @@ __global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_step(int J, i
 #endif
   if (PAIRS && pair == 1 && pstart) pair_start_sync(J, role == ROLE_SYRK ? 0 : w, uh, p, nt, pstart, ptag);
   if (LALL && role == ROLE_LPIECE) {
-    lall_piece(J, lit, sidx, p, P, nt, Npad, Lb, Ub, N, x, ls, d, pb, smax_of(ptag), lds);
+    lall_piece(J, lit, sidx, p, nt, Npad, Lb, Ub, N, x, ls, d, pb, ptag, lds);
   } else if (LALL && role == ROLE_SYRK && (pair & 2) && J >= 2) {
-    lall_syrk_item(J, p, P, nt, Npad, Lb, yflag, pb, smax_of(ptag), lds);
+    lall_syrk_item(J, p, nt, Npad, Lb, yflag, pb, ptag, lds);
   } else if (PAIRS && role == ROLE_PLA) {
     pla_item(J, w, p, nt, Npad, Lb, Ub, N, x, ls, d, pb, lds);
   } else if (PAIRS && role == ROLE_SYRKP) {

@@ -480,11 +480,22 @@ static bool lall_on() {
   if (const char* s = getenv("GPF_LA_ALL")) on = atoi(s) != 0;
   return on;
 }
+// piece size in 128-blocks (GPF_LA_ALL_PB, 1..4) and the pieces ahead of the tiles (GPF_LA_ALL_FIRST)
+static int lall_pb() {
+  int pb = 1;
+  if (const char* s = getenv("GPF_LA_ALL_PB")) pb = std::max(1, std::min(4, atoi(s)));
+  return pb;
+}
+static bool lall_first() {
+  bool on = true;
+  if (const char* s = getenv("GPF_LA_ALL_FIRST")) on = atoi(s) != 0;
+  return on;
+}
 // (the pieces per particle and launch grow as nt J / 2: the look-ahead is for short factorisations)
 constexpr int LALL_NT_MAX = 32;
 static int lall_smax(int nt) {
   int m = 1;
-  for (int J = 0; J < nt; ++J) m = std::max(m, gpf::lall_total(J, nt));
+  for (int J = 0; J < nt; ++J) m = std::max(m, gpf::lall_total(J, nt, lall_pb()));
   return m;
 }
 
@@ -615,9 +626,10 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
       // its tiles and SYRK workgroup consume launch J-1's
       if (lall_on() && l.ed && S == 1 && l.defer && nt >= 4 && nt <= LALL_NT_MAX) {
         l.pair = (gpf::lall_items(J, nt) > 0 ? 1 : 0) | (J >= 2 ? 2 : 0);
+        if ((l.pair & 1) && lall_first()) l.pair |= 4;
         l.la = 0;
         l.ro = 0;
-        l.grid = (unsigned)(l.gc * (nt - 1) + l.gc + (l.sy ? l.gc : 0) + l.gc * gpf::lall_total(J, nt));
+        l.grid = (unsigned)(l.gc * (nt - 1) + l.gc + (l.sy ? l.gc : 0) + l.gc * gpf::lall_total(J, nt, lall_pb()));
       }
       // one set of partial slots per group: groups run concurrently
       l.part_off = (size_t)l.p0 * (nt - 1) * Smax * T * T;
@@ -810,7 +822,7 @@ static int run_factor(gpf_ctx* c, int pc) {
                          l.pair ? (l.ed ? c->d_lb + (size_t)2 * p0 * smax * T * T : c->d_pb + gpf::pair_slot(p0, 0, nt))
                                 : nullptr,
                          (!l.ed && l.pair == 1 && psync) ? c->d_pstart + (size_t)p0 * (nt - 1) * gpf::PAIR_HMAX : nullptr,
-                         l.ed ? gpf::lall_tag(gc, smax) : (seq << 8) | l.J, c->prof ? c->d_clk : nullptr);
+                         l.ed ? gpf::lall_tag(gc, lall_pb(), smax) : (seq << 8) | l.J, c->prof ? c->d_clk : nullptr);
     });
     if (rc) return rc;
     total += fl * gc;
@@ -1618,45 +1630,49 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     }
     std::vector<int> lawg((size_t)l.gc, 0);
     const int nstd = (l.ed ? l.gc : 0) + (l.sy ? l.gc : 0) + l.gc * ntl;
+    const int lpb = lall_pb(), ltag = gpf::lall_tag(l.gc, lpb, lsmax);
     std::vector<int> lpc;
     if (l.ed && (l.pair & 1)) {
-      if (l.grid != (unsigned)(nstd + l.gc * gpf::lall_total(l.J, nt)))
+      if (l.grid != (unsigned)(nstd + l.gc * gpf::lall_total(l.J, nt, lpb)))
         return plan_fail(msg, msg_len, "J=%d g=%d: look-ahead launch grid %u", l.J, l.g, l.grid);
       lpc.assign((size_t)l.gc * lsmax, 0);
     }
     for (unsigned b = 0; b < l.grid; ++b) {
       int p = -1, w = -1, sidx = -1;
-      if (l.ed && (l.pair & 1) && (int)b >= nstd) {  // a look-ahead piece: every (particle, item, piece) once
+      if (l.ed && (l.pair & 1) && gpf::lall_is_piece((int)b, l.J, l.gc, nt, nstd, l.pair, ltag)) {
+        // a look-ahead piece: every (particle, item, piece) once
         int it = -1;
-        gpf::lall_decode((int)b - nstd, l.J, l.gc, nt, p, it, sidx);
-        if (p < 0 || p >= l.gc || it < 0 || it >= gpf::lall_items(l.J, nt) || sidx < 0 || sidx >= gpf::lall_np(l.J, it, nt))
+        gpf::lall_decode(gpf::lall_piece_index((int)b, l.gc, nt, nstd, l.pair), l.J, l.gc, nt, lpb, p, it, sidx);
+        if (p < 0 || p >= l.gc || it < 0 || it >= gpf::lall_items(l.J, nt) || sidx < 0 || sidx >= gpf::lall_np(l.J, it, nt, lpb))
           return plan_fail(msg, msg_len, "J=%d block %u: look-ahead piece decodes out of range", l.J, b);
-        const int o = gpf::lall_off(l.J, it, nt) + sidx;
-        if (o >= lsmax || gpf::lall_slot(l.J, it, sidx, p, l.gc, nt, lsmax) + (size_t)T * T > (size_t)2 * l.gc * lsmax * T * T ||
+        const int o = gpf::lall_off(l.J, it, nt, lpb) + sidx;
+        if (o >= lsmax || gpf::lall_slot(l.J, it, sidx, p, l.gc, nt, lsmax, lpb) + (size_t)T * T > (size_t)2 * l.gc * lsmax * T * T ||
             lpc[(size_t)p * lsmax + o]++)
           return plan_fail(msg, msg_len, "J=%d block %u: look-ahead piece slot %d duplicate or outside", l.J, b, o);
         ++wgs;
         continue;
       }
+      // (pieces ahead of the tiles: the block index the kernel hands step_decode)
+      const unsigned bt = (l.ed && (l.pair & 5) == 5) ? (unsigned)gpf::lall_tile_block((int)b, l.J, l.gc, nt, nstd, ltag) : b;
       const int role =
-          l.split == gpf::SPLIT_ALL ? gpf::step_decode<gpf::SPLIT_ALL>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, 0, 0, p, w, sidx)
-                                    : gpf::step_decode<gpf::SPLIT_NONE>(b, l.J, l.gc, nt, l.grp, l.S, l.ed, l.sy,
+          l.split == gpf::SPLIT_ALL ? gpf::step_decode<gpf::SPLIT_ALL>(bt, l.J, l.gc, nt, l.grp, l.S, l.ed, 0, 0, p, w, sidx)
+                                    : gpf::step_decode<gpf::SPLIT_NONE>(bt, l.J, l.gc, nt, l.grp, l.S, l.ed, l.sy,
                                                                         (l.la & 1) && !l.sy, p, w, sidx, l.ro);
       if (role == gpf::ROLE_DIAG) {  // one diagonal workgroup per particle, ahead of every tile of the launch
         // (reordered: right behind the particles' light U tiles, which wait for it, and the SYRK workgroups)
-        if (!l.ed || p < 0 || p >= l.gc || (unsigned)p + (l.ro ? 2 * l.gc : 0) != b || diag[p]++)
+        if (!l.ed || p < 0 || p >= l.gc || (unsigned)p + (l.ro ? 2 * l.gc : 0) != bt || diag[p]++)
           return plan_fail(msg, msg_len, "J=%d block %u: misplaced or duplicate diagonal workgroup (p=%d)", l.J, b, p);
         ++wgs;
         continue;
       }
       if (role == gpf::ROLE_LA) {  // one per particle, right behind the diagonal and SYRK workgroups
-        if (!(l.la & 1) || l.sy || p < 0 || p >= l.gc || (unsigned)p + (l.ed ? l.gc : 0) != b || lawg[p]++)
+        if (!(l.la & 1) || l.sy || p < 0 || p >= l.gc || (unsigned)p + (l.ed ? l.gc : 0) != bt || lawg[p]++)
           return plan_fail(msg, msg_len, "J=%d block %u: misplaced or duplicate look-ahead workgroup (p=%d)", l.J, b, p);
         ++wgs;
         continue;
       }
       if (role == gpf::ROLE_SYRK) {  // one per particle, right behind the diagonal workgroups (reordered: the light U tiles)
-        if (!l.sy || p < 0 || p >= l.gc || (unsigned)p + (l.ro || l.ed ? l.gc : 0) != b || syrk[p]++)
+        if (!l.sy || p < 0 || p >= l.gc || (unsigned)p + (l.ro || l.ed ? l.gc : 0) != bt || syrk[p]++)
           return plan_fail(msg, msg_len, "J=%d block %u: misplaced or duplicate SYRK workgroup (p=%d)", l.J, b, p);
         ++wgs;
         continue;
@@ -1687,7 +1703,7 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
       ++wgs;
     }
     for (size_t i = 0; i < lpc.size(); ++i)
-      if ((int)(i % lsmax) < gpf::lall_total(l.J, nt) && lpc[i] != 1)
+      if ((int)(i % lsmax) < gpf::lall_total(l.J, nt, lpb) && lpc[i] != 1)
         return plan_fail(msg, msg_len, "J=%d particle %d: look-ahead piece %d run %d times", l.J, (int)(i / lsmax),
                          (int)(i % lsmax), lpc[i]);
     for (int q = 0; q < l.gc; ++q) {

@@ -429,8 +429,9 @@ def test_paired_block_columns_bitwise(ctx, monkeypatch, N, d, P, groups, paired)
         assert _rel(out["1"][1][0], mo) < RTOL_MU_SD and _rel(out["1"][2][0], so) < RTOL_MU_SD
 
 
-@pytest.mark.parametrize("N,d,P", [(1024, 2, 32), (2049, 3, 12), (700, 4, 5), (1024, 2, 64)])
-def test_all_tile_lookahead_pieces(ctx, monkeypatch, N, d, P):
+@pytest.mark.parametrize("N,d,P,pb,first", [(1024, 2, 32, "1", "1"), (2049, 3, 12, "2", "0"), (700, 4, 5, "3", "1"),
+                                            (1024, 2, 64, "1", "1")])
+def test_all_tile_lookahead_pieces(ctx, monkeypatch, N, d, P, pb, first):
     """All-tile look-ahead in pieces (GPF_LA_ALL; gpf::lall_decode, r6): launch J runs every GEMM of
     launch J+1 over the columns final before it, in pieces of <= 2 blocks, and launch J+1 sums them.
     Against the launches without it (GPF_LA_ALL=0): the partial sums round differently from one MFMA
@@ -451,6 +452,8 @@ def test_all_tile_lookahead_pieces(ctx, monkeypatch, N, d, P):
     monkeypatch.setenv("GPF_PERSIST", "0")
     monkeypatch.setenv("GPF_SPLIT_K", "1")
     monkeypatch.setenv("GPF_LA_ALL", "1")
+    monkeypatch.setenv("GPF_LA_ALL_PB", pb)  # piece size in blocks
+    monkeypatch.setenv("GPF_LA_ALL_FIRST", first)  # pieces ahead of the tiles
     import gpfit
     st = gpfit.plan_check(P, (N + 127) // 128)
     g, gm, gs = ctx.eval_batch(Q, want_mu_sd=True)
