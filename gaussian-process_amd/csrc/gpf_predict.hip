@@ -27,6 +27,8 @@ __global__ __launch_bounds__(Geo<T>::NTH, 4) void k_predict_vsq(int Npad, const 
                                                          double* __restrict__ vsq, const double* __restrict__ z,
                                                          double* __restrict__ vz, int t0) {
   __shared__ __attribute__((aligned(16))) double smem[DL_STAGE];
+  // (r6: XCD-owned column tiles — every row tile of a column tile on one XCD — measured 2.55-2.59
+  // vs 2.50 ms and were removed; profiles/r6/ab_vsq_xcd.txt)
   const int q = blockIdx.x, t = t0 + (int)gridDim.y - 1 - (int)blockIdx.y;
   const Quad<T> qd;
   Acc<T> acc;

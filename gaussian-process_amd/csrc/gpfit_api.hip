@@ -473,10 +473,14 @@ static bool pair_on() {
 }
 
 // All-tile look-ahead in pieces (gpf::lall_decode) for the early-diagonal launches without split
-// (config B: fewer tiles than workgroup slots, launches bound by their deepest tile). GPF_LA_ALL =
-// 0/1 overrides. It replaces the critical-tile look-ahead (GPF_LOOKAHEAD) and the reordered dispatch.
+// (config B: fewer tiles than workgroup slots, launches bound by their deepest tile), from launch
+// GPF_LA_ALL_FROM on (default nt-2: the last launch, whose deepest U tile is the factorisation's
+// longest item, consumes them: config B 41.5-41.7k -> 42.4k evals/s; from launch 1 on, or nt-3, the
+// producing launches grow by more than the consumers shrink: 35-39k; profiles/r6/
+// ab_B_lookahead_pieces.txt). GPF_LA_ALL = 0/1 overrides. In the launches it covers it replaces the
+// critical-tile look-ahead (GPF_LOOKAHEAD) and the reordered dispatch.
 static bool lall_on() {
-  bool on = false;
+  bool on = true;
   if (const char* s = getenv("GPF_LA_ALL")) on = atoi(s) != 0;
   return on;
 }
@@ -485,6 +489,13 @@ static int lall_pb() {
   int pb = 1;
   if (const char* s = getenv("GPF_LA_ALL_PB")) pb = std::max(1, std::min(4, atoi(s)));
   return pb;
+}
+// the first launch that produces pieces (GPF_LA_ALL_FROM; default nt-2: only the last launch, whose
+// deepest U tile is the longest item of the factorisation, consumes them; negative: counted from nt)
+static int lall_from(int nt) {
+  int j = -2;
+  if (const char* s = getenv("GPF_LA_ALL_FROM")) j = atoi(s);
+  return std::max(1, j < 0 ? nt + j : j);
 }
 static bool lall_first() {
   bool on = true;
@@ -624,10 +635,14 @@ static void step_plan(int pc, int nt, int S, int Smax, std::vector<StepLaunch>& 
       if (l.pair == 1) l.grid = (unsigned)(l.gc * gpf::pair_grid_per_particle(J, nt));
       // all-tile look-ahead (early-diagonal launches): bit 0 this launch produces pieces for J+1, bit 1
       // its tiles and SYRK workgroup consume launch J-1's
-      if (lall_on() && l.ed && S == 1 && l.defer && nt >= 4 && nt <= LALL_NT_MAX) {
-        l.pair = (gpf::lall_items(J, nt) > 0 ? 1 : 0) | (J >= 2 ? 2 : 0);
+      const int j0 = lall_from(nt);
+      if (lall_on() && l.ed && S == 1 && l.defer && nt >= 4 && nt <= LALL_NT_MAX && J >= j0) {
+        // launches J >= j0 produce pieces for J+1, launches J > j0 consume them (and run no
+        // critical-tile look-ahead: the pieces carry the next critical tile too); launch j0 may still
+        // seed its critical tile from launch j0-1's look-ahead
+        l.pair = (gpf::lall_items(J, nt) > 0 ? 1 : 0) | (J >= 2 && J > j0 ? 2 : 0);
         if ((l.pair & 1) && lall_first()) l.pair |= 4;
-        l.la = 0;
+        l.la = J > j0 ? 0 : (l.la & 2);
         l.ro = 0;
         l.grid = (unsigned)(l.gc * (nt - 1) + l.gc + (l.sy ? l.gc : 0) + l.gc * gpf::lall_total(J, nt, lall_pb()));
       }
@@ -1563,7 +1578,8 @@ int gpf_plan_check(int pc, int nt, long long* stats, char* msg, int msg_len) {
     // all-tile look-ahead (early-diagonal launches, l.pair bits): pieces only from J >= 1 with a block
     // column behind, consumed by the next launch of the same group (which reads the other parity)
     if (l.ed && l.pair) {
-      if (l.split != gpf::SPLIT_NONE || !l.defer || l.la || l.ro || nt < 4 || ((l.pair & 1) && gpf::lall_items(l.J, nt) == 0) ||
+      if (l.split != gpf::SPLIT_NONE || !l.defer || (l.la & 1) || ((l.la & 2) && (l.pair & 2)) || l.ro || nt < 4 ||
+          ((l.pair & 1) && gpf::lall_items(l.J, nt) == 0) ||
           ((l.pair & 2) && (l.J < 2 || !(lall_prev[l.g] & 1) || pairJ[l.g] != l.J - 1)))
         return plan_fail(msg, msg_len, "J=%d g=%d: look-ahead pieces %d out of place", l.J, l.g, l.pair);
     }

@@ -36,7 +36,8 @@ ENVS = [
     {"GPF_PAIR": "1", "GPF_GROUPS": "3"}, {"GPF_PAIR": "1", "GPF_EARLY_DIAG": "0", "GPF_GROUPS": "1"},
     {"GPF_LA_ALL": "1"}, {"GPF_LA_ALL": "1", "GPF_EARLY_DIAG": "1", "GPF_GROUPS": "2"},  # r6: look-ahead pieces
     {"GPF_LA_ALL": "0"}, {"GPF_LA_ALL": "1", "GPF_LA_ALL_PB": "2", "GPF_LA_ALL_FIRST": "0"},
-    {"GPF_LA_ALL": "1", "GPF_LA_ALL_PB": "3", "GPF_EARLY_DIAG": "1"},
+    {"GPF_LA_ALL": "1", "GPF_LA_ALL_PB": "3", "GPF_EARLY_DIAG": "1", "GPF_LA_ALL_FROM": "1"},
+    {"GPF_LA_ALL": "1", "GPF_LA_ALL_FROM": "3"}, {"GPF_LA_ALL": "1", "GPF_LA_ALL_FROM": "-3"},
 ]
 
 
@@ -45,7 +46,7 @@ def env(monkeypatch):
     def apply(kv):
         for k in ("GPF_GROUPS", "GPF_SPLIT_K", "GPF_STEP_GROUP", "GPF_EARLY_DIAG",
                   "GPF_DEFER_SYRK", "GPF_SPLIT_K_SLOTS", "GPF_SPLIT_K_MINCH", "GPF_PERSIST", "GPF_REORDER",
-                  "GPF_PAIR", "GPF_LA_ALL", "GPF_LA_ALL_PB", "GPF_LA_ALL_FIRST"):
+                  "GPF_PAIR", "GPF_LA_ALL", "GPF_LA_ALL_PB", "GPF_LA_ALL_FIRST", "GPF_LA_ALL_FROM"):
             monkeypatch.delenv(k, raising=False)
         if kv and "GPF_PERSIST" not in kv:  # the launch-plan knobs: on the per-block-column launches
             monkeypatch.setenv("GPF_PERSIST", "0")
