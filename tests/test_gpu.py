@@ -980,9 +980,11 @@ def test_persistent_factor_bitwise(ctx, monkeypatch, N, d, P):
     again = ctx.eval_batch(Q, want_mu_sd=True)
     monkeypatch.setenv("GPF_PERSIST", "0")
     monkeypatch.setenv("GPF_SPLIT_K", "1")  # (few-tile launches would otherwise sum split-K pieces: other rounding)
+    monkeypatch.setenv("GPF_LA_ALL", "0")  # (likewise the early-diagonal launches' look-ahead pieces, r6)
     off = ctx.eval_batch(Q, want_mu_sd=True)
     monkeypatch.delenv("GPF_PERSIST")
     monkeypatch.delenv("GPF_SPLIT_K")
+    monkeypatch.delenv("GPF_LA_ALL")
     for a, b, c in zip(on, again, off):
         np.testing.assert_array_equal(a, b)
         np.testing.assert_array_equal(a, c)
