@@ -1047,6 +1047,10 @@ __device__ __forceinline__ void lall_syrk_item(int J, int p, int nt, int Npad, d
   if (threadIdx.x == 0) __hip_atomic_store(yflag + p, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The finished L and U tiles' stores in step_item (r6: non-temporal stores measured 1362-1365 vs
+// 1372-1376 evals/s on C, same box; profiles/r6/ab_store_nt_groups.txt)
+__device__ __forceinline__ void tile_st(double* p, double v) { *p = v; }
+
 // Tile w of block column J of particle p (the unit of work of k_step); role from step_decode.
 //   L tile (I = J+1+w):  D = A_IJ^T - L_J,<J L_I,<J^T  (the transposed panel C^T, so that each
 //                        wave holds all 128 k of the triangular multiply for its 16 rows of C)
@@ -1152,7 +1156,7 @@ if (w < nL)
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          lrow[16 * (2 * P + j) + 4 * e] = o[j][e];
+          tile_st(&lrow[16 * (2 * P + j) + 4 * e], o[j][e]);
           yr = fma(o[j][e], zj[16 * (2 * P + j) + 4 * e + g], yr);
         }
     }
@@ -1221,7 +1225,7 @@ if (w < nL)
         for (int e = 0; e < 4; ++e) {
           const int row = 16 * (2 * P + j) + 4 * e;  // + g
           const double v = o[j][e];
-          ucol[(size_t)row * ld] = v;
+          tile_st(&ucol[(size_t)row * ld], v);
           a2[h] = fma(v, v, a2[h]);
           az[h] = fma(v, zj[row + g], az[h]);
         }
