@@ -1023,7 +1023,9 @@ __device__ __forceinline__ void lall_piece(int J, int it, int s, int p, int nt, 
     const double* Ar = Lp + (size_t)(J + 2) * T * ld + (size_t)b0 * T;
     if (s == 0) acc.load(qd, Lp + (size_t)(J + 2) * T * ld + (size_t)(J + 2) * T, ld);
     else acc.zero();
-    gemm_stream_dl<false, true, TRI_C_LOWER>(acc, Ar, Npad, Ar, Npad, nb * T, lds, qd);
+    // (dense: the lower-only pattern with the whole accumulator live spilled k_step<0,1> — 802 VGPRs,
+    // 312 B/lane; the upper blocks only ever hold A's mirror, never read)
+    gemm_stream_dl<false, true>(acc, Ar, Npad, Ar, Npad, nb * T, lds, qd);
   }
   store_node(acc, lb + lall_slot(J, it, s, p, P_of(tag), nt, smax_of(tag), pb), qd);
 }
@@ -1040,8 +1042,8 @@ __device__ __forceinline__ void lall_syrk_item(int J, int p, int nt, int Npad, d
   Acc<T> acc;
   lall_seed(acc, lb, J, nt - 2, p, tag, nt);
   const double* Ar = Lp + (size_t)I * T * ld + (size_t)(J - 1) * T;
-  gemm_stream_dl<false, true, TRI_C_LOWER>(acc, Ar, Npad, Ar, Npad, T, lds, qd);
-  acc.store_wt(qd, Lp + (size_t)I * T * ld + (size_t)I * T, ld);  // (the upper half rewrites A's own values)
+  gemm_stream_dl<false, true>(acc, Ar, Npad, Ar, Npad, T, lds, qd);  // (dense, as lall_piece's)
+  acc.store_wt(qd, Lp + (size_t)I * T * ld + (size_t)I * T, ld);  // (the upper half: A's mirror, never read)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(yflag + p, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
