@@ -229,6 +229,9 @@ __device__ __forceinline__ void dl_load_s(const void* base, uint32_t off, double
 // they stop evicting the launch's shared A panels (row panel J) from the XCD's L2: r6, same box,
 // config C 1360 -> 1387 evals/s, the clock 2136 -> 2177 MHz, FETCH 2.25 -> 2.01 GB per group launch
 // (profiles/r6/ab_b_nt.txt). -DGPF_B_NT=0 builds the default policy everywhere (A/B).
+#ifndef GPF_SUM_SHFL  // 1: the lane-group sums by ds_bpermute (__shfl_xor), as up to round 6
+#define GPF_SUM_SHFL 0
+#endif
 #ifndef GPF_B_NT
 #define GPF_B_NT 1
 #endif
@@ -684,12 +687,40 @@ struct ClockSpan {  // the two start stamps wait in LDS (kept in registers they 
   }
 };
 
+// v + (v of lane l ^ 16) (ROWS = 16) or l ^ 32 (ROWS = 32) by the gfx950 permlane swaps (VALU, no
+// LDS crossbar round trip as ds_bpermute): swap(v, v) returns {v with the upper rows of each pair
+// replaced by the lower, v with the lower replaced by the upper}, so every lane finds its own value in
+// one result and its partner's in the other; their sum is v + partner (addition commutes: bitwise the
+// same as v + __shfl_xor(v, ROWS)).
+template <int ROWS>
+__device__ __forceinline__ double add_swapped(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+  unsigned a0, a1, b0, b1;
+  if constexpr (ROWS == 16) {
+    const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    a0 = a[0], a1 = a[1], b0 = b[0], b1 = b[1];
+  } else {
+    const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    a0 = a[0], a1 = a[1], b0 = b[0], b1 = b[1];
+  }
+  const double x = __builtin_bit_cast(double, ((unsigned long long)b0 << 32) | a0);
+  const double y = __builtin_bit_cast(double, ((unsigned long long)b1 << 32) | a1);
+  return x + y;
+}
+
 // Sum over the 4 lane groups {l, l^16, l^32, l^48} of a wave; the result is
 // bitwise identical in all four lanes ((g0+g1)+(g2+g3), addition commutes).
 __device__ __forceinline__ double sum_lane_groups(double v) {
+#if GPF_SUM_SHFL
   v = v + __shfl_xor(v, 16);
   v = v + __shfl_xor(v, 32);
   return v;
+#else
+  return add_swapped<32>(add_swapped<16>(v));
+#endif
 }
 
 }  // namespace gpf

@@ -253,14 +253,19 @@ __device__ __forceinline__ void db_fmac_bcast_from(int q, double (&x)[16], doubl
 }
 
 // ---- the panel: wave 0 ----
+#ifndef GPF_PANEL_GST_LATE  // 0: the panel's global stores ahead of the barrier into Q_k (round 5)
+#define GPF_PANEL_GST_LATE 1
+#endif
+#ifndef GPF_DB_PANEL_GST  // probe builds only: 0 drops the panel's global stores (L 1, U 2) to time them
+#define GPF_DB_PANEL_GST 3
+#endif
 // The 16 x 16 diagonal block A_kk, as an [A | I | y] elimination on one wave: lane r < 16 holds row r
 // of A (columns <= r), lane 16 + c column c of X_kk = L_kk^-1 (the identity to start), lane 32 the
 // block's 16 entries of y. Every role takes the same update, x[s] -= m * L(s, q), with its
 // multiplier m (A: L(r, q); X: X(q, c); y: z_q) — one fma per entry and column for the whole wave.
-// Writes L_kk (zeros above the diagonal) to global, X_kk to the LDS diagonal slot and to
-// U, z_k to the LDS y. Returns whether a pivot was not > 0.
-template <bool WT>
-__device__ __forceinline__ bool db_panel(double* lds, int k, double* __restrict__ Lt, double* __restrict__ Ut, size_t ld) {
+// Leaves L_kk (lanes 0..15) and X_kk (lanes 16..31) in x for db_panel_gst, writes X_kk to the LDS
+// diagonal slot and z_k to the LDS y. Returns whether a pivot was not > 0.
+__device__ __forceinline__ bool db_panel_core(double* lds, int k, double (&x)[16]) {
   const int r = threadIdx.x & 63;
   double* blk = lds + db_bid(k, k) * DB_BLK;  // A_kk; then X_kk
   const bool arow = r < 16, xcol = r >= 16 && r < 32, ylane = r == 32;
@@ -273,7 +278,6 @@ __device__ __forceinline__ bool db_panel(double* lds, int k, double* __restrict_
   const int row_off = arow ? db_bid(k, k) * DB_BLK + ro * DB_LD
                            : (xcol ? DB_UNIT + 15 - (ro - 16) : (ylane ? DB_Y + 16 * k : DB_UNIT));
   const double* src = lds + row_off;
-  double x[16];
 #pragma unroll
   for (int c = 0; c < 16; ++c) x[c] = src[c];
   bool bad = false;
@@ -310,20 +314,10 @@ __device__ __forceinline__ bool db_panel(double* lds, int k, double* __restrict_
       db_fmac_bcast_from<2>(q, x, row0_to_rows(m), m);
     }
   }
-  // (the diagonal row's own entries right of its pivot took updates with m = L(q, q): not stored)
-  if (arow) {
-    double* gl = Lt + (size_t)(16 * k + r) * ld + 16 * k;
-#pragma unroll
-    for (int c = 0; c < 16; c += 2) *reinterpret_cast<d2*>(gl + c) = d2{c <= r ? x[c] : 0.0, c + 1 <= r ? x[c + 1] : 0.0};
-  }
   if (xcol) {  // X_kk: lane 16 + c holds column c
     const int c = r - 16;
-    double* gu = Ut + (size_t)(16 * k) * ld + 16 * k + c;
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      blk[db_off(s, c)] = x[s];
-      gst<WT>(gu + (size_t)s * ld, x[s]);
-    }
+    for (int s = 0; s < 16; ++s) blk[db_off(s, c)] = x[s];
   }
   if (ylane) {
 #pragma unroll
@@ -331,7 +325,39 @@ __device__ __forceinline__ bool db_panel(double* lds, int k, double* __restrict_
   }
   return bad;
 }
+// The panel's global stores: L_kk (zeros above the diagonal) and X_kk (U_kk). Issued after the
+// barrier that hands X_kk to Q_k (db_path_panel), so they drain while wave 4 runs Q_k's chain row
+// instead of ahead of the barrier (-4.4% cycles per factor on the f128 probe,
+// profiles/r6/f128_q_chain_late_stores.txt; X_kk stored by its column's owner wave instead, on
+// another SIMD, measured no better and was dropped).
+template <bool WT>
+__device__ __forceinline__ void db_panel_gst(int k, const double (&x)[16], double* __restrict__ Lt, double* __restrict__ Ut,
+                                             size_t ld) {
+  const int r = threadIdx.x & 63;
+  // (the diagonal row's own entries right of its pivot took updates with m = L(q, q): not stored)
+  if (r < 16 && (GPF_DB_PANEL_GST & 1)) {
+    double* gl = Lt + (size_t)(16 * k + r) * ld + 16 * k;
+#pragma unroll
+    for (int c = 0; c < 16; c += 2) *reinterpret_cast<d2*>(gl + c) = d2{c <= r ? x[c] : 0.0, c + 1 <= r ? x[c + 1] : 0.0};
+  }
+  if (r >= 16 && r < 32 && (GPF_DB_PANEL_GST & 2)) {
+    double* gu = Ut + (size_t)(16 * k) * ld + 16 * k + (r - 16);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) gst<WT>(gu + (size_t)s * ld, x[s]);
+  }
+}
+// the panel with its stores in line (the probes)
+template <bool WT>
+__device__ __forceinline__ bool db_panel(double* lds, int k, double* __restrict__ Lt, double* __restrict__ Ut, size_t ld) {
+  double x[16];
+  const bool bad = db_panel_core(lds, k, x);
+  db_panel_gst<WT>(k, x, Lt, Ut, ld);
+  return bad;
+}
 
+#ifndef GPF_Q_CHAIN_FIRST  // 0: Q_k's row k+1 forms the y update before the next diagonal block
+#define GPF_Q_CHAIN_FIRST 1
+#endif
 // Q_k, block row i > k: L(i,k)^T = X_kk A(i,k)^T (the B operand A(i,k)^T is the A-operand read of
 // A(i,k)), y_i -= L(i,k) z_k, L(i,k) to LDS and L; row k+1 then updates the next diagonal block
 // A(k+1,k+1) -= L(k+1,k) L(k+1,k)^T (its A operand: the rows just stored, read back by this wave).
@@ -348,11 +374,25 @@ __device__ __forceinline__ void db_q_item(double* lds, int k, int i, double* __r
   d4 lt = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int s = 0; s < 4; ++s) lt = mfma(xa[s], ab[s], lt);
+#if GPF_Q_CHAIN_FIRST
+  // Row k+1 (the chain into panel k+1): the next diagonal block's MFMAs issue first, so that the
+  // y update's VALU work and lane sums below run while they execute instead of ahead of them.
+  d4 acc = cnext;
+  if (i == k + 1) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = mfma_neg_a(lt[s], lt[s], acc);
+  }
+#endif
   // y_i -= L(i,k) z_k: lane (g, c) holds L(i,k)(c, 4e + g)
   double yp = 0.0;
 #pragma unroll
   for (int e = 0; e < 4; ++e) yp = fma(lt[e], lds[DB_Y + 16 * k + 4 * e + g], yp);
   yp = sum_lane_groups(yp);
+#if GPF_Q_CHAIN_FIRST
+  if (i == k + 1) db_st(B(i, i), acc);
+  if (g == 0) lds[DB_Y + 16 * i + c] = lds[DB_Y + 16 * i + c] - yp;
+  db_st_t(Aik, lt);  // L(i,k) for the trailing updates and the inverse
+#else
   db_st_t(Aik, lt);  // L(i,k) for the trailing updates and the inverse
   if (g == 0) lds[DB_Y + 16 * i + c] = lds[DB_Y + 16 * i + c] - yp;
   if (i == k + 1) {
@@ -363,6 +403,7 @@ __device__ __forceinline__ void db_q_item(double* lds, int k, int i, double* __r
     for (int s = 0; s < 4; ++s) acc = mfma_neg_a(lt[s], lt[s], acc);
     db_st(B(i, i), acc);
   }
+#endif
   double* gl = Lt + (size_t)(16 * i + c) * ld + 16 * k + g;
 #pragma unroll
   for (int e = 0; e < 4; ++e) gl[4 * e] = lt[e];
@@ -471,9 +512,17 @@ __device__ __forceinline__ void db_path_panel(double* lds, double* __restrict__ 
   bool bad = false;
 #pragma unroll 1
   for (int k = 0; k < 8; ++k) {
+#if GPF_PANEL_GST_LATE
+    double x[16];
+    bad = db_panel_core(lds, k, x) | bad;
+    DB_STAMP(0, 2 * k);
+    lsync();
+    db_panel_gst<WT>(k, x, Lt, Ut, ld);
+#else
     bad = db_panel<WT>(lds, k, Lt, Ut, ld) | bad;
     DB_STAMP(0, 2 * k);
     lsync();
+#endif
     if (k < 7) {
       DB_STAMP(0, 2 * k + 1);
       lsync();
