@@ -1249,8 +1249,10 @@ if (w < nL)
 // SPLIT: SPLIT_ALL cuts every tile (launches with few tiles; always with the early diagonal
 // factor, ED = 1); SPLIT_NONE carries no split code at all, so its register allocation is that of
 // the plain schedule.
+// (SPLIT_ALL's flat finish takes ~110 KiB of LDS: one workgroup per CU, 2 waves per SIMD — the
+// occupancy its register allocation is asked for, instead of an unreachable 4)
 template <int SPLIT, int ED>
-__global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_step(int J, int nt, int Npad, double* __restrict__ Lb,
+__global__ __launch_bounds__(STEP_NTH, SPLIT == SPLIT_ALL ? 2 : STEP_WAVES_PER_SIMD) void k_step(int J, int nt, int Npad, double* __restrict__ Lb,
                                                   double* __restrict__ Ub, double* __restrict__ yb,
                                                   double* __restrict__ s2p, double* __restrict__ szp,
                                                   int* __restrict__ info, int P, int grp, int N,
@@ -1401,7 +1403,7 @@ __global__ __launch_bounds__(NTHR) void k_fill_hash(double* __restrict__ p, long
 }
 
 template <int NS>
-__global__ __launch_bounds__(STEP_NTH, STEP_WAVES_PER_SIMD) void k_gemm_bench(int mode, int D, int Npad, int P,
+__global__ __launch_bounds__(STEP_NTH, NS >= 3 ? 2 : STEP_WAVES_PER_SIMD) void k_gemm_bench(int mode, int D, int Npad, int P,
                                                                                    const double* __restrict__ Lb,
                                                                                    double* __restrict__ C,
                                                                                    unsigned long long* clk) {
