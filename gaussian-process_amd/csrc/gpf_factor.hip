@@ -361,7 +361,7 @@ constexpr int STEP_WAVES_PER_SIMD = 4;  // 2 workgroups of 8 waves per CU
 // and hardware placement of every k_step workgroup, per block column J.
 constexpr int WG_TRACE_J = 64, WG_TRACE_N = 4096;
 __device__ unsigned long long g_wg_trace[WG_TRACE_J][WG_TRACE_N][3];
-__device__ unsigned long long g_wg_phase[WG_TRACE_J][WG_TRACE_N][4];  // wave-0 phase ends (see step_item; [3]: split piece's GEMM before its tree)
+__device__ unsigned long long g_wg_phase[WG_TRACE_J][WG_TRACE_N][4];  // wave-0 phase ends (see step_item; [3]: a split piece's GEMM before its tree, a whole tile's U_JJ staged)
 __device__ __forceinline__ unsigned long long realtime() {
   unsigned long long t;
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -1140,6 +1140,7 @@ if (w < nL)
     if (ED && wait_diag(dflag + p, J, info + p, spins, sflag)) return;  // U_JJ, z_J (launch 0 too)
     if (tid < T) zj[tid] = yp[J * T + tid];
     tri_to_lds(Ujj, ld, lds);  // (its barrier also publishes z_J)
+    GPF_PHASE(3);
     // L_IJ^T = U_JJ D by row halves of L_IJ^T (= column halves of L_IJ): lane (g, c) of the wave
     // with slab cb gets L(cb + c, 16 jb + 4 e + g), stores it and adds its share of row cb + c of
     // L_IJ z_J (k ascending per lane, then the 4 lane groups)
@@ -1207,6 +1208,7 @@ if (w < nL)
     if (ED && wait_diag(dflag + p, J, info + p, spins, sflag)) return;  // U_JJ, z_J (U tiles exist for J > 0 only)
     if (tid < T) zj[tid] = yp[J * T + tid];
     tri_to_lds(Ujj, ld, lds);
+    GPF_PHASE(3);
     // U_JK = -U_JJ W by row halves; the column partials of colsum(U^2) and U^T z summed per half
     // (rows ascending per lane, then the 4 lane groups), then upper half + lower half
     double* ucol = launder(Ujk + (size_t)g * ld + qd.cb + cl);

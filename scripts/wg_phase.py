@@ -47,6 +47,7 @@ u64p = ctypes.POINTER(ctypes.c_ulonglong)
 assert probe.gpf_debug_wg_trace(tr.ctypes.data_as(u64p), nt, W) == 0
 assert probe.gpf_debug_wg_phase(ph.ctypes.data_as(u64p), nt, W) == 0
 tot = {}
+fsplit, fsum = {}, {}
 print("J  |  L: n   gemm    fin   syrk   rest |  U: n   gemm    fin   part | SYRK wg | span (us, mean per workgroup)")
 for J in range(nt):
     sy = 1 if 1 <= J <= nt - 2 else 0
@@ -89,6 +90,16 @@ for J in range(nt):
         line += " " * 8
     line += f" | {(en.max() - st.min()) * 1e-2:7.1f}"
     print(line)
+    for nm, m in (("L", isL), ("U", isU)):  # the finish split at U_JJ staged (phase 3)
+        if m.any():
+            stg, mul = (p[m, 3] - p[m, 0]) * 1e-2, (p[m, 1] - p[m, 3]) * 1e-2
+            fsum[nm + " fin: stage U_JJ"] = fsum.get(nm + " fin: stage U_JJ", 0.0) + stg.sum()
+            fsum[nm + " fin: multiply+store"] = fsum.get(nm + " fin: multiply+store", 0.0) + mul.sum()
+            fsplit.setdefault(J, []).append(f"{nm} stage {stg.mean():5.1f} mult {mul.mean():5.1f}")
 allt = sum(tot.values())
 print("share of workgroup-slot time: " + ", ".join(f"{k} {v / allt * 100:.1f}%" for k, v in tot.items()))
+print("finish split (us, mean per workgroup: U_JJ staging | triangular multiply + stores):")
+for J, v in fsplit.items():
+    print(f"{J:2d}  " + "  ".join(v))
+print("finish split, share of workgroup-slot time: " + ", ".join(f"{k} {v / allt * 100:.1f}%" for k, v in fsum.items()))
 ctx.close()
