@@ -579,7 +579,63 @@ __device__ __forceinline__ int tri_row_chunk(int ri, int& rr) {  // chunk row ri
   rr = ri - base;
   return m;
 }
-__device__ __forceinline__ void tri_to_lds(const double* __restrict__ U, size_t ld, double* s) {
+struct NoHook {
+  __device__ void operator()() const {}
+};
+#ifndef GPF_TRI_STAGE_SCALAR  // 0: round 5's per-lane chunk-row decode (tri_row_chunk per pair)
+#define GPF_TRI_STAGE_SCALAR 1
+#endif
+// Block b (0..35, chunk-major: chunk m holds blocks rb = m .. 7) -> chunk m, block row rb
+__host__ __device__ __forceinline__ void tri_block(int b, int& m, int& rb) {
+  m = 0;
+  int base = 0;
+#pragma unroll
+  for (int mm = 0; mm < 7; ++mm)
+    if (b >= base + (8 - m)) {
+      base += 8 - m;
+      ++m;
+    }
+  rb = m + (b - base);
+}
+// (Hook: trace builds only — called once the wave's loads have arrived)
+// r6 (GPF_TRI_STAGE_SCALAR): each thread keeps one (row, pair) slot of a 16 x 16 block — lane
+// offsets formed once — and walks the blocks b = group + 4u, group = tid / 128 wave-uniform, so the
+// block decode and its offsets are scalar work. The per-pair chunk-row decode of the round-5 form
+// was ~25 VALU instructions per pair, and VALU issue crawls on a SIMD whose matrix pipe the
+// co-resident workgroup's GEMM keeps busy: the staging's writes and barrier took ~12 us of its
+// ~20 us per finish (profiles/r6/phase_C_finish_split*.txt). Same LDS image.
+template <typename Hook = NoHook>
+__device__ __forceinline__ void tri_to_lds(const double* __restrict__ U, size_t ld, double* s, Hook hook = Hook()) {
+#if GPF_TRI_STAGE_SCALAR
+  {
+    const int tid = threadIdx.x;
+    const int grp = __builtin_amdgcn_readfirstlane(tid >> 7);  // 2 waves per group: uniform
+    const int r = (tid >> 3) & 15, kp = tid & 7;
+    const double* ul = U + (size_t)r * ld + 2 * kp;
+    d2 v[9];
+#pragma unroll
+    for (int u = 0; u < 9; ++u) {
+      int m, rb;
+      tri_block(grp + 4 * u, m, rb);
+      v[u] = *reinterpret_cast<const d2*>(ul + (size_t)(16 * rb) * ld + 16 * m);
+    }
+    if constexpr (!__is_same(Hook, NoHook)) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      hook();
+    }
+    double* sl = s + r * TRI_LD + 2 * kp;
+#pragma unroll
+    for (int u = 0; u < 9; ++u) {
+      int m, rb;
+      tri_block(grp + 4 * u, m, rb);
+      const int off = tri_chunk(m) + 16 * (rb - m) * TRI_LD;  // block (rb, m) in chunk m
+      sl[off] = v[u].x;
+      sl[off + 1] = v[u].y;
+    }
+    __syncthreads();
+    return;
+  }
+#endif
   int tid = threadIdx.x;
   d2 v[9];
 #pragma unroll
@@ -588,6 +644,10 @@ __device__ __forceinline__ void tri_to_lds(const double* __restrict__ U, size_t 
     int rr;
     const int m = tri_row_chunk(ri, rr);  // row 16 m + rr of U
     v[u] = *reinterpret_cast<const d2*>(U + (size_t)(16 * m + rr) * ld + 16 * m + 2 * kp);
+  }
+  if constexpr (!__is_same(Hook, NoHook)) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    hook();
   }
   asm volatile("" : "+v"(tid));  // (the destinations are recomputed: not 9 more registers held across the loads)
 #pragma unroll

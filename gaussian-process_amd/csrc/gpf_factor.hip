@@ -1207,7 +1207,11 @@ if (w < nL)
     GPF_PHASE(0);
     if (ED && wait_diag(dflag + p, J, info + p, spins, sflag)) return;  // U_JJ, z_J (U tiles exist for J > 0 only)
     if (tid < T) zj[tid] = yp[J * T + tid];
+#ifdef GPF_WG_TRACE
+    tri_to_lds(Ujj, ld, lds, [&] { GPF_PHASE(2); });  // (U tiles: slot 2 = the staging's loads arrived)
+#else
     tri_to_lds(Ujj, ld, lds);
+#endif
     GPF_PHASE(3);
     // U_JK = -U_JJ W by row halves; the column partials of colsum(U^2) and U^T z summed per half
     // (rows ascending per lane, then the 4 lane groups), then upper half + lower half

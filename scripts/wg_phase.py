@@ -95,7 +95,10 @@ for J in range(nt):
             stg, mul = (p[m, 3] - p[m, 0]) * 1e-2, (p[m, 1] - p[m, 3]) * 1e-2
             fsum[nm + " fin: stage U_JJ"] = fsum.get(nm + " fin: stage U_JJ", 0.0) + stg.sum()
             fsum[nm + " fin: multiply+store"] = fsum.get(nm + " fin: multiply+store", 0.0) + mul.sum()
-            fsplit.setdefault(J, []).append(f"{nm} stage {stg.mean():5.1f} mult {mul.mean():5.1f}")
+            extra = ""
+            if nm == "U" and (p[m, 2] > 0).all():  # trace builds: slot 2 of a U tile = its staging loads arrived
+                extra = f" (loads {((p[m, 2] - p[m, 0]) * 1e-2).mean():5.1f} + writes/barrier {((p[m, 3] - p[m, 2]) * 1e-2).mean():5.1f})"
+            fsplit.setdefault(J, []).append(f"{nm} stage {stg.mean():5.1f}{extra} mult {mul.mean():5.1f}")
 allt = sum(tot.values())
 print("share of workgroup-slot time: " + ", ".join(f"{k} {v / allt * 100:.1f}%" for k, v in tot.items()))
 print("finish split (us, mean per workgroup: U_JJ staging | triangular multiply + stores):")
