@@ -375,6 +375,9 @@ __device__ __forceinline__ unsigned long long realtime() {
 #define GPF_PHASE(k)
 #endif
 
+#ifndef GPF_COV_KOUTER  // 0: the covariance seed element by element (round 5)
+#define GPF_COV_KOUTER 1
+#endif
 // K(R, C) block of one particle (R != C: no diagonal entries, so no noise term) straight into the
 // accumulator layout (rows from block R, columns from block C), with k_build_cov's op order
 // (bitwise the same values, kernel_func GP_func.py:56-65; the two blocks enter symmetrically —
@@ -382,6 +385,7 @@ __device__ __forceinline__ unsigned long long realtime() {
 // squared norms of the tile's 128 rows and 128 columns are staged in LDS first. Replaces the
 // write of the K tile in the K build and its read back; only the diagonal blocks are still built
 // (k_build_cov, diag_only).
+template <bool KOUTER = (GPF_COV_KOUTER != 0)>
 __device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, const double* __restrict__ x,
                                              const double* __restrict__ lp, int d, int N, int R, int C,
                                              double* smem) {
@@ -402,10 +406,50 @@ __device__ __forceinline__ void cov_tile_acc(Acc<T>& acc, const Quad<T>& qd, con
         a[k * T + t] = v;
         nrm = nrm + v * v;
       }
+    } else {
+      for (int k = 0; k < d; ++k) a[k * T + t] = 0.0;  // (padding: finite, replaced by 0 below)
     }
     (rows ? na : nb)[t] = nrm;
   }
   __syncthreads();
+  // (r6) coordinate k outermost: the dot products accumulate in the accumulators themselves, the
+  // lane's one column value per k is read once, and the runtime-d loop runs d times per tile instead
+  // of per element — the seed's VALU work shrinks (it runs beside the co-resident workgroup's
+  // MFMAs, where VALU issue is slow). Per element the same operations in the same order.
+  if constexpr (KOUTER) {
+    static_assert(Acc<T>::MBC == 1, "one column per lane");
+    const int col = qd.col(0);
+    const double b0 = sb[col];
+#pragma unroll
+    for (int mi = 0; mi < Acc<T>::MBR; ++mi) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc.v[mi][0][r] = sa[qd.row(mi, r)] * b0;
+      __builtin_amdgcn_sched_barrier(0);  // (the row reads in groups of 4: not all 32 in flight)
+    }
+    for (int k = 1; k < d; ++k) {
+      const double bk = sb[k * T + col];
+#pragma unroll
+      for (int mi = 0; mi < Acc<T>::MBR; ++mi) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc.v[mi][0][r] = fma(sa[k * T + qd.row(mi, r)], bk, acc.v[mi][0][r]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    const double nc = nb[col];
+    const bool cin = C * T + col < N;
+#pragma unroll
+    for (int mi = 0; mi < Acc<T>::MBR; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = qd.row(mi, r);
+        double r2 = (na[row] + nc) - 2.0 * acc.v[mi][0][r];
+        r2 = r2 > 0.0 ? r2 : 0.0;  // np.maximum(sq_dist, 0)
+        acc.v[mi][0][r] = (cin && R * T + row < N) ? exp(-0.5 * r2) : 0.0;
+        __builtin_amdgcn_sched_barrier(0);  // (one exp at a time: the 32 interleaved spilled)
+      }
+    __syncthreads();
+    return;
+  }
 #pragma unroll
   for (int mi = 0; mi < Acc<T>::MBR; ++mi)
 #pragma unroll
@@ -708,7 +752,10 @@ __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad
   Acc<T> acc;
   if (LT)
     split_gemm<false, true, true>(acc, Lp + (size_t)J * T * ld, Npad, Lp + (size_t)I * T * ld, Npad, J * T / DL_KC,
-                                  np, sidx, lds, qd, [&](Acc<T>& a) { cov_tile_acc(a, qd, x, lp, d, N, J, I, lds); });
+                                  np, sidx, lds, qd, [&](Acc<T>& a) {
+                                    // (element by element here: the k-outer form gave k_step<SPLIT_ALL> a private segment)
+                                    cov_tile_acc<false>(a, qd, x, lp, d, N, J, I, lds);
+                                  });
   else  // (the triangular first block runs dense: its upper part holds zeros)
     split_gemm<true, false, false>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
                                    Up + (size_t)K * T * ld + (size_t)K * T, Npad, (J - K) * T / DL_KC, np, sidx, lds, qd,
