@@ -375,6 +375,9 @@ __device__ __forceinline__ unsigned long long realtime() {
 #define GPF_PHASE(k)
 #endif
 
+#ifndef GPF_FLAT_KOUTER  // 0: the all-tile split's seed element by element
+#define GPF_FLAT_KOUTER 1
+#endif
 #ifndef GPF_COV_KOUTER  // 0: the covariance seed element by element (round 5)
 #define GPF_COV_KOUTER 1
 #endif
@@ -753,8 +756,8 @@ __device__ __forceinline__ void flat_piece(int J, int w, int p, int nt, int Npad
   if (LT)
     split_gemm<false, true, true>(acc, Lp + (size_t)J * T * ld, Npad, Lp + (size_t)I * T * ld, Npad, J * T / DL_KC,
                                   np, sidx, lds, qd, [&](Acc<T>& a) {
-                                    // (element by element here: the k-outer form gave k_step<SPLIT_ALL> a private segment)
-                                    cov_tile_acc<false>(a, qd, x, lp, d, N, J, I, lds);
+                                    // (k outer here too: prediction factor -1.8% despite a 20 B private segment, ab_cov_seed_kouter.txt)
+                                    cov_tile_acc<GPF_FLAT_KOUTER != 0>(a, qd, x, lp, d, N, J, I, lds);
                                   });
   else  // (the triangular first block runs dense: its upper part holds zeros)
     split_gemm<true, false, false>(acc, Lp + (size_t)J * T * ld + (size_t)K * T, Npad,
